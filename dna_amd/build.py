@@ -1,0 +1,88 @@
+"""Build the native library dna_amd/lib/libdna_amd.so (HIP kernels for gfx950 + host C++).
+
+    python -m dna_amd.build            # incremental
+    python -m dna_amd.build --clean
+
+Device code: hipcc --offload-arch=gfx950 (cross-compiles without a GPU). Host-only sources
+(BPE tokenizer, masking, FASTA) build with g++. The .so is built in-tree so it travels with the
+repo snapshot to the GPU box; it is git-ignored.
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+BUILD = os.path.join(ROOT, "build", "native")
+LIB = os.path.join(HERE, "lib", "libdna_amd.so")
+ARCH = os.environ.get("DNA_AMD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-I", INCLUDE, "-I", CSRC,
+             "-Wno-unused-result"]
+CXX_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-I", INCLUDE, "-I", CSRC, "-Wall",
+             "-Wno-unused-function"]
+
+
+def _headers_mtime():
+    hs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    return max((os.path.getmtime(h) for h in hs), default=0)
+
+
+def _compile(src):
+    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
+        return obj, None
+    if src.endswith(".hip"):
+        cmd = [HIPCC] + HIP_FLAGS + ["-c", src, "-o", obj]
+    else:
+        cmd = ["g++"] + CXX_FLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    return obj, None
+
+
+def build(verbose=False, jobs=None):
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    errors, objs = [], []
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        for obj, err in ex.map(_compile, srcs):
+            objs.append(obj)
+            if err:
+                errors.append(err)
+    if errors:
+        raise RuntimeError("native build failed:\n" + "\n".join(errors))
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-pthread", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"built {LIB}")
+    return LIB
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    args = ap.parse_args()
+    if args.clean:
+        shutil.rmtree(BUILD, ignore_errors=True)
+        if os.path.exists(LIB):
+            os.remove(LIB)
+    build(verbose=True, jobs=args.j)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,743 @@
+// Fused ALiBi + key-pad attention for DNABERT-2 (MosaicBERT), forward and backward, gfx950.
+//
+// Replaces bert_layers.py:160-196 (PyTorch attention with an fp32 [b,H,S,S] bias built at
+// :421-448) and the disabled Triton slot flash_attn_triton.py:1077-1130. Scores never leave the
+// CU: S = Q K^T * scale + bias with bias[h,i,j] = -slope_h*|i-j| + (key j is pad ? -10000 : 0)
+// computed in registers, online softmax in log2 domain, P V on MFMA.
+//
+// bf16 path (head_dim 64): MFMA v_mfma_f32_32x32x16_bf16. A workgroup = 4 waves = 128 queries
+// of one (batch, head); each wave owns 32 queries and sweeps the keys in tiles of 64 staged in
+// LDS (K XOR-swizzled for conflict-free ds_read_b128 row reads; V read transposed with
+// ds_read_b64_tr_b16). The "swapped" products keep the query on the MFMA lane:
+//   S^T[key][q] = K . Q^T       (A = K rows from LDS, B = Q held in registers)
+//   O^T[d][q]  += V^T . P^T     (A = V^T via tr reads, B = P^T straight from the accumulator)
+// so the softmax statistics of a query live in one lane pair (lane, lane^32).
+// Backward: dQ kernel (queries on lanes, like forward) and dK/dV kernel (keys on lanes, sweeping
+// query tiles), both recomputing P from the forward LSE -- no atomics, deterministic.
+//
+// fp32 path: exact-arithmetic reference-grade kernels (one thread per query / key) used for the
+// 1e-3 fp32 parity mode; not a throughput path.
+#include "common.h"
+
+namespace dna {
+namespace attn {
+
+constexpr int D = 64;       // head dim
+constexpr int BQ = 128;     // queries per workgroup (4 waves x 32)
+constexpr int BK = 64;      // keys per LDS tile
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+constexpr float PAD_BIAS = -10000.0f;  // bert_layers.py:424
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+// element offset of (row, col) in a [64][64] bf16 tile with 16-byte chunks XOR-swizzled by row:
+// rows r and r+1 share a 256-byte bank row, so the swizzle key is (r>>1)&7 -> conflict-free
+// ds_read_b128 for 16 lanes reading 16 consecutive rows at one chunk.
+__device__ __forceinline__ int swz(int r, int c) {
+  return r * D + ((((c >> 3) ^ (r >> 1)) & 7) << 3) + (c & 7);
+}
+
+__device__ __forceinline__ bf16x4 tr_read(const bf16* lds_elem_ptr) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(lds_elem_ptr));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+__device__ __forceinline__ bf16x8 cat(bf16x4 a, bf16x4 b) {
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// key index (within a 32-row block) held by accumulator register r of lane half hh
+__device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+// ----------------------------------------------------------------------------- bf16 forward
+struct TileRegs {
+  bf16x8 k[2], v[2];
+};
+
+__global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ qkv,
+                                                        const uint8_t* __restrict__ key_valid,
+                                                        const float* __restrict__ slopes, int S,
+                                                        int H, float scale_log2,
+                                                        bf16* __restrict__ out,
+                                                        float* __restrict__ lse) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Ks = reinterpret_cast<bf16*>(smem);            // [2][64*64] swizzled
+  bf16* Vs = Ks + 2 * BK * D;                           // [2][64*64] plain
+  float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);  // [2][64] pad bias (log2 units)
+
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int ql = lane & 31, hh = lane >> 5;
+  const int ld = 3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * ld;
+  const int q0 = blockIdx.x * BQ + wave * 32;
+  const int qi = q0 + ql;
+  const int qrow = min(qi, S - 1);
+  const float slope2 = slopes[h] * LOG2E;
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    qf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)qrow * ld + h * D + 16 * s + 8 * hh);
+
+  // staging assignment: 512 16-byte chunks per K (and V) tile, 2 per thread
+  auto load_tile = [&](int kt, TileRegs& t, float& bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int c = tid + i * 256, r = c >> 3, ch = c & 7;
+      const bf16* src = base + (size_t)(kt * BK + r) * ld + h * D + ch * 8;
+      t.k[i] = *reinterpret_cast<const bf16x8*>(src + H * D);
+      t.v[i] = *reinterpret_cast<const bf16x8*>(src + 2 * H * D);
+    }
+    bias = 0.f;
+    if (tid < BK && key_valid) bias = key_valid[(size_t)b * S + kt * BK + tid] ? 0.f : PAD_BIAS * LOG2E;
+  };
+  auto store_tile = [&](int buf, const TileRegs& t, float bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int c = tid + i * 256, r = c >> 3, ch = c & 7;
+      *reinterpret_cast<bf16x8*>(Ks + buf * BK * D + swz(r, ch * 8)) = t.k[i];
+      *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + r * D + ch * 8) = t.v[i];
+    }
+    if (tid < BK) kb[buf * BK + tid] = bias;
+  };
+
+  f32x16 oacc[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+
+  const int nt = S / BK;
+  {
+    TileRegs t; float bias;
+    load_tile(0, t, bias);
+    store_tile(0, t, bias);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int buf = kt & 1;
+    TileRegs nx; float nbias = 0.f;
+    if (kt + 1 < nt) load_tile(kt + 1, nx, nbias);
+
+    const bf16* K = Ks + buf * BK * D;
+    const bf16* V = Vs + buf * BK * D;
+    const float* kbias = kb + buf * BK;
+
+    // S^T = K Q^T for the two 32-key halves
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kh][i] = 0.f;
+      const int r = kh * 32 + ql;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 a = *reinterpret_cast<const bf16x8*>(K + swz(r, 16 * s + 8 * hh));
+        sacc[kh] = mfma(a, qf[s], sacc[kh]);
+      }
+    }
+    // scores in log2 units + running max
+    float tmax = -INFINITY;
+    const int kbase = kt * BK;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int kr = kh * 32 + 8 * g + 4 * hh;  // first of 4 consecutive keys
+        const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + kr);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const float rel = fabsf((float)(qi - (kbase + kr + e)));
+          float x = fmaf(sacc[kh][r], scale_log2, fmaf(-slope2, rel, pb[e]));
+          sacc[kh][r] = x;
+          tmax = fmaxf(tmax, x);
+        }
+      }
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mnew);
+    m = mnew;
+    float psum = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = exp2f(sacc[kh][r] - mnew);
+        sacc[kh][r] = p;
+        psum += p;
+      }
+    l = l * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+
+    // O^T += V^T P^T
+    const int g16 = lane >> 4, i16 = lane & 15;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pbf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pbf[j] = (bf16)sacc[kh][8 * s + j];
+        const int krow = kh * 32 + 16 * s + 4 * (g16 >> 1) + (i16 >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+          bf16x8 a = cat(tr_read(V + krow * D + dcol), tr_read(V + (krow + 8) * D + dcol));
+          oacc[dt] = mfma(a, pbf, oacc[dt]);
+        }
+      }
+    }
+    if (kt + 1 < nt) store_tile(buf ^ 1, nx, nbias);
+    __syncthreads();
+  }
+
+  const float ltot = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.f / ltot;
+  if (qi < S) {
+    bf16* orow = out + ((size_t)b * S + qi) * (H * D) + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (bf16)(oacc[dt][4 * g + e] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * g + 4 * hh) = v;
+      }
+    if (hh == 0) lse[((size_t)b * H + h) * S + qi] = (m + __log2f(ltot)) * LN2;
+  }
+}
+
+// ----------------------------------------------------------------------------- delta = rowsum(dO*O)
+template <typename T>
+__global__ void delta_kernel(const T* __restrict__ out, const T* __restrict__ dout, int T_rows,
+                             int H, int S, float* __restrict__ delta) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (row, head)
+  if (idx >= T_rows * H) return;
+  const int row = idx / H, h = idx % H;
+  const T* o = out + (size_t)row * H * D + h * D;
+  const T* g = dout + (size_t)row * H * D + h * D;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int d = 0; d < D; ++d) acc = fmaf(to_f32(o[d]), to_f32(g[d]), acc);
+  const int b = row / S, s = row % S;
+  delta[((size_t)b * H + h) * S + s] = acc;
+}
+
+// ----------------------------------------------------------------------------- bf16 dQ
+// Queries on lanes (as forward). Per 64-key tile: S^T (8 MFMA), dP^T = V dO^T (8), dQ^T += K^T dS^T (8).
+__global__ __launch_bounds__(256) void dq_bf16_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, const uint8_t* __restrict__ key_valid,
+    const float* __restrict__ slopes, int S, int H, float scale_log2, float scale,
+    bf16* __restrict__ dqkv) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Ks = reinterpret_cast<bf16*>(smem);     // [2][64*64] swizzled
+  bf16* Vs = Ks + 2 * BK * D;                    // [2][64*64] swizzled
+  float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);
+
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int ql = lane & 31, hh = lane >> 5;
+  const int ld = 3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * ld;
+  const int qi = blockIdx.x * BQ + wave * 32 + ql;
+  const int qrow = min(qi, S - 1);
+  const float slope2 = slopes[h] * LOG2E;
+  const float lse2 = lse[((size_t)b * H + h) * S + qrow] * LOG2E;
+  const float dl = delta[((size_t)b * H + h) * S + qrow];
+
+  bf16x8 qf[4], df[4];
+  const bf16* dorow = dout + ((size_t)b * S + qrow) * (H * D) + h * D;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)qrow * ld + h * D + 16 * s + 8 * hh);
+    df[s] = *reinterpret_cast<const bf16x8*>(dorow + 16 * s + 8 * hh);
+  }
+
+  auto load_tile = [&](int kt, TileRegs& t, float& bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int c = tid + i * 256, r = c >> 3, ch = c & 7;
+      const bf16* src = base + (size_t)(kt * BK + r) * ld + h * D + ch * 8;
+      t.k[i] = *reinterpret_cast<const bf16x8*>(src + H * D);
+      t.v[i] = *reinterpret_cast<const bf16x8*>(src + 2 * H * D);
+    }
+    bias = 0.f;
+    if (tid < BK && key_valid) bias = key_valid[(size_t)b * S + kt * BK + tid] ? 0.f : PAD_BIAS * LOG2E;
+  };
+  auto store_tile = [&](int buf, const TileRegs& t, float bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int c = tid + i * 256, r = c >> 3, ch = c & 7;
+      *reinterpret_cast<bf16x8*>(Ks + buf * BK * D + swz(r, ch * 8)) = t.k[i];
+      *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + swz(r, ch * 8)) = t.v[i];
+    }
+    if (tid < BK) kb[buf * BK + tid] = bias;
+  };
+
+  f32x16 dq[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
+
+  const int nt = S / BK;
+  {
+    TileRegs t; float bias;
+    load_tile(0, t, bias);
+    store_tile(0, t, bias);
+  }
+  __syncthreads();
+  const int g16 = lane >> 4, i16 = lane & 15;
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int buf = kt & 1;
+    TileRegs nx; float nbias = 0.f;
+    if (kt + 1 < nt) load_tile(kt + 1, nx, nbias);
+    const bf16* K = Ks + buf * BK * D;
+    const bf16* V = Vs + buf * BK * D;
+    const float* kbias = kb + buf * BK;
+    const int kbase = kt * BK;
+
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      f32x16 sa, pa;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { sa[i] = 0.f; pa[i] = 0.f; }
+      const int r = kh * 32 + ql;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 ak = *reinterpret_cast<const bf16x8*>(K + swz(r, 16 * s + 8 * hh));
+        bf16x8 av = *reinterpret_cast<const bf16x8*>(V + swz(r, 16 * s + 8 * hh));
+        sa = mfma(ak, qf[s], sa);
+        pa = mfma(av, df[s], pa);
+      }
+      // dS^T = P^T (dP^T - delta), P^T = exp2(S c + bias - lse2)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int kr = kh * 32 + 8 * g + 4 * hh;
+        const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + kr);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = 4 * g + e;
+          const float rel = fabsf((float)(qi - (kbase + kr + e)));
+          float x = fmaf(sa[rr], scale_log2, fmaf(-slope2, rel, pb[e]));
+          float p = exp2f(x - lse2);
+          sa[rr] = p * (pa[rr] - dl);
+        }
+      }
+      // dQ^T[d][q] += K^T[d][key] dS^T[key][q]   (k-steps over 16 keys)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 db;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) db[j] = (bf16)sa[8 * s + j];
+        const int krow = kh * 32 + 16 * s + 4 * (g16 >> 1) + (i16 >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+          bf16x8 a = cat(tr_read(K + swz(krow, dcol)), tr_read(K + swz(krow + 8, dcol)));
+          dq[dt] = mfma(a, db, dq[dt]);
+        }
+      }
+    }
+    if (kt + 1 < nt) store_tile(buf ^ 1, nx, nbias);
+    __syncthreads();
+  }
+  if (qi < S) {
+    bf16* row = dqkv + ((size_t)b * S + qi) * ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (bf16)(dq[dt][4 * g + e] * scale);
+        *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * hh) = v;
+      }
+  }
+}
+
+// ----------------------------------------------------------------------------- bf16 dK / dV
+// Keys on lanes: a workgroup = 4 waves x 32 keys; sweeps query tiles of 64 (two 32-halves).
+// Per 32-query half: S (4 MFMA), dP = dO V^T (4), dV^T += dO^T P (4), dK^T += Q^T dS (4).
+constexpr int BKW = 128;  // keys per workgroup
+constexpr int BQT = 64;   // queries per LDS tile
+
+__global__ __launch_bounds__(256) void dkdv_bf16_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, const uint8_t* __restrict__ key_valid,
+    const float* __restrict__ slopes, int S, int H, float scale_log2, float scale,
+    bf16* __restrict__ dqkv) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Qs = reinterpret_cast<bf16*>(smem);      // [2][64*64] swizzled
+  bf16* Os = Qs + 2 * BQT * D;                    // [2][64*64] dO, swizzled
+  float* ls = reinterpret_cast<float*>(Os + 2 * BQT * D);  // [2][64] lse (log2)
+  float* ds = ls + 2 * BQT;                                 // [2][64] delta
+
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int kl = lane & 31, hh = lane >> 5;
+  const int ld = 3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * ld;
+  const bf16* obase = dout + (size_t)b * S * (H * D);
+  const int kj = blockIdx.x * BKW + wave * 32 + kl;
+  const int krow = min(kj, S - 1);
+  const float slope2 = slopes[h] * LOG2E;
+  const float kbias = (key_valid && !key_valid[(size_t)b * S + krow]) ? PAD_BIAS * LOG2E : 0.f;
+  const float* lse_bh = lse + ((size_t)b * H + h) * S;
+  const float* dl_bh = delta + ((size_t)b * H + h) * S;
+
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)krow * ld + H * D + h * D + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)krow * ld + 2 * H * D + h * D + 16 * s + 8 * hh);
+  }
+
+  struct QRegs { bf16x8 q[2], o[2]; float l, d; };
+  auto load_tile = [&](int qt, QRegs& t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int c = tid + i * 256, r = c >> 3, ch = c & 7;
+      const size_t row = (size_t)(qt * BQT + r);
+      t.q[i] = *reinterpret_cast<const bf16x8*>(base + row * ld + h * D + ch * 8);
+      t.o[i] = *reinterpret_cast<const bf16x8*>(obase + row * (H * D) + h * D + ch * 8);
+    }
+    if (tid < BQT) { t.l = lse_bh[qt * BQT + tid] * LOG2E; t.d = dl_bh[qt * BQT + tid]; }
+  };
+  auto store_tile = [&](int buf, const QRegs& t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int c = tid + i * 256, r = c >> 3, ch = c & 7;
+      *reinterpret_cast<bf16x8*>(Qs + buf * BQT * D + swz(r, ch * 8)) = t.q[i];
+      *reinterpret_cast<bf16x8*>(Os + buf * BQT * D + swz(r, ch * 8)) = t.o[i];
+    }
+    if (tid < BQT) { ls[buf * BQT + tid] = t.l; ds[buf * BQT + tid] = t.d; }
+  };
+
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = 0.f; }
+
+  const int nt = S / BQT;
+  {
+    QRegs t;
+    load_tile(0, t);
+    store_tile(0, t);
+  }
+  __syncthreads();
+  const int g16 = lane >> 4, i16 = lane & 15;
+
+  for (int qt = 0; qt < nt; ++qt) {
+    const int buf = qt & 1;
+    QRegs nx;
+    if (qt + 1 < nt) load_tile(qt + 1, nx);
+    const bf16* Q = Qs + buf * BQT * D;
+    const bf16* O = Os + buf * BQT * D;
+    const float* L = ls + buf * BQT;
+    const float* DL = ds + buf * BQT;
+    const int qbase = qt * BQT;
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      f32x16 sa, pa;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { sa[i] = 0.f; pa[i] = 0.f; }
+      const int r = qh * 32 + kl;  // A-operand row = query
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 aq = *reinterpret_cast<const bf16x8*>(Q + swz(r, 16 * s + 8 * hh));
+        bf16x8 ao = *reinterpret_cast<const bf16x8*>(O + swz(r, 16 * s + 8 * hh));
+        sa = mfma(aq, kf[s], sa);  // S[q][key]
+        pa = mfma(ao, vf[s], pa);  // dP[q][key]
+      }
+      f32x16 pp;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int qr = qh * 32 + 8 * g + 4 * hh;
+        const f32x4 lq = *reinterpret_cast<const f32x4*>(L + qr);
+        const f32x4 dq4 = *reinterpret_cast<const f32x4*>(DL + qr);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = 4 * g + e;
+          const float rel = fabsf((float)(qbase + qr + e - kj));
+          float x = fmaf(sa[rr], scale_log2, fmaf(-slope2, rel, kbias));
+          float p = exp2f(x - lq[e]);
+          pp[rr] = p;
+          sa[rr] = p * (pa[rr] - dq4[e]);  // dS
+        }
+      }
+      // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb, sb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { pb[j] = (bf16)pp[8 * s + j]; sb[j] = (bf16)sa[8 * s + j]; }
+        const int qrow = qh * 32 + 16 * s + 4 * (g16 >> 1) + (i16 >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+          bf16x8 ao = cat(tr_read(O + swz(qrow, dcol)), tr_read(O + swz(qrow + 8, dcol)));
+          bf16x8 aq = cat(tr_read(Q + swz(qrow, dcol)), tr_read(Q + swz(qrow + 8, dcol)));
+          dv[dt] = mfma(ao, pb, dv[dt]);
+          dk[dt] = mfma(aq, sb, dk[dt]);
+        }
+      }
+    }
+    if (qt + 1 < nt) store_tile(buf ^ 1, nx);
+    __syncthreads();
+  }
+  if (kj < S) {
+    bf16* row = dqkv + ((size_t)b * S + kj) * ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 vk, vv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vk[e] = (bf16)(dk[dt][4 * g + e] * scale);
+          vv[e] = (bf16)dv[dt][4 * g + e];
+        }
+        *reinterpret_cast<bf16x4*>(row + H * D + 32 * dt + 8 * g + 4 * hh) = vk;
+        *reinterpret_cast<bf16x4*>(row + 2 * H * D + 32 * dt + 8 * g + 4 * hh) = vv;
+      }
+  }
+}
+
+// ----------------------------------------------------------------------------- fp32 path
+// One thread per query (forward, dQ) or per key (dK/dV); K/V (or Q/dO) tiles staged in LDS.
+constexpr int F32_TILE = 64;
+
+__device__ __forceinline__ float bias_nat(float slope, int i, int j, const uint8_t* kv, size_t off) {
+  float bb = -slope * fabsf((float)(i - j));
+  if (kv && !kv[off + j]) bb += PAD_BIAS;
+  return bb;
+}
+
+__global__ __launch_bounds__(64) void fwd_f32_kernel(const float* __restrict__ qkv,
+                                                      const uint8_t* __restrict__ kv,
+                                                      const float* __restrict__ slopes, int S,
+                                                      int H, float scale, float* __restrict__ out,
+                                                      float* __restrict__ lse) {
+  __shared__ float Kt[F32_TILE][D + 1], Vt[F32_TILE][D + 1];
+  const int h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
+  const int qi = blockIdx.x * F32_TILE + t;
+  const int ld = 3 * H * D;
+  const float* base = qkv + (size_t)b * S * ld;
+  const float slope = slopes[h];
+  float q[D], o[D];
+  const int qr = min(qi, S - 1);
+  for (int d = 0; d < D; ++d) { q[d] = base[(size_t)qr * ld + h * D + d]; o[d] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < S; k0 += F32_TILE) {
+    __syncthreads();
+    for (int idx = t; idx < F32_TILE * D; idx += 64) {
+      int r = idx / D, d = idx % D, j = min(k0 + r, S - 1);
+      Kt[r][d] = base[(size_t)j * ld + H * D + h * D + d];
+      Vt[r][d] = base[(size_t)j * ld + 2 * H * D + h * D + d];
+    }
+    __syncthreads();
+    const int kn = min(F32_TILE, S - k0);
+    for (int r = 0; r < kn; ++r) {
+      float sdot = 0.f;
+      for (int d = 0; d < D; ++d) sdot = fmaf(q[d], Kt[r][d], sdot);
+      float x = sdot * scale + bias_nat(slope, qi, k0 + r, kv, (size_t)b * S);
+      float mn = fmaxf(m, x);
+      float a = __expf(m - mn), p = __expf(x - mn);
+      l = l * a + p;
+      for (int d = 0; d < D; ++d) o[d] = fmaf(p, Vt[r][d], o[d] * a);
+      m = mn;
+    }
+  }
+  if (qi < S) {
+    float* orow = out + ((size_t)b * S + qi) * (H * D) + h * D;
+    for (int d = 0; d < D; ++d) orow[d] = o[d] / l;
+    lse[((size_t)b * H + h) * S + qi] = m + __logf(l);
+  }
+}
+
+__global__ __launch_bounds__(64) void dq_f32_kernel(const float* __restrict__ qkv,
+                                                     const float* __restrict__ dout,
+                                                     const float* __restrict__ lse,
+                                                     const float* __restrict__ delta,
+                                                     const uint8_t* __restrict__ kv,
+                                                     const float* __restrict__ slopes, int S,
+                                                     int H, float scale, float* __restrict__ dqkv) {
+  __shared__ float Kt[F32_TILE][D + 1], Vt[F32_TILE][D + 1];
+  const int h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
+  const int qi = blockIdx.x * F32_TILE + t;
+  const int ld = 3 * H * D;
+  const float* base = qkv + (size_t)b * S * ld;
+  const float slope = slopes[h];
+  const int qr = min(qi, S - 1);
+  float q[D], g[D], dq[D];
+  for (int d = 0; d < D; ++d) {
+    q[d] = base[(size_t)qr * ld + h * D + d];
+    g[d] = dout[((size_t)b * S + qr) * (H * D) + h * D + d];
+    dq[d] = 0.f;
+  }
+  const float L = lse[((size_t)b * H + h) * S + qr], dl = delta[((size_t)b * H + h) * S + qr];
+  for (int k0 = 0; k0 < S; k0 += F32_TILE) {
+    __syncthreads();
+    for (int idx = t; idx < F32_TILE * D; idx += 64) {
+      int r = idx / D, d = idx % D, j = min(k0 + r, S - 1);
+      Kt[r][d] = base[(size_t)j * ld + H * D + h * D + d];
+      Vt[r][d] = base[(size_t)j * ld + 2 * H * D + h * D + d];
+    }
+    __syncthreads();
+    const int kn = min(F32_TILE, S - k0);
+    for (int r = 0; r < kn; ++r) {
+      float sdot = 0.f, pdot = 0.f;
+      for (int d = 0; d < D; ++d) { sdot = fmaf(q[d], Kt[r][d], sdot); pdot = fmaf(g[d], Vt[r][d], pdot); }
+      float p = __expf(sdot * scale + bias_nat(slope, qi, k0 + r, kv, (size_t)b * S) - L);
+      float dsv = p * (pdot - dl) * scale;
+      for (int d = 0; d < D; ++d) dq[d] = fmaf(dsv, Kt[r][d], dq[d]);
+    }
+  }
+  if (qi < S) {
+    float* row = dqkv + ((size_t)b * S + qi) * ld + h * D;
+    for (int d = 0; d < D; ++d) row[d] = dq[d];
+  }
+}
+
+__global__ __launch_bounds__(64) void dkdv_f32_kernel(const float* __restrict__ qkv,
+                                                       const float* __restrict__ dout,
+                                                       const float* __restrict__ lse,
+                                                       const float* __restrict__ delta,
+                                                       const uint8_t* __restrict__ kv,
+                                                       const float* __restrict__ slopes, int S,
+                                                       int H, float scale,
+                                                       float* __restrict__ dqkv) {
+  __shared__ float Qt[F32_TILE][D + 1], Gt[F32_TILE][D + 1];
+  __shared__ float Lt[F32_TILE], Dt[F32_TILE];
+  const int h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
+  const int kj = blockIdx.x * F32_TILE + t;
+  const int ld = 3 * H * D;
+  const float* base = qkv + (size_t)b * S * ld;
+  const float slope = slopes[h];
+  const int kr = min(kj, S - 1);
+  float k[D], v[D], dk[D], dv[D];
+  for (int d = 0; d < D; ++d) {
+    k[d] = base[(size_t)kr * ld + H * D + h * D + d];
+    v[d] = base[(size_t)kr * ld + 2 * H * D + h * D + d];
+    dk[d] = dv[d] = 0.f;
+  }
+  const float kb = (kv && !kv[(size_t)b * S + kr]) ? PAD_BIAS : 0.f;
+  for (int q0 = 0; q0 < S; q0 += F32_TILE) {
+    __syncthreads();
+    for (int idx = t; idx < F32_TILE * D; idx += 64) {
+      int r = idx / D, d = idx % D, i = min(q0 + r, S - 1);
+      Qt[r][d] = base[(size_t)i * ld + h * D + d];
+      Gt[r][d] = dout[((size_t)b * S + i) * (H * D) + h * D + d];
+    }
+    if (t < F32_TILE) {
+      int i = min(q0 + t, S - 1);
+      Lt[t] = lse[((size_t)b * H + h) * S + i];
+      Dt[t] = delta[((size_t)b * H + h) * S + i];
+    }
+    __syncthreads();
+    const int qn = min(F32_TILE, S - q0);
+    for (int r = 0; r < qn; ++r) {
+      float sdot = 0.f, pdot = 0.f;
+      for (int d = 0; d < D; ++d) { sdot = fmaf(Qt[r][d], k[d], sdot); pdot = fmaf(Gt[r][d], v[d], pdot); }
+      float p = __expf(sdot * scale - slope * fabsf((float)(q0 + r - kj)) + kb - Lt[r]);
+      float dsv = p * (pdot - Dt[r]) * scale;
+      for (int d = 0; d < D; ++d) { dv[d] = fmaf(p, Gt[r][d], dv[d]); dk[d] = fmaf(dsv, Qt[r][d], dk[d]); }
+    }
+  }
+  if (kj < S) {
+    float* row = dqkv + ((size_t)b * S + kj) * ld + h * D;
+    for (int d = 0; d < D; ++d) { row[H * D + d] = dk[d]; row[2 * H * D + d] = dv[d]; }
+  }
+}
+
+constexpr size_t FWD_LDS = 2 * (2 * BK * D * sizeof(bf16)) + 2 * BK * sizeof(float);
+constexpr size_t DKDV_LDS = 2 * (2 * BQT * D * sizeof(bf16)) + 4 * BQT * sizeof(float);
+
+}  // namespace attn
+}  // namespace dna
+
+using namespace dna;
+using namespace dna::attn;
+
+static int check_common(const void* qkv, const float* slopes, int batch, int seqlen, int heads,
+                        int head_dim, int dtype, const char* fn) {
+  DNA_CHECK_ARG(qkv && slopes, "%s: null pointer", fn);
+  DNA_CHECK_ARG(batch > 0 && seqlen > 0 && heads > 0, "%s: bad shape b=%d S=%d H=%d", fn, batch,
+                seqlen, heads);
+  if (head_dim != D) {
+    set_error("%s: head_dim %d unsupported (64 only)", fn, head_dim);
+    return DNA_ERR_UNSUPPORTED;
+  }
+  DNA_CHECK_ARG(dtype == DNA_F32 || dtype == DNA_BF16, "%s: bad dtype %d", fn, dtype);
+  if (dtype == DNA_BF16 && seqlen % BK != 0) {
+    set_error("%s: bf16 path needs seqlen %% 64 == 0 (got %d)", fn, seqlen);
+    return DNA_ERR_UNSUPPORTED;
+  }
+  return DNA_OK;
+}
+
+extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const float* slopes,
+                            int batch, int seqlen, int heads, int head_dim, int dtype,
+                            float softmax_scale, void* out, float* lse, void* stream) {
+  int st = check_common(qkv, slopes, batch, seqlen, heads, head_dim, dtype, "dna_attn_fwd");
+  if (st) return st;
+  DNA_CHECK_ARG(out && lse, "dna_attn_fwd: null output");
+  hipStream_t s = as_stream(stream);
+  if (dtype == DNA_BF16) {
+    dim3 grid((seqlen + BQ - 1) / BQ, heads, batch);
+    hipLaunchKernelGGL(fwd_bf16_kernel, grid, dim3(256), FWD_LDS, s, (const bf16*)qkv, key_valid,
+                       slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+  } else {
+    dim3 grid((seqlen + F32_TILE - 1) / F32_TILE, heads, batch);
+    hipLaunchKernelGGL(fwd_f32_kernel, grid, dim3(64), 0, s, (const float*)qkv, key_valid, slopes,
+                       seqlen, heads, softmax_scale, (float*)out, lse);
+  }
+  DNA_LAUNCH_CHECK("dna_attn_fwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
+                            const uint8_t* key_valid, const float* slopes, int batch, int seqlen,
+                            int heads, int head_dim, int dtype, float softmax_scale, void* dqkv,
+                            float* delta_ws, void* stream) {
+  int st = check_common(qkv, slopes, batch, seqlen, heads, head_dim, dtype, "dna_attn_bwd");
+  if (st) return st;
+  DNA_CHECK_ARG(out && dout && lse && dqkv && delta_ws, "dna_attn_bwd: null pointer");
+  hipStream_t s = as_stream(stream);
+  const int rows = batch * seqlen;
+  const int nd = (rows * heads + 255) / 256;
+  if (dtype == DNA_BF16) {
+    hipLaunchKernelGGL(delta_kernel<bf16>, dim3(nd), dim3(256), 0, s, (const bf16*)out,
+                       (const bf16*)dout, rows, heads, seqlen, delta_ws);
+    hipLaunchKernelGGL(dq_bf16_kernel, dim3((seqlen + BQ - 1) / BQ, heads, batch), dim3(256),
+                       FWD_LDS, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws, key_valid,
+                       slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv);
+    hipLaunchKernelGGL(dkdv_bf16_kernel, dim3((seqlen + BKW - 1) / BKW, heads, batch), dim3(256),
+                       DKDV_LDS, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws, key_valid,
+                       slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv);
+  } else {
+    hipLaunchKernelGGL(delta_kernel<float>, dim3(nd), dim3(256), 0, s, (const float*)out,
+                       (const float*)dout, rows, heads, seqlen, delta_ws);
+    dim3 grid((seqlen + F32_TILE - 1) / F32_TILE, heads, batch);
+    hipLaunchKernelGGL(dq_f32_kernel, grid, dim3(64), 0, s, (const float*)qkv, (const float*)dout,
+                       lse, delta_ws, key_valid, slopes, seqlen, heads, softmax_scale,
+                       (float*)dqkv);
+    hipLaunchKernelGGL(dkdv_f32_kernel, grid, dim3(64), 0, s, (const float*)qkv,
+                       (const float*)dout, lse, delta_ws, key_valid, slopes, seqlen, heads,
+                       softmax_scale, (float*)dqkv);
+  }
+  DNA_LAUNCH_CHECK("dna_attn_bwd");
+  return DNA_OK;
+}

@@ -1,0 +1,101 @@
+// Shared device/host helpers for the dna_amd HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dna_amd.h"
+
+namespace dna {
+
+// ---------------------------------------------------------------------------------------- errors
+// Thread-local last-error string behind dna_last_error() (include/dna_amd.h).
+void set_error(const char* fmt, ...);
+
+#define DNA_CHECK_ARG(cond, ...)                   \
+  do {                                             \
+    if (!(cond)) {                                 \
+      ::dna::set_error(__VA_ARGS__);               \
+      return DNA_ERR_INVALID;                      \
+    }                                              \
+  } while (0)
+
+#define DNA_LAUNCH_CHECK(name)                                                   \
+  do {                                                                           \
+    hipError_t e_ = hipGetLastError();                                           \
+    if (e_ != hipSuccess) {                                                      \
+      ::dna::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));    \
+      return DNA_ERR_HIP;                                                        \
+    }                                                                            \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------- types
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// ---------------------------------------------------------------------------------------- RNG
+// Philox4x32-10 (Salmon et al., SC'11): counter-based, so the backward pass regenerates the
+// forward dropout mask from (seed, offset, element index) instead of storing it.
+struct Philox {
+  __device__ __forceinline__ static uint4 gen(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+      uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+      uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+      c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+      k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+  }
+};
+
+// Keep-mask for 4 consecutive elements starting at element index `idx4 * 4`.
+// An element is kept when its 32-bit uniform is >= p * 2^32.
+__device__ __forceinline__ uint32_t dropout_keep4(uint64_t seed, uint64_t offset, uint64_t idx4,
+                                                  uint32_t thresh) {
+  uint64_t c = idx4 + offset;
+  uint4 r = Philox::gen((uint32_t)c, (uint32_t)(c >> 32), 0x5EEDu, 0u, (uint32_t)seed,
+                        (uint32_t)(seed >> 32));
+  return (r.x >= thresh ? 1u : 0u) | (r.y >= thresh ? 2u : 0u) | (r.z >= thresh ? 4u : 0u) |
+         (r.w >= thresh ? 8u : 0u);
+}
+
+__host__ __device__ __forceinline__ uint32_t dropout_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+// ---------------------------------------------------------------------------------------- math
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace dna

@@ -1,0 +1,142 @@
+// GeGLU (+ dropout) of BertGatedLinearUnitMLP (bert_layers.py:292-296), fwd and bwd.
+//   a = dropout( gelu_erf(g[:, :F]) * g[:, F:] ),  g = gated_layers(x) with F = intermediate_size.
+// HBM-bound elementwise: 8 consecutive outputs per thread (16-B bf16 vectors), grid-stride.
+// Algorithmic bytes per output element: fwd 2*s (read g1, g2) + s (write a); bwd 3*s + 2*s.
+#include "common.h"
+
+namespace dna {
+namespace geglu {
+
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16* p) { v = *reinterpret_cast<const bf16x8*>(p); }
+  __device__ __forceinline__ float operator[](int i) const { return (float)v[i]; }
+  __device__ __forceinline__ static void store(bf16* p, const float (&f)[8]) {
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (bf16)f[i];
+    *reinterpret_cast<bf16x8*>(p) = o;
+  }
+};
+template <> struct Vec8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const f32x4*>(p);
+    b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  __device__ __forceinline__ float operator[](int i) const { return i < 4 ? a[i] : b[i - 4]; }
+  __device__ __forceinline__ static void store(float* p, const float (&f)[8]) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{f[0], f[1], f[2], f[3]};
+    *reinterpret_cast<f32x4*>(p + 4) = f32x4{f[4], f[5], f[6], f[7]};
+  }
+};
+
+__device__ __forceinline__ uint32_t keep8(uint64_t seed, uint64_t off, uint64_t elem, uint32_t th) {
+  // elem is a multiple of 8: two Philox groups of 4
+  return dropout_keep4(seed, off, elem >> 2, th) | (dropout_keep4(seed, off, (elem >> 2) + 1, th) << 4);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void fwd_kernel(const T* __restrict__ g, int rows, int F,
+                                                  float p, uint32_t th, float ks, uint64_t seed,
+                                                  uint64_t off, T* __restrict__ a) {
+  const size_t n8 = (size_t)rows * F / 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = i * 8;
+    const size_t r = e / F, c = e % F;
+    Vec8<T> g1, g2;
+    g1.load(g + r * 2 * F + c);
+    g2.load(g + r * 2 * F + F + c);
+    float o[8];
+    uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = gelu_erf(g1[j]) * g2[j];
+      o[j] = p > 0.f ? (((keep >> j) & 1) ? v * ks : 0.f) : v;
+    }
+    Vec8<T>::store(a + e, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bwd_kernel(const T* __restrict__ da, const T* __restrict__ g,
+                                                  int rows, int F, float p, uint32_t th, float ks,
+                                                  uint64_t seed, uint64_t off, T* __restrict__ dg) {
+  const size_t n8 = (size_t)rows * F / 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = i * 8;
+    const size_t r = e / F, c = e % F;
+    Vec8<T> g1, g2, d;
+    g1.load(g + r * 2 * F + c);
+    g2.load(g + r * 2 * F + F + c);
+    d.load(da + e);
+    uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
+    float o1[8], o2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float dd = d[j];
+      if (p > 0.f) dd = ((keep >> j) & 1) ? dd * ks : 0.f;
+      const float x = g1[j];
+      o1[j] = dd * g2[j] * gelu_erf_grad(x);
+      o2[j] = dd * gelu_erf(x);
+    }
+    Vec8<T>::store(dg + r * 2 * F + c, o1);
+    Vec8<T>::store(dg + r * 2 * F + F + c, o2);
+  }
+}
+
+inline int grid_for(size_t n8) {
+  size_t b = (n8 + 255) / 256;
+  return (int)(b < 4096 ? (b ? b : 1) : 4096);
+}
+
+}  // namespace geglu
+}  // namespace dna
+
+using namespace dna;
+
+extern "C" int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, float p_drop,
+                             uint64_t seed, uint64_t offset, void* a, void* stream) {
+  DNA_CHECK_ARG(g && a, "dna_geglu_fwd: null pointer");
+  DNA_CHECK_ARG(inter % 8 == 0 && rows >= 0, "dna_geglu_fwd: intermediate %% 8 != 0");
+  DNA_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "dna_geglu_fwd: bad p");
+  if (rows == 0) return DNA_OK;
+  const int grid = geglu::grid_for((size_t)rows * inter / 8);
+  hipStream_t s = as_stream(stream);
+  const uint32_t th = dropout_threshold(p_drop);
+  const float ks = 1.f / (1.f - p_drop);
+  if (dtype == DNA_BF16)
+    hipLaunchKernelGGL(geglu::fwd_kernel<bf16>, dim3(grid), dim3(256), 0, s, (const bf16*)g,
+                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a);
+  else if (dtype == DNA_F32)
+    hipLaunchKernelGGL(geglu::fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)g,
+                       rows, inter, p_drop, th, ks, seed, offset, (float*)a);
+  else
+    DNA_CHECK_ARG(false, "dna_geglu_fwd: bad dtype");
+  DNA_LAUNCH_CHECK("dna_geglu_fwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_geglu_bwd(const void* da, const void* g, int dtype, int rows, int inter,
+                             float p_drop, uint64_t seed, uint64_t offset, void* dg, void* stream) {
+  DNA_CHECK_ARG(da && g && dg, "dna_geglu_bwd: null pointer");
+  DNA_CHECK_ARG(inter % 8 == 0 && rows >= 0, "dna_geglu_bwd: intermediate %% 8 != 0");
+  if (rows == 0) return DNA_OK;
+  const int grid = geglu::grid_for((size_t)rows * inter / 8);
+  hipStream_t s = as_stream(stream);
+  const uint32_t th = dropout_threshold(p_drop);
+  const float ks = 1.f / (1.f - p_drop);
+  if (dtype == DNA_BF16)
+    hipLaunchKernelGGL(geglu::bwd_kernel<bf16>, dim3(grid), dim3(256), 0, s, (const bf16*)da,
+                       (const bf16*)g, rows, inter, p_drop, th, ks, seed, offset, (bf16*)dg);
+  else if (dtype == DNA_F32)
+    hipLaunchKernelGGL(geglu::bwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)da,
+                       (const float*)g, rows, inter, p_drop, th, ks, seed, offset, (float*)dg);
+  else
+    DNA_CHECK_ARG(false, "dna_geglu_bwd: bad dtype");
+  DNA_LAUNCH_CHECK("dna_geglu_bwd");
+  return DNA_OK;
+}

@@ -1,0 +1,256 @@
+"""Autograd Functions over the dna_amd C ABI (HIP kernels on the current torch stream).
+
+Each Function is one fused HIP op with a hand-written backward; GEMMs are the only work left to
+the vendor library (hipBLASLt through torch.mm), with fp32 weight-gradient outputs.
+No CPU fallback: every op raises if the native library is missing or a tensor is not on a GPU.
+"""
+import math
+
+import torch
+
+from . import _native as N
+
+_DT = {torch.float32: N.F32, torch.bfloat16: N.BF16}
+
+
+def _dt(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"dna_amd: unsupported dtype {t.dtype} (fp32 / bf16 only)")
+
+
+def _gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("dna_amd ops run on the GPU only (no CPU fallback); "
+                               f"got a tensor on {t.device}")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+class DropoutRNG:
+    """Counter-based dropout stream: every dropout site draws (seed, offset) and advances the
+    offset by the number of Philox4x32 groups it consumes, so backward regenerates the mask."""
+
+    def __init__(self, seed=2222):
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.offset = 0
+
+    def take(self, n_elements):
+        off = self.offset
+        self.offset += (int(n_elements) + 3) // 4 + 1
+        return self.seed, off
+
+
+# ----------------------------------------------------------------------------------- embeddings
+class EmbeddingLN(torch.autograd.Function):
+    """dropout(LN(E[ids] + type_row)) -> (y fp32, y_bf16|None)   (bert_layers.py:62-107)."""
+
+    @staticmethod
+    def forward(ctx, ids, E, tt, gamma, beta, eps, p, seed, off, want_f32, want_bf16):
+        _gpu(ids, E, tt, gamma, beta)
+        ctx.set_materialize_grads(False)
+        T, (V, d) = ids.numel(), E.shape
+        y = torch.empty(T, d, device=E.device, dtype=torch.float32) if want_f32 else None
+        yb = torch.empty(T, d, device=E.device, dtype=torch.bfloat16) if want_bf16 else None
+        mean = torch.empty(T, device=E.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        ids = ids.contiguous()
+        N.call("dna_embed_ln_fwd", ids.data_ptr(), E.data_ptr(), tt[0].data_ptr(),
+               gamma.data_ptr(), beta.data_ptr(), T, d, V, eps, p, seed, off, _p(y), _p(yb),
+               mean.data_ptr(), rstd.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(ids, E, tt, gamma, mean, rstd)
+        ctx.cfg = (eps, p, seed, off)
+        return y, yb
+
+    @staticmethod
+    def backward(ctx, dy, dyb):
+        ids, E, tt, gamma, mean, rstd = ctx.saved_tensors
+        _, p, seed, off = ctx.cfg
+        T, (V, d) = ids.numel(), E.shape
+        dE = torch.zeros_like(E)
+        dtt = torch.zeros_like(tt)
+        dg = torch.empty_like(gamma)
+        db = torch.empty_like(gamma)
+        nws = N.lib().dna_ln_bwd_workspace(T, d)
+        ws = torch.empty(max(nws, 16), device=E.device, dtype=torch.uint8)
+        dy = None if dy is None else dy.contiguous()
+        dyb = None if dyb is None else dyb.contiguous()
+        N.call("dna_embed_ln_bwd", _p(dy), _p(dyb), ids.data_ptr(), E.data_ptr(),
+               tt[0].data_ptr(), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), T, d, V, 0,
+               p, seed, off, dE.data_ptr(), dtt[0].data_ptr(), dg.data_ptr(), db.data_ptr(),
+               ws.data_ptr(), nws, N.stream_ptr())
+        return None, dE, dtt, dg, db, None, None, None, None, None, None
+
+
+# ----------------------------------------------------------------------------------- fused LN
+class FusedLayerNorm(torch.autograd.Function):
+    """LN(dropout(act(x + bias)) + residual) -> (y fp32|None, y_bf16|None).
+
+    BertSelfOutput (bert_layers.py:209-214), GeGLU-MLP tail (:298-300), head transform
+    (:524-528, act=gelu, eps=1e-12)."""
+
+    @staticmethod
+    def forward(ctx, x, bias, residual, gamma, beta, eps, act, p, seed, off, want_f32, want_bf16):
+        _gpu(x, bias, residual, gamma, beta)
+        ctx.set_materialize_grads(False)
+        x = x.contiguous()
+        n, d = x.shape
+        y = torch.empty(n, d, device=x.device, dtype=torch.float32) if want_f32 else None
+        yb = torch.empty(n, d, device=x.device, dtype=torch.bfloat16) if want_bf16 else None
+        mean = torch.empty(n, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        residual = None if residual is None else residual.contiguous()
+        N.call("dna_ln_fwd", x.data_ptr(), _dt(x), _p(bias), act, p, seed, off, _p(residual),
+               gamma.data_ptr(), beta.data_ptr(), n, d, eps, _p(y), _p(yb), mean.data_ptr(),
+               rstd.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(x, bias, residual, gamma, mean, rstd)
+        ctx.cfg = (act, p, seed, off)
+        return y, yb
+
+    @staticmethod
+    def backward(ctx, dy, dyb):
+        x, bias, residual, gamma, mean, rstd = ctx.saved_tensors
+        act, p, seed, off = ctx.cfg
+        n, d = x.shape
+        dx = torch.empty_like(x)
+        dres = torch.empty(n, d, device=x.device, dtype=torch.float32) if residual is not None else None
+        dg = torch.empty_like(gamma)
+        db = torch.empty_like(gamma)
+        dbias = torch.empty_like(bias) if bias is not None else None
+        nws = N.lib().dna_ln_bwd_workspace(n, d)
+        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
+        dy = None if dy is None else dy.contiguous()
+        dyb = None if dyb is None else dyb.contiguous()
+        N.call("dna_ln_bwd", _p(dy), _p(dyb), x.data_ptr(), _dt(x), _p(bias), act, p, seed, off,
+               _p(residual), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, d, _p(dres),
+               dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _p(dbias), ws.data_ptr(), nws,
+               N.stream_ptr())
+        return dx, dbias, dres, dg, db, None, None, None, None, None, None, None
+
+
+# ----------------------------------------------------------------------------------- attention
+class AlibiAttention(torch.autograd.Function):
+    """softmax(q k^T * scale - slope_h |i-j| + pad_bias) v on packed qkv [T, 3*H*D]."""
+
+    @staticmethod
+    def forward(ctx, qkv, key_valid, slopes, b, S, H, scale):
+        _gpu(qkv, key_valid, slopes)
+        qkv = qkv.contiguous()
+        T = qkv.shape[0]
+        D = qkv.shape[1] // (3 * H)
+        out = torch.empty(T, H * D, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(b, H, S, device=qkv.device, dtype=torch.float32)
+        N.call("dna_attn_fwd", qkv.data_ptr(), _p(key_valid), slopes.data_ptr(), b, S, H, D,
+               _dt(qkv), scale, out.data_ptr(), lse.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(qkv, out, lse, key_valid, slopes)
+        ctx.cfg = (b, S, H, D, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse, key_valid, slopes = ctx.saved_tensors
+        b, S, H, D, scale = ctx.cfg
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(b * H * S, device=qkv.device, dtype=torch.float32)
+        dout = dout.contiguous()
+        N.call("dna_attn_bwd", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+               _p(key_valid), slopes.data_ptr(), b, S, H, D, _dt(qkv), scale, dqkv.data_ptr(),
+               delta.data_ptr(), N.stream_ptr())
+        return dqkv, None, None, None, None, None, None
+
+
+def alibi_attention(qkv, key_valid, slopes, b, S, H, scale=None):
+    D = qkv.shape[1] // (3 * H)
+    return AlibiAttention.apply(qkv, key_valid, slopes, b, S, H,
+                                scale if scale is not None else 1.0 / math.sqrt(D))
+
+
+# ----------------------------------------------------------------------------------- GeGLU
+class GeGLU(torch.autograd.Function):
+    """dropout(gelu(g[:, :F]) * g[:, F:])   (bert_layers.py:292-296)."""
+
+    @staticmethod
+    def forward(ctx, g, p, seed, off):
+        _gpu(g)
+        g = g.contiguous()
+        n, F2 = g.shape
+        a = torch.empty(n, F2 // 2, device=g.device, dtype=g.dtype)
+        N.call("dna_geglu_fwd", g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off, a.data_ptr(),
+               N.stream_ptr())
+        ctx.save_for_backward(g)
+        ctx.cfg = (p, seed, off)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        (g,) = ctx.saved_tensors
+        p, seed, off = ctx.cfg
+        n, F2 = g.shape
+        dg = torch.empty_like(g)
+        da = da.contiguous()
+        N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off,
+               dg.data_ptr(), N.stream_ptr())
+        return dg, None, None, None
+
+
+# ----------------------------------------------------------------------------------- loss
+class MaskedCrossEntropy(torch.autograd.Function):
+    """sum_r CE(logits[r], target[r]) / denom  (fp32 math on bf16 or fp32 logits)."""
+
+    @staticmethod
+    def forward(ctx, logits, target, denom):
+        _gpu(logits, target)
+        logits = logits.contiguous()
+        M, V = logits.shape
+        loss = torch.empty(M, device=logits.device, dtype=torch.float32)
+        lse = torch.empty_like(loss)
+        target = target.contiguous()
+        N.call("dna_xent_fwd", logits.data_ptr(), _dt(logits), target.data_ptr(), M, V,
+               loss.data_ptr(), lse.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(logits, target, lse)
+        ctx.denom = float(denom)
+        return loss.sum() / ctx.denom
+
+    @staticmethod
+    def backward(ctx, dloss):
+        logits, target, lse = ctx.saved_tensors
+        M, V = logits.shape
+        dl = torch.empty_like(logits)
+        dloss = dloss.detach().to(torch.float32).contiguous().reshape(1)
+        N.call("dna_xent_bwd", logits.data_ptr(), _dt(logits), target.data_ptr(), lse.data_ptr(),
+               dloss.data_ptr(), 1.0 / ctx.denom, M, V, dl.data_ptr(), N.stream_ptr())
+        return dl, None, None
+
+
+# ----------------------------------------------------------------------------------- GEMM
+class Linear(torch.autograd.Function):
+    """y = x @ w_lp^T (+ b): forward and dgrad on the compute dtype copy `w_lp` of the fp32
+    master weight `w`; wgrad produced directly in fp32 (hipBLASLt, out_dtype=float32)."""
+
+    @staticmethod
+    def forward(ctx, x, w, w_lp, b):
+        ctx.save_for_backward(x, w_lp)
+        ctx.has_b = b is not None
+        if b is not None:
+            return torch.addmm(b.to(x.dtype), x, w_lp.t())
+        return torch.mm(x, w_lp.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_lp = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.mm(dy, w_lp) if ctx.needs_input_grad[0] else None
+        if x.dtype == torch.float32:
+            dw = torch.mm(dy.t(), x)
+        else:
+            dw = torch.mm(dy.t(), x, out_dtype=torch.float32)
+        db = dy.sum(0, dtype=torch.float32) if ctx.has_b else None
+        return dx, dw, None, db
+
+
+def linear(x, w, w_lp, b=None):
+    return Linear.apply(x, w, w_lp if w_lp is not None else w, b)

@@ -1,0 +1,193 @@
+/*
+ * dna_amd.h -- C ABI of the MI355X-native DNABERT-2 masked-LM pretraining hot path.
+ *
+ * Every entry point takes plain pointers + sizes (device pointers for the kernels, host
+ * pointers for the data path) and an opaque `stream` (a hipStream_t, NULL = default stream).
+ * Kernels enqueue asynchronously and never allocate; scratch comes in through `workspace`.
+ * Return value: DNA_OK (0) or a DNA_ERR_* code; dna_last_error() gives a thread-local message.
+ * Layouts are row-major. "T" below is batch*seqlen (padded layout: pads stay in place and are
+ * excluded from attention by `key_valid`, exactly as the reference's -10000 pad bias does).
+ *
+ * Each function names the reference interface it replaces (paths under /root/reference).
+ * The Python host side (dna_amd/) binds these through ctypes; INTEGRATION.md shows the
+ * binding a maintainer of the reference would add.
+ */
+#ifndef DNA_AMD_H
+#define DNA_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DNA_AMD_ABI_VERSION 1
+
+enum dna_status {
+  DNA_OK = 0,
+  DNA_ERR_INVALID = 1,     /* bad shape / dtype / null pointer */
+  DNA_ERR_HIP = 2,         /* HIP launch or runtime failure */
+  DNA_ERR_UNSUPPORTED = 3, /* valid request this build does not implement (e.g. head_dim) */
+  DNA_ERR_IO = 4,          /* file missing / unreadable / malformed */
+  DNA_ERR_NOMEM = 5        /* host allocation failed or caller buffer too small */
+};
+
+enum dna_dtype { DNA_F32 = 0, DNA_BF16 = 1 };
+enum dna_act { DNA_ACT_NONE = 0, DNA_ACT_GELU = 1 };
+
+int dna_abi_version(void);
+const char* dna_last_error(void);
+
+/* ------------------------------------------------------------------ attention (ALiBi + key pad)
+ * Replaces the PyTorch attention path of BertUnpadSelfAttention.forward
+ * (src/models/DNABERT2/bert_layers.py:160-196, active because flash_attn_qkvpacked_func is forced
+ * to None at :31) and the kernel slot flash_attn_qkvpacked_func(qkv, bias)
+ * (src/models/DNABERT2/flash_attn_triton.py:1077-1130) with bias = alibi + (1-mask)*-10000
+ * (bert_layers.py:421-448) computed in-kernel instead of materialised as [b,H,S,S].
+ *
+ *   qkv      [T, 3*heads*head_dim]  (columns: t*H*D + h*D + d, t in {q,k,v}), dtype
+ *   key_valid[T] uint8 (1 = real token, 0 = pad) or NULL (all valid)
+ *   slopes   [heads] fp32 ALiBi slopes (bert_layers.py:378-396), device memory
+ *   out      [T, heads*head_dim] dtype;  lse [batch, heads, seqlen] fp32 (natural-log LSE)
+ * Supported: head_dim 64; bf16 uses MFMA tiles (seqlen % 64 == 0), fp32 any seqlen.
+ */
+int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const float* slopes, int batch,
+                 int seqlen, int heads, int head_dim, int dtype, float softmax_scale, void* out,
+                 float* lse, void* stream);
+
+/* Backward of dna_attn_fwd (replaces autograd through bert_layers.py:167-178 and
+ * _flash_attn_backward, flash_attn_triton.py:941-1074). Writes dqkv [T, 3*H*D] (dtype).
+ * delta_ws: fp32 workspace of batch*heads*seqlen floats (rowsum(dO*O)). */
+int dna_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
+                 const uint8_t* key_valid, const float* slopes, int batch, int seqlen, int heads,
+                 int head_dim, int dtype, float softmax_scale, void* dqkv, float* delta_ws,
+                 void* stream);
+
+/* ------------------------------------------------------------------ fused (bias, act, dropout, residual) + LayerNorm
+ * y = LN( dropout( act(x + bias) ) + residual ) over the last dim.
+ * Replaces BertSelfOutput.forward (bert_layers.py:209-214: act none, residual),
+ * the add+LN tail of BertGatedLinearUnitMLP.forward (:298-300: p_drop 0, residual) and
+ * BertPredictionHeadTransform.forward (:524-528: act gelu, no residual, eps 1e-12).
+ *   x [rows, cols] x_dtype; bias [cols] fp32 or NULL; residual [rows, cols] fp32 or NULL;
+ *   y [rows, cols] fp32 or NULL; y_bf16 [rows, cols] bf16 or NULL; mean/rstd [rows] fp32.
+ * Dropout mask = Philox4x32-10(seed, offset + element index / 4): regenerated in backward. */
+int dna_ln_fwd(const void* x, int x_dtype, const float* bias, int act, float p_drop,
+               uint64_t seed, uint64_t offset, const float* residual, const float* gamma,
+               const float* beta, int rows, int cols, float eps, float* y, void* y_bf16,
+               float* mean, float* rstd, void* stream);
+
+/* Backward of dna_ln_fwd. The output gradient is dy (fp32) + dy_bf16 (bf16), either may be NULL.
+ * Writes: dresidual [rows, cols] fp32 (NULL to skip), dx [rows, cols] x_dtype,
+ * dgamma/dbeta/dbias [cols] fp32 (each NULL to skip; written, not accumulated).
+ * workspace >= dna_ln_bwd_workspace(rows, cols) bytes. */
+size_t dna_ln_bwd_workspace(int rows, int cols);
+int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, int x_dtype,
+               const float* bias, int act, float p_drop, uint64_t seed, uint64_t offset,
+               const float* residual, const float* gamma, const float* mean, const float* rstd,
+               int rows, int cols, float* dresidual, void* dx, float* dgamma, float* dbeta,
+               float* dbias, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------ embeddings
+ * y = dropout( LN( word_emb[ids] + type_row ) )   (BertEmbeddings.forward, bert_layers.py:62-107;
+ * token_type_ids are all zero so type_row = token_type_embeddings.weight[0]).
+ *   ids [rows] int64; word_emb [vocab, cols] fp32; y fp32 / y_bf16 (either may be NULL). */
+int dna_embed_ln_fwd(const int64_t* ids, const float* word_emb, const float* type_row,
+                     const float* gamma, const float* beta, int rows, int cols, int vocab,
+                     float eps, float p_drop, uint64_t seed, uint64_t offset, float* y,
+                     void* y_bf16, float* mean, float* rstd, void* stream);
+
+/* Backward. dword_emb [vocab, cols] is ACCUMULATED into (+=, fp32 atomics; rows whose id equals
+ * padding_idx are skipped -- nn.Embedding(padding_idx=0), bert_layers.py:45-47). dtype_row,
+ * dgamma, dbeta [cols] are written. workspace >= dna_ln_bwd_workspace(rows, cols). */
+int dna_embed_ln_bwd(const float* dy, const void* dy_bf16, const int64_t* ids,
+                     const float* word_emb, const float* type_row, const float* gamma,
+                     const float* mean, const float* rstd, int rows, int cols, int vocab,
+                     int padding_idx, float p_drop, uint64_t seed, uint64_t offset,
+                     float* dword_emb, float* dtype_row, float* dgamma, float* dbeta,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------ GeGLU (+ dropout)
+ * a = dropout( gelu_erf(g[:, :inter]) * g[:, inter:] )   (bert_layers.py:292-296)
+ *   g [rows, 2*inter] dtype -> a [rows, inter] dtype. */
+int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, float p_drop, uint64_t seed,
+                  uint64_t offset, void* a, void* stream);
+int dna_geglu_bwd(const void* da, const void* g, int dtype, int rows, int inter, float p_drop,
+                  uint64_t seed, uint64_t offset, void* dg, void* stream);
+
+/* ------------------------------------------------------------------ masked-LM cross entropy
+ * Per-row CE over the masked rows only (the model computes logits only for labels>0 rows,
+ * bert_layers.py:795,:820-824; task loss bert_cross_entropy, src/tasks/metrics.py:268-273).
+ *   logits [rows, vocab] dtype; target [rows] int64 -> row_loss, row_lse [rows] fp32. */
+int dna_xent_fwd(const void* logits, int dtype, const int64_t* target, int rows, int vocab,
+                 float* row_loss, float* row_lse, void* stream);
+/* dlogits = (softmax - onehot) * dloss[0] * scale, in logits' dtype. dloss: device scalar. */
+int dna_xent_bwd(const void* logits, int dtype, const int64_t* target, const float* row_lse,
+                 const float* dloss, float scale, int rows, int vocab, void* dlogits,
+                 void* stream);
+
+/* ------------------------------------------------------------------ optimizer (flat buffers)
+ * Lightning gradient_clip_val=1.0 (torch.nn.utils.clip_grad_norm_) + torch AdamW
+ * (train.py:462-542, registry.optimizer["adamw"]) over ONE flat fp32 parameter buffer.
+ * dna_sumsq writes sum(x^2) to out[0] (device). dna_adamw_step reads that sum (if grad_sumsq is
+ * not NULL) and applies clip coef min(1, max_norm/(sqrt(sumsq)+1e-6)) * grad_scale to each grad,
+ * then the decoupled-weight-decay Adam update; optionally refreshes a bf16 copy of the params. */
+size_t dna_sumsq_workspace(size_t n);
+int dna_sumsq(const float* x, size_t n, float* out, void* workspace, size_t workspace_bytes,
+              void* stream);
+int dna_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                   void* param_bf16, size_t n, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int step, const float* grad_sumsq, float max_grad_norm,
+                   float grad_scale, void* stream);
+
+/* ------------------------------------------------------------------ data path (host, C++)
+ * BPE tokenizer: bit-exact with the reference's HF `tokenizers` BPE for
+ * DNABERT-2-117M/tokenizer.json as called at src/dataloaders/datasets/hg38_dataset.py:369-379.
+ * Accepts an HF tokenizer.json or dna_amd/data/dnabert2_bpe.json. Handles are immutable after
+ * creation: thread-safe and fork-safe (DataLoader workers). */
+typedef struct dna_bpe dna_bpe;
+dna_bpe* dna_bpe_create(const char* json_path);
+void dna_bpe_destroy(dna_bpe* h);
+int dna_bpe_vocab_size(const dna_bpe* h);
+/* Raw encode (no special tokens). Returns the token count (may exceed cap: then only cap ids
+ * were written) or a negative DNA_ERR_* code. */
+int dna_bpe_encode(const dna_bpe* h, const char* text, int len, int32_t* out_ids, int cap);
+/* Dataset-style batch encode: ids = ([CLS] + bpe[:P-2] + [SEP] + [PAD]*)[1:-1] (add_eos 0) or
+ * [1:] (add_eos 1). out_ids [n, P-2+add_eos]; out_lens [n] = bpe tokens kept (may be NULL).
+ * nthreads <= 0: one thread per hardware core. */
+int dna_bpe_encode_batch(const dna_bpe* h, const char* const* seqs, const int* lens, int n,
+                         int pad_max_length, int add_eos, int32_t* out_ids, int32_t* out_lens,
+                         int nthreads);
+
+/* bert_mask (hg38_dataset.py:238-286): mask = (seq != pad) & U1 < mask_prob; labels = seq or -100;
+ * U2 < 1-rand-unchanged -> mask_id; next rand_prob -> uniform non-special id; rest unchanged.
+ * _from_draws takes the uniforms / random ids explicitly (exact parity with the reference draws);
+ * dna_bert_mask draws them from Philox4x32-10 keyed by (seed, sample_id). */
+int dna_bert_mask_from_draws(const int64_t* seq, int n, const float* u1, const float* u2,
+                             const int64_t* rand_tok, int mask_id, int pad_id, float mask_prob,
+                             float rand_prob, float unchanged_prob, int64_t* out_seq,
+                             uint8_t* out_mask, int64_t* out_labels);
+int dna_bert_mask(const int64_t* seq, int n, int vocab, const int64_t* special_ids, int n_special,
+                  int mask_id, int pad_id, float mask_prob, float rand_prob, float unchanged_prob,
+                  uint64_t seed, uint64_t sample_id, int64_t* out_seq, uint8_t* out_mask,
+                  int64_t* out_labels);
+
+/* FASTA (+ .fai; created in memory when absent) via mmap -- replaces pyfaidx.Fasta used by
+ * FastaInterval (hg38_dataset.py:40-124). Case is preserved like pyfaidx's default. */
+typedef struct dna_fasta dna_fasta;
+dna_fasta* dna_fasta_open(const char* path);
+void dna_fasta_close(dna_fasta* h);
+int dna_fasta_num_records(const dna_fasta* h);
+const char* dna_fasta_record_name(const dna_fasta* h, int i);
+int64_t dna_fasta_record_length(const dna_fasta* h, const char* name);
+/* FastaInterval.__call__ (hg38_dataset.py:72-124) for BED interval [start, end):
+ * writes the window to out (not NUL-terminated), its length to out_len. rc != 0 reverse-
+ * complements (the caller draws the rc_aug coin). */
+int dna_fasta_interval(const dna_fasta* h, const char* name, int64_t start, int64_t end,
+                       int64_t max_length, int pad_interval, int rc, char* out, int64_t cap,
+                       int64_t* out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DNA_AMD_H */

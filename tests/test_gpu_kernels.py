@@ -1,0 +1,210 @@
+"""Per-kernel parity of the HIP path against plain PyTorch fp32 restatements (oracle/bert_ref.py
+formulas), forward and backward, bf16 and fp32. GPU only."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import bert_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ref_attention(qkv, key_valid, H, b, S):
+    """fp32 PyTorch attention with the reference bias (bert_layers.py:167-178, :421-448)."""
+    T, three_hd = qkv.shape
+    D = three_hd // (3 * H)
+    x = qkv.float().view(b, S, 3, H, D)
+    q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+    bias = bert_ref.attention_bias(key_valid.view(b, S).bool().cpu(), H).to(qkv.device)
+    s = q @ k.transpose(-1, -2) / math.sqrt(D) + bias
+    p = torch.softmax(s, -1)
+    return (p @ v).transpose(1, 2).reshape(T, H * D)
+
+
+def _qkv(b, S, H, dtype, pad_rows=(), seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    qkv = torch.randn(b * S, 3 * H * 64, generator=g).to(DEV)
+    valid = torch.ones(b, S, dtype=torch.uint8)
+    for r, n in pad_rows:
+        valid[r, n:] = 0
+    return qkv.to(dtype), valid.reshape(-1).to(DEV)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize("b,S,H,pads", [(2, 128, 2, [(1, 77)]), (1, 512, 12, []),
+                                        (3, 64, 1, [(0, 5), (2, 63)]), (2, 256, 4, [(0, 200)])])
+def test_attention_forward(dtype, tol, b, S, H, pads):
+    from dna_amd import functional as DF
+    from dna_amd.config import alibi_slopes
+    qkv, kv = _qkv(b, S, H, dtype, pads)
+    slopes = torch.tensor(alibi_slopes(H), device=DEV)
+    out = DF.alibi_attention(qkv, kv, slopes, b, S, H)
+    ref = _ref_attention(qkv.float(), kv, H, b, S)
+    valid = kv.bool()
+    err = (out.float() - ref)[valid].abs().max().item()
+    assert err < tol, err
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 6e-2)])
+@pytest.mark.parametrize("b,S,H,pads", [(2, 128, 2, [(1, 77)]), (1, 512, 12, [(0, 400)]),
+                                        (2, 64, 1, [])])
+def test_attention_backward(dtype, tol, b, S, H, pads):
+    from dna_amd import functional as DF
+    from dna_amd.config import alibi_slopes
+    qkv, kv = _qkv(b, S, H, dtype, pads, seed=1)
+    slopes = torch.tensor(alibi_slopes(H), device=DEV)
+    g = torch.randn(b * S, H * 64, device=DEV) * kv[:, None].float()  # pad rows get no grad
+    q1 = qkv.clone().requires_grad_(True)
+    DF.alibi_attention(q1, kv, slopes, b, S, H).backward(g.to(dtype))
+    q2 = qkv.float().clone().requires_grad_(True)
+    _ref_attention(q2, kv, H, b, S).backward(g)
+    gv = q2.grad.view(b * S, 3, H * 64)
+    hv = q1.grad.float().view(b * S, 3, H * 64)
+    valid = kv.bool()
+    scale = gv[valid].abs().max().item()
+    err = (hv - gv)[valid].abs().max().item()
+    assert err < tol * max(scale, 1.0), (err, scale)
+    # pad rows: gradients must be exactly zero (they never reach the loss)
+    assert hv[~valid].abs().max().item() == 0.0 if (~valid).any() else True
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols", [64, 128, 768])
+@pytest.mark.parametrize("act,use_bias,use_res", [(0, True, True), (1, True, False), (0, False, True)])
+def test_fused_layernorm(dtype, cols, act, use_bias, use_res):
+    from dna_amd import functional as DF
+    torch.manual_seed(0)
+    n = 333
+    x = torch.randn(n, cols, device=DEV).to(dtype)
+    bias = torch.randn(cols, device=DEV) * 0.1 if use_bias else None
+    res = torch.randn(n, cols, device=DEV) if use_res else None
+    gm = 1 + 0.1 * torch.randn(cols, device=DEV)
+    bt = 0.1 * torch.randn(cols, device=DEV)
+    leaves = [t.clone().requires_grad_(True) if t is not None else None for t in (x, bias, res, gm, bt)]
+    y, yb = DF.FusedLayerNorm.apply(*leaves, 1e-12, act, 0.0, 0, 0, True, True)
+    refl = [t.detach().float().clone().requires_grad_(True) if t is not None else None for t in (x, bias, res, gm, bt)]
+    u = refl[0] + (refl[1] if use_bias else 0)
+    if act == 1:
+        u = torch.nn.functional.gelu(u)
+    if use_res:
+        u = u + refl[2]
+    yr = torch.nn.functional.layer_norm(u, (cols,), refl[3], refl[4], 1e-12)
+    assert (y - yr).abs().max().item() < 1e-4
+    assert (yb.float() - yr).abs().max().item() < 3e-2
+    dy = torch.randn(n, cols, device=DEV)
+    dyb = torch.randn(n, cols, device=DEV).to(torch.bfloat16)
+    (y * dy).sum().backward(retain_graph=True)
+    (yb.float() * dyb.float()).sum().backward()
+    (yr * (dy + dyb.float())).sum().backward()
+    tol = 2e-4 if dtype == torch.float32 else 3e-2
+    for a, r in zip(leaves, refl):
+        if a is None:
+            continue
+        sc = max(r.grad.abs().max().item(), 1.0)
+        assert (a.grad.float() - r.grad).abs().max().item() < tol * sc
+
+
+def test_dropout_mask_consistent_fwd_bwd():
+    """GeGLU dropout: backward regenerates the forward mask (Philox), keep rate ~0.9."""
+    from dna_amd import functional as DF
+    torch.manual_seed(0)
+    n, F = 512, 3072
+    g = torch.randn(n, 2 * F, device=DEV).abs().add(0.5).requires_grad_(True)
+    a = DF.GeGLU.apply(g, 0.1, 1234, 77)
+    kept = a != 0
+    rate = kept.float().mean().item()
+    assert abs(rate - 0.9) < 0.005, rate
+    da = torch.randn(n, F, device=DEV)
+    a.backward(da)
+    g2 = g.detach().clone().requires_grad_(True)
+    x1, x2 = g2[:, :F], g2[:, F:]
+    ref = torch.nn.functional.gelu(x1) * x2 * kept.float() / 0.9
+    ref.backward(da)
+    assert (g.grad - g2.grad).abs().max().item() < 1e-4
+    # a different offset gives a different mask
+    a2 = DF.GeGLU.apply(g.detach(), 0.1, 1234, 78 + n * F)
+    assert ((a2 != 0) != kept).float().mean().item() > 0.1
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+def test_geglu(dtype, tol):
+    from dna_amd import functional as DF
+    torch.manual_seed(0)
+    n, F = 100, 512
+    g = torch.randn(n, 2 * F, device=DEV).to(dtype).requires_grad_(True)
+    a = DF.GeGLU.apply(g, 0.0, 0, 0)
+    g2 = g.detach().float().clone().requires_grad_(True)
+    ref = torch.nn.functional.gelu(g2[:, :F]) * g2[:, F:]
+    assert (a.float() - ref).abs().max().item() < tol * 4
+    da = torch.randn(n, F, device=DEV)
+    a.backward(da.to(dtype))
+    ref.backward(da)
+    assert (g.grad.float() - g2.grad).abs().max().item() < tol * 8
+
+
+@pytest.mark.parametrize("cols", [64, 128, 768])
+def test_embedding_ln(cols):
+    from dna_amd import functional as DF
+    torch.manual_seed(0)
+    V, n = 4096, 700
+    ids = torch.randint(0, V, (n,), device=DEV)
+    ids[:50] = 0  # padding_idx rows
+    E = (torch.randn(V, cols, device=DEV) * 0.02).requires_grad_(True)
+    tt = (torch.randn(2, cols, device=DEV) * 0.02).requires_grad_(True)
+    gm = (1 + 0.1 * torch.randn(cols, device=DEV)).requires_grad_(True)
+    bt = (0.1 * torch.randn(cols, device=DEV)).requires_grad_(True)
+    y, yb = DF.EmbeddingLN.apply(ids, E, tt, gm, bt, 1e-12, 0.0, 0, 0, True, True)
+    E2, tt2, gm2, bt2 = (t.detach().clone().requires_grad_(True) for t in (E, tt, gm, bt))
+    yr = torch.nn.functional.layer_norm(
+        torch.nn.functional.embedding(ids, E2, padding_idx=0) + tt2[0], (cols,), gm2, bt2, 1e-12)
+    assert (y - yr).abs().max().item() < 1e-4
+    dy = torch.randn(n, cols, device=DEV)
+    (y * dy).sum().backward()
+    (yr * dy).sum().backward()
+    for a, r in ((E, E2), (tt, tt2), (gm, gm2), (bt, bt2)):
+        assert (a.grad - r.grad).abs().max().item() < 1e-3 * max(1.0, r.grad.abs().max().item())
+    assert E.grad[0].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-4)])
+def test_masked_cross_entropy(dtype, tol):
+    from dna_amd import functional as DF
+    torch.manual_seed(0)
+    M, V = 77, 4096
+    x = torch.randn(M, V, device=DEV).to(dtype).requires_grad_(True)
+    t = torch.randint(0, V, (M,), device=DEV)
+    loss = DF.MaskedCrossEntropy.apply(x, t, 100)
+    x2 = x.detach().float().clone().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(x2, t, reduction="sum") / 100
+    assert abs(loss.item() - ref.item()) < 1e-4
+    (loss * 3).backward()
+    (ref * 3).backward()
+    assert (x.grad.float() - x2.grad).abs().max().item() < (tol if dtype == torch.float32 else 2e-4)
+
+
+def test_fused_adamw_matches_torch():
+    from dna_amd.flat import FlatParams
+    from dna_amd.optim import FusedAdamW
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(37, 19), torch.nn.Linear(19, 5)).to(DEV)
+    ref = [p.detach().clone().requires_grad_(True) for p in m.parameters()]
+    flat = FlatParams(m, DEV)
+    opt = FusedAdamW(flat, lr=5e-3, weight_decay=1e-2, max_grad_norm=1.0)
+    topt = torch.optim.AdamW(ref, lr=5e-3, weight_decay=1e-2)
+    for step in range(5):
+        grads = [torch.randn_like(p) * 2 for p in ref]
+        flat.zero_grad()
+        for p, g in zip(m.parameters(), grads):
+            p.grad.copy_(g)
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        topt.step()
+        opt.step()
+        for p, r in zip(m.parameters(), ref):
+            assert (p.detach() - r.detach()).abs().max().item() < 1e-6
+    assert (flat.shadow.float() - flat.flat).abs().max().item() < 1e-2
