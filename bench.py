@@ -1,0 +1,205 @@
+#!/usr/bin/env python
+"""MLM pretraining throughput of DNABERT-2-117M at seq_len 512 on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+One step = forward (HIP kernels) + fused masked-CE + backward + RCCL gradient all-reduce + global
+clip + AdamW on a per-GPU batch of B synthetic hg38 windows (uniform ACGT, 4096 bp -> exactly 512
+BPE tokens each, BERT 15 % masking), random-init weights of the 117,074,176-parameter
+architecture, bf16 compute, dropout 0.1. Batches are tokenised/masked on the host before timing
+and sit in HBM; K steps are timed between barrier + synchronize, max over ranks.
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP events on the launch
+stream over the timed region) and the CPU baseline (oracle restatement on this host's cores).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MLM sequences/sec, DNABERT-2-117M seq_len=512, at 1/2/4/8 MI355X"
+MODEL_CFG = dict(vocab_size=4096, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                 intermediate_size=3072, hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.0,
+                 layer_norm_eps=1e-12, max_position_embeddings=512, type_vocab_size=2,
+                 pad_token_id=0, alibi_starting_size=512, hidden_act="gelu",
+                 initializer_range=0.02, hyena_framework=True)
+SEQ, WINDOW_BP = 512, 4096
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+TRAIN_FLOP_PER_SEQ = 3.586e11  # 3 x fwd FLOPs at S=512 incl. last-layer subset
+
+
+def make_batches(n_batches, batch, rank, device):
+    from dna_amd.hg38 import bert_mask_fast
+    from dna_amd.synthetic import random_windows
+    from dna_amd.tokenizer import DNABertTokenizer
+    from dna_amd.trainer import DeviceBatch
+    tok = DNABertTokenizer()
+    out = []
+    for i in range(n_batches):
+        wins = random_windows(batch, WINDOW_BP, seed=10_000 * rank + i)
+        ids = torch.from_numpy(tok.encode_windows(wins, SEQ + 2, nthreads=min(16, os.cpu_count() or 1)))
+        assert ids.shape == (batch, SEQ)
+        assert int((ids == tok.pad_token_id).sum()) == 0, "4096-bp windows must fill 512 tokens"
+        ms, mk, lb = [], [], []
+        for j in range(batch):
+            s, m, l = bert_mask_fast(ids[j], tok.mask_token_id, tok.pad_token_id, tok.vocab_size,
+                                     tok.all_special_ids, seed=2222, sample_id=(rank << 40) | (i * batch + j))
+            ms.append(s); mk.append(m); lb.append(l)
+        out.append(DeviceBatch.from_host(torch.stack(ms), torch.stack(mk), torch.stack(lb), ids,
+                                         device))
+    return out
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """Oracle restatement (PyTorch CPU fp32, oracle/bert_ref.py, pinned to the reference) timing
+    the same step (fwd + bert_cross_entropy + bwd + clip + AdamW, dropout 0.1) on a bounded sample."""
+    from oracle import bert_ref
+    threads = min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    cfg = dict(MODEL_CFG)
+    sd = {}
+    for n, shape in bert_ref.state_dict_shapes(cfg):
+        t = torch.randn(shape) * 0.02 if len(shape) > 1 else torch.zeros(shape)
+        if "LayerNorm" in n or "layernorm" in n:
+            t = torch.ones(shape) if n.endswith("weight") else torch.zeros(shape)
+        sd[n] = t.requires_grad_(True)
+    opt = torch.optim.AdamW(list(sd.values()), lr=5e-4, weight_decay=1e-5)
+    drop = lambda t, site: torch.nn.functional.dropout(t, 0.1, True)
+
+    def step(b):
+        rng = np.random.default_rng(b)
+        ids = torch.as_tensor(rng.integers(5, 4096, size=(b, SEQ)))
+        u = torch.as_tensor(rng.random((b, SEQ)))
+        mask = u < 0.15
+        labels = torch.where(mask, ids, torch.full_like(ids, -100))
+        masked = torch.where(mask, torch.full_like(ids, 4), ids)
+        opt.zero_grad()
+        _, _, dense = bert_ref.dnabert2_forward(sd, cfg, masked, labels, dropout=drop)
+        loss = bert_ref.bert_cross_entropy(dense, mask, ids)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(list(sd.values()), 1.0)
+        opt.step()
+
+    step(1)  # warmup
+    b, n_seq, t_used = 2, 0, 0.0
+    while t_used < seconds_budget * 0.5 and n_seq < 64:
+        t0 = time.perf_counter()
+        step(b)
+        t_used += time.perf_counter() - t0
+        n_seq += b
+    return {"value": round(n_seq / t_used, 4), "unit": "sequences/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n_seq} sequences (batches of {b}) of DNABERT-2-117M S=512 fp32 train steps "
+                      f"(fwd+loss+bwd+clip+AdamW) with the oracle restatement on {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DNA_BENCH_BATCH", 128)))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from dna_amd.bert_layers import BertForMaskedLM
+    from dna_amd.functional import OpTimer
+    from dna_amd.trainer import MLMTrainer
+
+    torch.manual_seed(2222)
+    model = BertForMaskedLM(MODEL_CFG, precision="bf16")
+    trainer = MLMTrainer(model, device, lr=5e-4, weight_decay=1e-5, max_grad_norm=1.0)
+    batches = make_batches(4, args.batch, rank, device)
+
+    for i in range(args.warmup):
+        trainer.step(batches[i % len(batches)])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer = OpTimer() if not args.no_kernel_timing else None
+    t0 = time.perf_counter()
+    if timer:
+        timer.__enter__()
+    for i in range(args.steps):
+        loss = trainer.step(batches[i % len(batches)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    if timer:
+        timer.__exit__()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    final_loss = float(loss.item())
+
+    seqs = args.batch * args.steps * world
+    value = seqs / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    roofline, kernels = None, {}
+    if timer:
+        summ = timer.summary()
+        total_ms = {k: n * ms for k, (n, ms, u) in summ.items()}
+        for k, (n, ms, units) in summ.items():
+            tf = units / (ms * 1e-3) / 1e12
+            kernels[k] = {"launches_per_step": n / args.steps, "avg_ms": round(ms, 4),
+                          "share_of_step": round(total_ms[k] / (elapsed * 1e3), 4),
+                          "achieved_tflops": round(tf, 1)}
+        dom = max(total_ms, key=total_ms.get)
+        n, ms, units = summ[dom]
+        ach = units / (ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 1),
+                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "sequences/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic hg38 windows (uniform ACGT 4096 bp -> 512 BPE tokens, 15% BERT "
+                    "masking), random-init weights",
+            "config": {"workload": "DNABERT-2-117M MLM pretrain seq_len=512 bf16 (BASELINE configs[1])",
+                       "model": "DNABERT-2-117M", "global_batch": args.batch * world,
+                       "seq_len": SEQ, "parallelism": f"dp{world}"},
+            "model_tflops_per_gpu": round(value / world * TRAIN_FLOP_PER_SEQ / 1e12, 1),
+            "model_mfu": round(value / world * TRAIN_FLOP_PER_SEQ / 1e12 / PEAK_BF16_TFLOPS, 4),
+            "final_loss": round(final_loss, 4),
+            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

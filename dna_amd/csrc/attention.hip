@@ -238,10 +238,10 @@ __global__ void delta_kernel(const T* __restrict__ out, const T* __restrict__ do
 // ----------------------------------------------------------------------------- bf16 dQ
 // Queries on lanes (as forward). Per 64-key tile: S^T (8 MFMA), dP^T = V dO^T (8), dQ^T += K^T dS^T (8).
 __global__ __launch_bounds__(256) void dq_bf16_kernel(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, const uint8_t* __restrict__ key_valid,
-    const float* __restrict__ slopes, int S, int H, float scale_log2, float scale,
-    bf16* __restrict__ dqkv) {
+    const bf16* __restrict__ qkv, const bf16* __restrict__ out, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta,
+    const uint8_t* __restrict__ key_valid, const float* __restrict__ slopes, int S, int H,
+    float scale_log2, float scale, bf16* __restrict__ dqkv) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Ks = reinterpret_cast<bf16*>(smem);     // [2][64*64] swizzled
   bf16* Vs = Ks + 2 * BK * D;                    // [2][64*64] swizzled
@@ -256,15 +256,20 @@ __global__ __launch_bounds__(256) void dq_bf16_kernel(
   const int qrow = min(qi, S - 1);
   const float slope2 = slopes[h] * LOG2E;
   const float lse2 = lse[((size_t)b * H + h) * S + qrow] * LOG2E;
-  const float dl = delta[((size_t)b * H + h) * S + qrow];
 
   bf16x8 qf[4], df[4];
-  const bf16* dorow = dout + ((size_t)b * S + qrow) * (H * D) + h * D;
+  const size_t orow_off = ((size_t)b * S + qrow) * (H * D) + h * D;
+  float dl = 0.f;  // delta = rowsum(dO * O): this lane holds half the row, lane^32 the other
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     qf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)qrow * ld + h * D + 16 * s + 8 * hh);
-    df[s] = *reinterpret_cast<const bf16x8*>(dorow + 16 * s + 8 * hh);
+    df[s] = *reinterpret_cast<const bf16x8*>(dout + orow_off + 16 * s + 8 * hh);
+    const bf16x8 o8 = *reinterpret_cast<const bf16x8*>(out + orow_off + 16 * s + 8 * hh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl = fmaf((float)df[s][j], (float)o8[j], dl);
   }
+  dl += __shfl_xor(dl, 32, 64);
+  if (hh == 0 && qi < S) delta[((size_t)b * H + h) * S + qi] = dl;
 
   auto load_tile = [&](int kt, TileRegs& t, float& bias) {
 #pragma unroll
@@ -719,11 +724,11 @@ extern "C" int dna_attn_bwd(const void* qkv, const void* out, const void* dout, 
   const int rows = batch * seqlen;
   const int nd = (rows * heads + 255) / 256;
   if (dtype == DNA_BF16) {
-    hipLaunchKernelGGL(delta_kernel<bf16>, dim3(nd), dim3(256), 0, s, (const bf16*)out,
-                       (const bf16*)dout, rows, heads, seqlen, delta_ws);
+    // dQ kernel also produces delta = rowsum(dO*O), consumed by the dK/dV kernel after it
     hipLaunchKernelGGL(dq_bf16_kernel, dim3((seqlen + BQ - 1) / BQ, heads, batch), dim3(256),
-                       FWD_LDS, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws, key_valid,
-                       slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv);
+                       FWD_LDS, s, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
+                       delta_ws, key_valid, slopes, seqlen, heads, softmax_scale * LOG2E,
+                       softmax_scale, (bf16*)dqkv);
     hipLaunchKernelGGL(dkdv_bf16_kernel, dim3((seqlen + BKW - 1) / BKW, heads, batch), dim3(256),
                        DKDV_LDS, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws, key_valid,
                        slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv);

@@ -14,7 +14,7 @@ namespace dna {
 namespace ln {
 
 constexpr int WAVES = 4;  // rows per block in the forward
-constexpr int BWD_BLOCKS = 512;
+constexpr int BWD_BLOCKS = 256;
 
 // column of value k of a lane
 template <bool VEC>
@@ -335,16 +335,24 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(EmbBwdArgs a) {
   block_partials<NV, VEC>(acc_g, acc_b, acc_t, a.cols, a.part);
 }
 
-// sum partials over blocks: out_q[c] = sum_b part[b][q][c]
-__global__ void reduce_partials(const float* __restrict__ part, int nblocks, int cols,
-                                float* o0, float* o1, float* o2) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 3 * cols) return;
+// sum partials over blocks: out_q[c] = sum_b part[b][q][c]. Block = 64 columns x 4 row
+// groups (coalesced 256-B rows), fixed summation order (deterministic).
+__global__ __launch_bounds__(256) void reduce_partials(const float* __restrict__ part, int nblocks,
+                                                       int cols, float* o0, float* o1, float* o2) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + tx;
   float s = 0.f;
-  for (int b = 0; b < nblocks; ++b) s += part[(size_t)b * 3 * cols + i];
-  const int q = i / cols, c = i % cols;
-  float* o = q == 0 ? o0 : (q == 1 ? o1 : o2);
-  if (o) o[c] = s;
+  if (i < 3 * cols)
+    for (int b = ty; b < nblocks; b += 4) s += part[(size_t)b * 3 * cols + i];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && i < 3 * cols) {
+    s = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+    const int q = i / cols, c = i % cols;
+    float* o = q == 0 ? o0 : (q == 1 ? o1 : o2);
+    if (o) o[c] = s;
+  }
 }
 
 template <typename F>
@@ -437,7 +445,7 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
       hipLaunchKernelGGL((bwd_kernel<float, NV, VEC>), dim3(nb), dim3(256), lds, s, a);
   });
   if (st) return st;
-  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 255) / 256), dim3(256), 0, s,
+  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(256), 0, s,
                      (const float*)workspace, nb, cols, dgamma, dbeta, dbias);
   DNA_LAUNCH_CHECK("dna_ln_bwd");
   return DNA_OK;
@@ -492,7 +500,7 @@ extern "C" int dna_embed_ln_bwd(const float* dy, const void* dy_bf16, const int6
   });
   if (st) return st;
   // partial slots: 0 dgamma, 1 dbeta, 2 d(type_row)
-  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 255) / 256), dim3(256), 0, s,
+  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(256), 0, s,
                      (const float*)workspace, nb, cols, dgamma, dbeta, dtype_row);
   DNA_LAUNCH_CHECK("dna_embed_ln_bwd");
   return DNA_OK;

@@ -31,6 +31,48 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+class OpTimer:
+    """Optional HIP-event timing of ops on the stream they launch on (bench.py roofline).
+    Disabled (None) by default: zero overhead on the product path."""
+    active = None
+
+    def __init__(self):
+        self.pending = []  # (name, units, start_event, end_event)
+
+    def __enter__(self):
+        OpTimer.active = self
+        return self
+
+    def __exit__(self, *exc):
+        OpTimer.active = None
+
+    def summary(self):
+        """{name: (launches, mean_ms, units_per_launch)} after a device synchronize."""
+        acc = {}
+        for name, units, a, b in self.pending:
+            n, t, u = acc.get(name, (0, 0.0, 0.0))
+            acc[name] = (n + 1, t + a.elapsed_time(b), u + units)
+        return {k: (n, t / n, u / n) for k, (n, t, u) in acc.items()}
+
+
+class _timed:
+    __slots__ = ("name", "units", "t", "a")
+
+    def __init__(self, name, units):
+        self.name, self.units, self.t = name, units, OpTimer.active
+
+    def __enter__(self):
+        if self.t is not None:
+            self.a = torch.cuda.Event(enable_timing=True)
+            self.a.record()
+
+    def __exit__(self, *exc):
+        if self.t is not None:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            self.t.pending.append((self.name, self.units, self.a, b))
+
+
 class DropoutRNG:
     """Counter-based dropout stream: every dropout site draws (seed, offset) and advances the
     offset by the number of Philox4x32 groups it consumes, so backward regenerates the mask."""
@@ -144,8 +186,9 @@ class AlibiAttention(torch.autograd.Function):
         D = qkv.shape[1] // (3 * H)
         out = torch.empty(T, H * D, device=qkv.device, dtype=qkv.dtype)
         lse = torch.empty(b, H, S, device=qkv.device, dtype=torch.float32)
-        N.call("dna_attn_fwd", qkv.data_ptr(), _p(key_valid), slopes.data_ptr(), b, S, H, D,
-               _dt(qkv), scale, out.data_ptr(), lse.data_ptr(), N.stream_ptr())
+        with _timed("attn_fwd", 4.0 * b * H * S * S * D):
+            N.call("dna_attn_fwd", qkv.data_ptr(), _p(key_valid), slopes.data_ptr(), b, S, H, D,
+                   _dt(qkv), scale, out.data_ptr(), lse.data_ptr(), N.stream_ptr())
         ctx.save_for_backward(qkv, out, lse, key_valid, slopes)
         ctx.cfg = (b, S, H, D, scale)
         return out
@@ -157,9 +200,10 @@ class AlibiAttention(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(b * H * S, device=qkv.device, dtype=torch.float32)
         dout = dout.contiguous()
-        N.call("dna_attn_bwd", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
-               _p(key_valid), slopes.data_ptr(), b, S, H, D, _dt(qkv), scale, dqkv.data_ptr(),
-               delta.data_ptr(), N.stream_ptr())
+        with _timed("attn_bwd", 10.0 * b * H * S * S * D):
+            N.call("dna_attn_bwd", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(),
+                   lse.data_ptr(), _p(key_valid), slopes.data_ptr(), b, S, H, D, _dt(qkv), scale,
+                   dqkv.data_ptr(), delta.data_ptr(), N.stream_ptr())
         return dqkv, None, None, None, None, None, None
 
 
@@ -235,19 +279,26 @@ class Linear(torch.autograd.Function):
     def forward(ctx, x, w, w_lp, b):
         ctx.save_for_backward(x, w_lp)
         ctx.has_b = b is not None
-        if b is not None:
-            return torch.addmm(b.to(x.dtype), x, w_lp.t())
-        return torch.mm(x, w_lp.t())
+        flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
+        with _timed("gemm", flops):
+            if b is not None:
+                return torch.addmm(b.to(x.dtype), x, w_lp.t())
+            return torch.mm(x, w_lp.t())
 
     @staticmethod
     def backward(ctx, dy):
         x, w_lp = ctx.saved_tensors
         dy = dy.contiguous()
-        dx = torch.mm(dy, w_lp) if ctx.needs_input_grad[0] else None
-        if x.dtype == torch.float32:
-            dw = torch.mm(dy.t(), x)
-        else:
-            dw = torch.mm(dy.t(), x, out_dtype=torch.float32)
+        flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            with _timed("gemm", flops):
+                dx = torch.mm(dy, w_lp)
+        with _timed("gemm", flops):
+            if x.dtype == torch.float32:
+                dw = torch.mm(dy.t(), x)
+            else:
+                dw = torch.mm(dy.t(), x, out_dtype=torch.float32)
         db = dy.sum(0, dtype=torch.float32) if ctx.has_b else None
         return dx, dw, None, db
 

@@ -1,0 +1,78 @@
+"""Training step engine for DNABERT-2 MLM pretraining (replaces the Lightning fit loop's
+per-batch work: SequenceLightningModule._shared_step/training_step, train.py:339-440, plus
+Lightning's backward, DDP gradient all-reduce, clip_grad_norm_ and AdamW/scheduler steps).
+
+One step = embedding/encoder/head forward on HIP kernels -> fused masked-CE loss -> backward
+(gradient buckets all-reduced over RCCL as they complete) -> global-norm clip + AdamW on the
+flat buffers -> LR schedule. No host synchronisation inside a step: the batch's row indices
+(MLMIndex) are computed on the host while it is collated.
+"""
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from .bert_layers import BertForMaskedLM, MLMIndex
+from .ddp import GradBucketReducer
+from .flat import FlatParams
+from .optim import FusedAdamW, LinearLRSchedulerWarmup
+
+
+@dataclass
+class DeviceBatch:
+    masked_ids: torch.Tensor  # [b, S] int64 on device
+    mask: torch.Tensor        # [b, S] bool
+    labels: torch.Tensor      # [b, S] int64
+    target: torch.Tensor      # [b, S] int64 (original ids)
+    index: MLMIndex           # on device
+    n_mask: int
+    n_unk_masked: int
+
+    @staticmethod
+    def from_host(masked_ids, mask, labels, target, device, pad_token_id=3):
+        """Collated CPU tensors -> device batch; row bookkeeping done on the host (no GPU sync)."""
+        idx = MLMIndex.build(masked_ids, labels, pad_token_id)
+        n_mask = int(mask.sum())
+        n_unk = n_mask - int(idx.target.numel())
+        pin = lambda t: t.pin_memory() if torch.cuda.is_available() else t
+        dev = lambda t: pin(t).to(device, non_blocking=True)
+        return DeviceBatch(dev(masked_ids), dev(mask), dev(labels), dev(target),
+                           MLMIndex(*(dev(t) for t in (idx.subset_idx, idx.head_idx, idx.target,
+                                                       idx.flat_masked))), n_mask, n_unk)
+
+
+class MLMTrainer:
+    def __init__(self, model: BertForMaskedLM, device, lr=5e-4, weight_decay=1e-5,
+                 betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0, scheduler=None,
+                 bucket_mb=25.0):
+        self.model = model.to(device).train()
+        self.device = device
+        self.flat = FlatParams(self.model, device)
+        self.opt = FusedAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                              max_grad_norm=max_grad_norm)
+        self.sched = None
+        if scheduler is not None:
+            self.sched = LinearLRSchedulerWarmup(self.opt, **scheduler)
+        self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb)
+        self.world = self.reducer.world
+        if self.world > 1:  # DDP construction broadcast (C2 in SURVEY §2.2)
+            dist.broadcast(self.flat.flat, src=0)
+            self.flat.refresh_shadow()
+        # per-rank dropout streams must differ
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        self.model.dropout_rng.seed = (self.model.dropout_rng.seed * 1000003 + rank) & (2 ** 63 - 1)
+        self.global_step = 0
+
+    def step(self, batch: DeviceBatch) -> torch.Tensor:
+        self.opt.zero_grad()
+        self.reducer.prepare()
+        loss, _ = self.model.mlm_loss(batch.masked_ids, batch.mask, batch.index, batch.n_mask,
+                                      batch.n_unk_masked)
+        loss.backward()
+        self.reducer.finish()
+        self.opt.step(grad_scale=self.reducer.grad_scale)
+        if self.sched is not None:
+            self.sched.step()
+        self.global_step += 1
+        return loss.detach()

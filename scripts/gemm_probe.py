@@ -1,0 +1,44 @@
+#!/usr/bin/env python
+"""Time hipBLASLt (torch.mm) on every GEMM shape of the DNABERT-2 training step (GPU)."""
+import sys
+
+import torch
+
+T = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+SHAPES = {"Wqkv": (768, 2304), "Wo": (768, 768), "Wg": (768, 6144), "Wwo": (3072, 768)}
+
+
+def bench(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(True), torch.cuda.Event(True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    dev = "cuda"
+    for name, (K, N) in SHAPES.items():
+        x = torch.randn(T, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+        dy = torch.randn(T, N, device=dev).to(torch.bfloat16)
+        fl = 2.0 * T * K * N
+        res = {
+            "fwd x@W^T": bench(lambda: torch.mm(x, w.t())),
+            "dgrad dy@W": bench(lambda: torch.mm(dy, w)),
+            "wgrad dy^T@x bf16": bench(lambda: torch.mm(dy.t(), x)),
+            "wgrad dy^T@x fp32out": bench(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32)),
+            "wgrad x^T@dy bf16": bench(lambda: torch.mm(x.t(), dy)),
+        }
+        for k, ms in res.items():
+            print(f"{name:5s} T={T} K={K} N={N} {k:22s} {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
