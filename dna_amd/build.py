@@ -25,6 +25,7 @@ ARCH = os.environ.get("DNA_AMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-I", INCLUDE, "-I", CSRC,
+             "-mllvm", "-amdgpu-mfma-vgpr-form",
              "-Wno-unused-result"]
 CXX_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-I", INCLUDE, "-I", CSRC, "-Wall",
              "-Wno-unused-function"]

@@ -56,6 +56,17 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // key index (within a 32-row block) held by accumulator register r of lane half hh
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
 
+// raw v_exp_f32 (2^x): arguments here are <= ~0 (scores minus their running max / LSE), where
+// the denormal-range fixups of exp2f() are not needed.
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// ALiBi distance term of accumulator register r (key offset within a 64-key tile, lane half hh)
+// in log2 units: slope2 * ((r&3) + 8*(r>>2) + 32*kh) + slope2*4*hh  -- one FMA.
+template <int KH, int R>
+__device__ __forceinline__ float alibi_b(float slope2, float h4) {
+  return fmaf(slope2, (float)(KH * 32 + (R & 3) + 8 * (R >> 2)), h4);
+}
+
 // ----------------------------------------------------------------------------- bf16 forward
 struct TileRegs {
   bf16x8 k[2], v[2];
@@ -115,17 +126,20 @@ __global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ 
   float m = -INFINITY, l = 0.f;
 
   const int nt = S / BK;
+  const int kt0 = (blockIdx.x * BQ / BK) % nt;  // diagonal tiles first: the max settles early
   {
     TileRegs t; float bias;
-    load_tile(0, t, bias);
+    load_tile(kt0, t, bias);
     store_tile(0, t, bias);
   }
   __syncthreads();
 
-  for (int kt = 0; kt < nt; ++kt) {
-    const int buf = kt & 1;
+  const float h4 = slope2 * 4.f * hh;
+  for (int it = 0; it < nt; ++it) {
+    const int kt = (kt0 + it) % nt;
+    const int buf = it & 1;
     TileRegs nx; float nbias = 0.f;
-    if (kt + 1 < nt) load_tile(kt + 1, nx, nbias);
+    if (it + 1 < nt) load_tile((kt0 + it + 1) % nt, nx, nbias);
 
     const bf16* K = Ks + buf * BK * D;
     const bf16* V = Vs + buf * BK * D;
@@ -144,42 +158,73 @@ __global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ 
         sacc[kh] = mfma(a, qf[s], sacc[kh]);
       }
     }
-    // scores in log2 units + running max
-    float tmax = -INFINITY;
+    // scores in log2 units: x = s*scale*log2e + bias2. For a tile wholly left (right) of this
+    // wave's 32 queries and without pads, bias2 = +-slope2*(key offset) + u with a per-lane u:
+    // x~ = fma(s, c, +-b_r) and u folds into the running max (2 VALU per score instead of 5).
+    float tmax = -INFINITY, u = 0.f;
     const int kbase = kt * BK;
+    const bool haspad = key_valid && __any(kbias[lane] != 0.f);
+    const bool left = !haspad && kbase + BK - 1 < q0;
+    const bool right = !haspad && kbase > q0 + 31;
+    if (left || right) {
+      u = left ? slope2 * (float)(kbase - qi) : slope2 * (float)(qi - kbase);
+#define DNA_SEP(KH, R, SG)                                                   \
+  {                                                                         \
+    float x = fmaf(sacc[KH][R], scale_log2, SG alibi_b<KH, R>(slope2, h4));  \
+    sacc[KH][R] = x;                                                        \
+    tmax = fmaxf(tmax, x);                                                  \
+  }
+#define DNA_SEP16(KH, SG)                                                                     \
+  DNA_SEP(KH, 0, SG) DNA_SEP(KH, 1, SG) DNA_SEP(KH, 2, SG) DNA_SEP(KH, 3, SG)                 \
+  DNA_SEP(KH, 4, SG) DNA_SEP(KH, 5, SG) DNA_SEP(KH, 6, SG) DNA_SEP(KH, 7, SG)                 \
+  DNA_SEP(KH, 8, SG) DNA_SEP(KH, 9, SG) DNA_SEP(KH, 10, SG) DNA_SEP(KH, 11, SG)               \
+  DNA_SEP(KH, 12, SG) DNA_SEP(KH, 13, SG) DNA_SEP(KH, 14, SG) DNA_SEP(KH, 15, SG)
+      if (left) {
+        DNA_SEP16(0, +)
+        DNA_SEP16(1, +)
+      } else {
+        DNA_SEP16(0, -)
+        DNA_SEP16(1, -)
+      }
+#undef DNA_SEP16
+#undef DNA_SEP
+    } else {
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
+      for (int kh = 0; kh < 2; ++kh) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int kr = kh * 32 + 8 * g + 4 * hh;  // first of 4 consecutive keys
-        const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + kr);
+        for (int g = 0; g < 4; ++g) {
+          const int kr = kh * 32 + 8 * g + 4 * hh;  // first of 4 consecutive keys
+          const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + kr);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * g + e;
-          const float rel = fabsf((float)(qi - (kbase + kr + e)));
-          float x = fmaf(sacc[kh][r], scale_log2, fmaf(-slope2, rel, pb[e]));
-          sacc[kh][r] = x;
-          tmax = fmaxf(tmax, x);
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            const float rel = fabsf((float)(qi - (kbase + kr + e)));
+            float x = fmaf(sacc[kh][r], scale_log2, fmaf(-slope2, rel, pb[e]));
+            sacc[kh][r] = x;
+            tmax = fmaxf(tmax, x);
+          }
         }
       }
     }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) + u;
     const float mnew = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mnew);
+    const float alpha = ex2(m - mnew);
     m = mnew;
+    const float mu = mnew - u;
     float psum = 0.f;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = exp2f(sacc[kh][r] - mnew);
+        float p = ex2(sacc[kh][r] - mu);
         sacc[kh][r] = p;
         psum += p;
       }
     l = l * alpha + psum;
+    if (__any(alpha != 1.f)) {  // wave-uniform: skipped once the running max has settled
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
-
+      for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+    }
     // O^T += V^T P^T
     const int g16 = lane >> 4, i16 = lane & 15;
 #pragma unroll
@@ -198,7 +243,7 @@ __global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ 
         }
       }
     }
-    if (kt + 1 < nt) store_tile(buf ^ 1, nx, nbias);
+    if (it + 1 < nt) store_tile(buf ^ 1, nx, nbias);
     __syncthreads();
   }
 
@@ -305,6 +350,8 @@ __global__ __launch_bounds__(256) void dq_bf16_kernel(
   __syncthreads();
   const int g16 = lane >> 4, i16 = lane & 15;
 
+  const int q0 = blockIdx.x * BQ + wave * 32;
+  const float h4 = slope2 * 4.f * hh;
   for (int kt = 0; kt < nt; ++kt) {
     const int buf = kt & 1;
     TileRegs nx; float nbias = 0.f;
@@ -313,6 +360,11 @@ __global__ __launch_bounds__(256) void dq_bf16_kernel(
     const bf16* V = Vs + buf * BK * D;
     const float* kbias = kb + buf * BK;
     const int kbase = kt * BK;
+    // separable ALiBi (see the forward): tiles wholly left/right of this wave's queries, no pads
+    const bool haspad = key_valid && __any(kbias[lane] != 0.f);
+    const bool left = !haspad && kbase + BK - 1 < q0;
+    const bool right = !haspad && kbase > q0 + 31;
+    const float lu = lse2 - (left ? slope2 * (float)(kbase - qi) : slope2 * (float)(qi - kbase));
 
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
@@ -328,17 +380,26 @@ __global__ __launch_bounds__(256) void dq_bf16_kernel(
         pa = mfma(av, df[s], pa);
       }
       // dS^T = P^T (dP^T - delta), P^T = exp2(S c + bias - lse2)
+      if (left || right) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int kr = kh * 32 + 8 * g + 4 * hh;
-        const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + kr);
+        for (int rr = 0; rr < 16; ++rr) {
+          const float br = fmaf(slope2, (float)(kh * 32 + (rr & 3) + 8 * (rr >> 2)), h4);
+          const float x = fmaf(sa[rr], scale_log2, left ? br : -br);
+          sa[rr] = ex2(x - lu) * (pa[rr] - dl);
+        }
+      } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rr = 4 * g + e;
-          const float rel = fabsf((float)(qi - (kbase + kr + e)));
-          float x = fmaf(sa[rr], scale_log2, fmaf(-slope2, rel, pb[e]));
-          float p = exp2f(x - lse2);
-          sa[rr] = p * (pa[rr] - dl);
+        for (int g = 0; g < 4; ++g) {
+          const int kr = kh * 32 + 8 * g + 4 * hh;
+          const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + kr);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rr = 4 * g + e;
+            const float rel = fabsf((float)(qi - (kbase + kr + e)));
+            float x = fmaf(sa[rr], scale_log2, fmaf(-slope2, rel, pb[e]));
+            float p = ex2(x - lse2);
+            sa[rr] = p * (pa[rr] - dl);
+          }
         }
       }
       // dQ^T[d][q] += K^T[d][key] dS^T[key][q]   (k-steps over 16 keys)
@@ -400,6 +461,7 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
   const int krow = min(kj, S - 1);
   const float slope2 = slopes[h] * LOG2E;
   const float kbias = (key_valid && !key_valid[(size_t)b * S + krow]) ? PAD_BIAS * LOG2E : 0.f;
+  const float h4kv = slope2 * 4.f * hh;
   const float* lse_bh = lse + ((size_t)b * H + h) * S;
   const float* dl_bh = delta + ((size_t)b * H + h) * S;
 
@@ -453,8 +515,12 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
     const float* L = ls + buf * BQT;
     const float* DL = ds + buf * BQT;
     const int qbase = qt * BQT;
+    const int kw0 = blockIdx.x * BKW + wave * 32;
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
+      const int qb = qbase + qh * 32;
+      const bool after = qb > kw0 + 31;   // every query of this half is right of every key
+      const bool before = qb + 31 < kw0;  // every query is left of every key
       f32x16 sa, pa;
 #pragma unroll
       for (int i = 0; i < 16; ++i) { sa[i] = 0.f; pa[i] = 0.f; }
@@ -467,6 +533,9 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
         pa = mfma(ao, vf[s], pa);  // dP[q][key]
       }
       f32x16 pp;
+      // after: bias2 = -slope2*(q - k) = -(slope2*c_r + h4 - u); before: +(slope2*c_r + h4 + u)
+      const float hu = after ? h4kv - slope2 * (float)(kj - qb) - kbias
+                             : h4kv + slope2 * (float)(qb - kj) + kbias;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int qr = qh * 32 + 8 * g + 4 * hh;
@@ -475,9 +544,15 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int rr = 4 * g + e;
-          const float rel = fabsf((float)(qbase + qr + e - kj));
-          float x = fmaf(sa[rr], scale_log2, fmaf(-slope2, rel, kbias));
-          float p = exp2f(x - lq[e]);
+          float x;
+          if (after || before) {
+            const float br = fmaf(slope2, (float)(8 * g + e), hu);
+            x = fmaf(sa[rr], scale_log2, after ? -br : br);
+          } else {
+            const float rel = fabsf((float)(qbase + qr + e - kj));
+            x = fmaf(sa[rr], scale_log2, fmaf(-slope2, rel, kbias));
+          }
+          float p = ex2(x - lq[e]);
           pp[rr] = p;
           sa[rr] = p * (pa[rr] - dq4[e]);  // dS
         }

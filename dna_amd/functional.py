@@ -295,12 +295,35 @@ class Linear(torch.autograd.Function):
             with _timed("gemm", flops):
                 dx = torch.mm(dy, w_lp)
         with _timed("gemm", flops):
-            if x.dtype == torch.float32:
-                dw = torch.mm(dy.t(), x)
-            else:
-                dw = torch.mm(dy.t(), x, out_dtype=torch.float32)
+            dw = wgrad(dy, x)
         db = dy.sum(0, dtype=torch.float32) if ctx.has_b else None
         return dx, dw, None, db
+
+
+def wgrad_splits(rows, m, n, target_tiles=512, max_splits=16):
+    """Split-K factor for dW = dY^T X: the contraction runs over all `rows` tokens while the
+    output has only (m/256)*(n/256) tiles (9..72 for DNABERT-2), far fewer than 256 CUs."""
+    tiles = max(1, (m // 256) * (n // 256))
+    s = 1
+    while s < max_splits and tiles * s < target_tiles:
+        s *= 2
+    while s > 1 and (rows % s or rows // s < 256):
+        s //= 2
+    return s
+
+
+def wgrad(dy, x):
+    """fp32 dW [m, n] = dy[rows, m]^T x[rows, n] (split-K batched GEMM + fp32 sum for bf16)."""
+    if x.dtype == torch.float32:
+        return torch.mm(dy.t(), x)
+    rows, m = dy.shape
+    n = x.shape[1]
+    s = wgrad_splits(rows, m, n)
+    if s == 1:
+        return torch.mm(dy.t(), x, out_dtype=torch.float32)
+    a = dy.view(s, rows // s, m).transpose(1, 2)
+    b = x.view(s, rows // s, n)
+    return torch.bmm(a, b, out_dtype=torch.float32).sum(0)
 
 
 def linear(x, w, w_lp, b=None):

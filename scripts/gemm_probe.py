@@ -40,5 +40,27 @@ def main():
                   flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and (len(sys.argv) < 3 or sys.argv[2] != "splitk"):
     main()
+
+
+def probe_splitk():
+    dev = "cuda"
+    for name, (K, N) in SHAPES.items():
+        x = torch.randn(T, K, device=dev).to(torch.bfloat16)
+        dy = torch.randn(T, N, device=dev).to(torch.bfloat16)
+        fl = 2.0 * T * K * N
+        for s in (4, 8, 16, 32):
+            a = dy.view(s, T // s, N).transpose(1, 2)
+            b = x.view(s, T // s, K)
+            ms = bench(lambda: torch.bmm(a, b).sum(0, dtype=torch.float32))
+            print(f"{name:5s} splitK={s:2d} bmm bf16 + sum      {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s", flush=True)
+            try:
+                ms = bench(lambda: torch.bmm(a, b, out_dtype=torch.float32).sum(0))
+                print(f"{name:5s} splitK={s:2d} bmm fp32out + sum   {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s", flush=True)
+            except Exception as e:  # noqa: BLE001
+                print("bmm out_dtype unsupported:", str(e)[:80])
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "splitk":
+    probe_splitk()

@@ -208,3 +208,35 @@ def test_fused_adamw_matches_torch():
         for p, r in zip(m.parameters(), ref):
             assert (p.detach() - r.detach()).abs().max().item() < 1e-6
     assert (flat.shadow.float() - flat.flat).abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("rows,m,n", [(65536, 768, 768), (8192, 2304, 768), (1000, 768, 3072),
+                                      (4096, 6144, 768)])
+def test_wgrad_splitk(rows, m, n):
+    from dna_amd.functional import wgrad
+    torch.manual_seed(0)
+    dy = torch.randn(rows, m, device=DEV).to(torch.bfloat16)
+    x = torch.randn(rows, n, device=DEV).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    got = wgrad(dy, x)
+    assert got.dtype == torch.float32
+    assert (got - ref).abs().max().item() < 2e-3 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 5e-2)])
+def test_attention_forward_spiked_max(dtype, tol):
+    """Force late running-max jumps: the key tiles are visited diagonal-first, so a key far from
+    the diagonal with a huge score makes the max grow on a late tile (rescale branch taken)."""
+    from dna_amd import functional as DF
+    from dna_amd.config import alibi_slopes
+    b, S, H = 2, 512, 12
+    qkv, kv = _qkv(b, S, H, torch.float32, [], seed=3)
+    x = qkv.view(b, S, 3, H, 64)
+    for (bi, qi, kj) in [(0, 3, 500), (0, 300, 10), (1, 511, 0), (1, 64, 448), (0, 128, 129)]:
+        x[bi, kj, 1, :, :] = 6.0 * x[bi, qi, 0, :, :] / x[bi, qi, 0, :, :].norm(dim=-1, keepdim=True)
+    qkv = qkv.to(dtype)
+    slopes = torch.tensor(alibi_slopes(H), device=DEV)
+    out = DF.alibi_attention(qkv, kv, slopes, b, S, H)
+    ref = _ref_attention(qkv.float(), kv, H, b, S)
+    err = (out.float() - ref).abs().max().item()
+    assert err < tol, err
