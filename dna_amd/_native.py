@@ -35,6 +35,10 @@ _SIGS = {
                               _vp, _vp, _vp]),
     "dna_embed_ln_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _u64,
                               _u64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dna_embed_ln_bwd_rows": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _f, _u64,
+                                   _u64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dna_embed_grad_segsum": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "dna_sum_slices_accum": (_i, [_vp, _i, _sz, _vp, _vp]),
     "dna_geglu_fwd": (_i, [_vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_geglu_bwd": (_i, [_vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_xent_fwd": (_i, [_vp, _i, _vp, _i, _i, _vp, _vp, _vp]),

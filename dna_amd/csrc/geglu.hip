@@ -38,17 +38,18 @@ __device__ __forceinline__ uint32_t keep8(uint64_t seed, uint64_t off, uint64_t 
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void fwd_kernel(const T* __restrict__ g, int rows, int F,
+__global__ __launch_bounds__(128) void fwd_kernel(const T* __restrict__ g, int rows, int F,
                                                   float p, uint32_t th, float ks, uint64_t seed,
                                                   uint64_t off, T* __restrict__ a) {
-  const size_t n8 = (size_t)rows * F / 8;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8;
-       i += (size_t)gridDim.x * blockDim.x) {
-    const size_t e = i * 8;
-    const size_t r = e / F, c = e % F;
+  // 2-D launch: blockIdx.y walks rows, x covers one row's F/8 vectors (no 64-bit div/mod)
+  const int f8 = F / 8;
+  for (int r = blockIdx.y; r < rows; r += gridDim.y)
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < f8; v += gridDim.x * blockDim.x) {
+    const size_t c = (size_t)v * 8;
+    const size_t e = (size_t)r * F + c;
     Vec8<T> g1, g2;
-    g1.load(g + r * 2 * F + c);
-    g2.load(g + r * 2 * F + F + c);
+    g1.load(g + (size_t)r * 2 * F + c);
+    g2.load(g + (size_t)r * 2 * F + F + c);
     float o[8];
     uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
 #pragma unroll
@@ -61,17 +62,17 @@ __global__ __launch_bounds__(256) void fwd_kernel(const T* __restrict__ g, int r
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void bwd_kernel(const T* __restrict__ da, const T* __restrict__ g,
+__global__ __launch_bounds__(128) void bwd_kernel(const T* __restrict__ da, const T* __restrict__ g,
                                                   int rows, int F, float p, uint32_t th, float ks,
                                                   uint64_t seed, uint64_t off, T* __restrict__ dg) {
-  const size_t n8 = (size_t)rows * F / 8;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8;
-       i += (size_t)gridDim.x * blockDim.x) {
-    const size_t e = i * 8;
-    const size_t r = e / F, c = e % F;
+  const int f8 = F / 8;
+  for (int r = blockIdx.y; r < rows; r += gridDim.y)
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < f8; v += gridDim.x * blockDim.x) {
+    const size_t c = (size_t)v * 8;
+    const size_t e = (size_t)r * F + c;
     Vec8<T> g1, g2, d;
-    g1.load(g + r * 2 * F + c);
-    g2.load(g + r * 2 * F + F + c);
+    g1.load(g + (size_t)r * 2 * F + c);
+    g2.load(g + (size_t)r * 2 * F + F + c);
     d.load(da + e);
     uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
     float o1[8], o2[8];
@@ -83,14 +84,15 @@ __global__ __launch_bounds__(256) void bwd_kernel(const T* __restrict__ da, cons
       o1[j] = dd * g2[j] * gelu_erf_grad(x);
       o2[j] = dd * gelu_erf(x);
     }
-    Vec8<T>::store(dg + r * 2 * F + c, o1);
-    Vec8<T>::store(dg + r * 2 * F + F + c, o2);
+    Vec8<T>::store(dg + (size_t)r * 2 * F + c, o1);
+    Vec8<T>::store(dg + (size_t)r * 2 * F + F + c, o2);
   }
 }
 
-inline int grid_for(size_t n8) {
-  size_t b = (n8 + 255) / 256;
-  return (int)(b < 4096 ? (b ? b : 1) : 4096);
+inline dim3 grid_for(int rows, int F) {
+  const int bx = (F / 8 + 127) / 128;  // 3072/8 = 384 vectors -> 3 blocks of 128 per row
+  const int by = rows < 8192 ? (rows ? rows : 1) : 8192;
+  return dim3(bx, by);
 }
 
 }  // namespace geglu
@@ -104,15 +106,15 @@ extern "C" int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, floa
   DNA_CHECK_ARG(inter % 8 == 0 && rows >= 0, "dna_geglu_fwd: intermediate %% 8 != 0");
   DNA_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "dna_geglu_fwd: bad p");
   if (rows == 0) return DNA_OK;
-  const int grid = geglu::grid_for((size_t)rows * inter / 8);
+  const dim3 grid = geglu::grid_for(rows, inter);
   hipStream_t s = as_stream(stream);
   const uint32_t th = dropout_threshold(p_drop);
   const float ks = 1.f / (1.f - p_drop);
   if (dtype == DNA_BF16)
-    hipLaunchKernelGGL(geglu::fwd_kernel<bf16>, dim3(grid), dim3(256), 0, s, (const bf16*)g,
+    hipLaunchKernelGGL(geglu::fwd_kernel<bf16>, grid, dim3(128), 0, s, (const bf16*)g,
                        rows, inter, p_drop, th, ks, seed, offset, (bf16*)a);
   else if (dtype == DNA_F32)
-    hipLaunchKernelGGL(geglu::fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)g,
+    hipLaunchKernelGGL(geglu::fwd_kernel<float>, grid, dim3(128), 0, s, (const float*)g,
                        rows, inter, p_drop, th, ks, seed, offset, (float*)a);
   else
     DNA_CHECK_ARG(false, "dna_geglu_fwd: bad dtype");
@@ -125,15 +127,15 @@ extern "C" int dna_geglu_bwd(const void* da, const void* g, int dtype, int rows,
   DNA_CHECK_ARG(da && g && dg, "dna_geglu_bwd: null pointer");
   DNA_CHECK_ARG(inter % 8 == 0 && rows >= 0, "dna_geglu_bwd: intermediate %% 8 != 0");
   if (rows == 0) return DNA_OK;
-  const int grid = geglu::grid_for((size_t)rows * inter / 8);
+  const dim3 grid = geglu::grid_for(rows, inter);
   hipStream_t s = as_stream(stream);
   const uint32_t th = dropout_threshold(p_drop);
   const float ks = 1.f / (1.f - p_drop);
   if (dtype == DNA_BF16)
-    hipLaunchKernelGGL(geglu::bwd_kernel<bf16>, dim3(grid), dim3(256), 0, s, (const bf16*)da,
+    hipLaunchKernelGGL(geglu::bwd_kernel<bf16>, grid, dim3(128), 0, s, (const bf16*)da,
                        (const bf16*)g, rows, inter, p_drop, th, ks, seed, offset, (bf16*)dg);
   else if (dtype == DNA_F32)
-    hipLaunchKernelGGL(geglu::bwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)da,
+    hipLaunchKernelGGL(geglu::bwd_kernel<float>, grid, dim3(128), 0, s, (const float*)da,
                        (const float*)g, rows, inter, p_drop, th, ks, seed, offset, (float*)dg);
   else
     DNA_CHECK_ARG(false, "dna_geglu_bwd: bad dtype");

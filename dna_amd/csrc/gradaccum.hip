@@ -1,0 +1,112 @@
+// Gradient accumulation kernels that write straight into the flat fp32 .grad buffer.
+//
+//  * dna_sum_slices_accum: out += sum_k parts[k] -- the split-K weight-gradient partials of a
+//    [s, M, N] batched GEMM folded into the parameter's gradient in one pass (no separate reduce
+//    + AccumulateGrad add; replaces autograd's accumulation for Linear weights).
+//  * dna_embed_grad_segsum: d(word_embeddings) from per-token row gradients, by token id:
+//    rows visited in id-sorted order, summed in registers per run of equal ids, one atomic row
+//    flush per run per 32-row chunk -- frequent BPE tokens (thousands of rows per id in a
+//    65,536-token batch) no longer serialise on one row (nn.Embedding backward with
+//    padding_idx=0, bert_layers.py:45-47).
+#include "common.h"
+
+namespace dna {
+namespace gacc {
+
+__global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict__ parts, int s,
+                                                         size_t n, float* __restrict__ out) {
+  const size_t n4 = n / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gridDim.x * blockDim.x) {
+    f32x4 acc = reinterpret_cast<const f32x4*>(out)[i];
+    for (int k = 0; k < s; ++k) acc += reinterpret_cast<const f32x4*>(parts + (size_t)k * n)[i];
+    reinterpret_cast<f32x4*>(out)[i] = acc;
+  }
+  for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float acc = out[i];
+    for (int k = 0; k < s; ++k) acc += parts[(size_t)k * n + i];
+    out[i] = acc;
+  }
+}
+
+constexpr int SEG_CHUNK = 32;
+
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ drows,
+                                                     const int64_t* __restrict__ sorted_ids,
+                                                     const int64_t* __restrict__ perm, int rows,
+                                                     int cols, int vocab, int pad_idx,
+                                                     float* __restrict__ dE) {
+  const int lane = threadIdx.x & 63;
+  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int p0 = chunk * SEG_CHUNK;
+  if (p0 >= rows) return;
+  const int p1 = min(rows, p0 + SEG_CHUNK);
+  float acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.f;
+  long cur = (long)sorted_ids[p0];
+  auto flush = [&](long id) {
+    if (id == pad_idx || id < 0 || id >= vocab) return;
+    float* dst = dE + (size_t)id * cols;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) atomicAdd(dst + k * 64 + lane, acc[k]);
+  };
+  for (int p = p0; p < p1; ++p) {
+    const long id = (long)sorted_ids[p];
+    if (id != cur) {
+      flush(cur);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) acc[k] = 0.f;
+      cur = id;
+    }
+    const float* src = drows + (size_t)perm[p] * cols;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] += src[k * 64 + lane];
+  }
+  flush(cur);
+}
+
+}  // namespace gacc
+}  // namespace dna
+
+using namespace dna;
+
+extern "C" int dna_sum_slices_accum(const float* parts, int s, size_t n, float* out, void* stream) {
+  DNA_CHECK_ARG(parts && out && s >= 1, "dna_sum_slices_accum: bad args");
+  DNA_CHECK_ARG((((uintptr_t)parts | (uintptr_t)out) & 15) == 0 && n % 4 == 0,
+                "dna_sum_slices_accum: needs 16-byte aligned buffers and n %% 4 == 0");
+  size_t blocks = (n / 4 + 255) / 256;
+  int nb = (int)(blocks < 4096 ? (blocks ? blocks : 1) : 4096);
+  hipLaunchKernelGGL(gacc::sum_slices_kernel, dim3(nb), dim3(256), 0, as_stream(stream), parts, s,
+                     n, out);
+  DNA_LAUNCH_CHECK("dna_sum_slices_accum");
+  return DNA_OK;
+}
+
+extern "C" int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_ids,
+                                     const int64_t* perm, int rows, int cols, int vocab,
+                                     int padding_idx, float* dword_emb, void* stream) {
+  DNA_CHECK_ARG(drows && sorted_ids && perm && dword_emb, "dna_embed_grad_segsum: null pointer");
+  DNA_CHECK_ARG(cols % 64 == 0 && cols <= 1024, "dna_embed_grad_segsum: cols %% 64 != 0");
+  if (rows == 0) return DNA_OK;
+  const int chunks = (rows + gacc::SEG_CHUNK - 1) / gacc::SEG_CHUNK;
+  dim3 grid((chunks + 3) / 4);
+  hipStream_t s = as_stream(stream);
+  switch (cols / 64) {
+#define DNA_SEG_CASE(K)                                                                         \
+  case K:                                                                                       \
+    hipLaunchKernelGGL(gacc::segsum_kernel<K>, grid, dim3(256), 0, s, drows, sorted_ids, perm,   \
+                       rows, cols, vocab, padding_idx, dword_emb);                               \
+    break;
+    DNA_SEG_CASE(1) DNA_SEG_CASE(2) DNA_SEG_CASE(3) DNA_SEG_CASE(4) DNA_SEG_CASE(6)
+    DNA_SEG_CASE(8) DNA_SEG_CASE(12) DNA_SEG_CASE(16)
+#undef DNA_SEG_CASE
+    default:
+      set_error("dna_embed_grad_segsum: cols=%d unsupported", cols);
+      return DNA_ERR_UNSUPPORTED;
+  }
+  DNA_LAUNCH_CHECK("dna_embed_grad_segsum");
+  return DNA_OK;
+}

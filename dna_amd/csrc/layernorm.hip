@@ -14,7 +14,7 @@ namespace dna {
 namespace ln {
 
 constexpr int WAVES = 4;  // rows per block in the forward
-constexpr int BWD_BLOCKS = 256;
+constexpr int BWD_BLOCKS = 512;
 
 // column of value k of a lane
 template <bool VEC>
@@ -276,6 +276,7 @@ struct EmbBwdArgs {
   const float* dy; const bf16* dyb; const int64_t* ids; const float* E; const float* tt;
   const float* gamma; const float* mean; const float* rstd; int rows, cols, vocab, pad_idx;
   float p; uint32_t th; float kscale; uint64_t seed, off; float* dE; float* part;
+  float* drows;  // if set: d(embedding row) per token is written here instead of atomics into dE
 };
 
 template <int NV, bool VEC>
@@ -324,12 +325,18 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(EmbBwdArgs a) {
     }
     const float c1 = wave_sum(s1) * inv_cols, c2 = wave_sum(s2) * inv_cols;
     const bool to_table = id != a.pad_idx;
-    float* drow = a.dE + (size_t)id * a.cols;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const float d = rs * (g[k] - c1 - v[k] * c2);
       acc_t[k] += d;
-      if (to_table) atomicAdd(drow + col_of<VEC>(k, lane), d);
+      g[k] = d;
+    }
+    if (a.drows) {
+      store_row<float, NV, VEC>(a.drows + ro, lane, g);
+    } else if (to_table) {
+      float* drow = a.dE + (size_t)id * a.cols;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) atomicAdd(drow + col_of<VEC>(k, lane), g[k]);
     }
   }
   block_partials<NV, VEC>(acc_g, acc_b, acc_t, a.cols, a.part);
@@ -475,14 +482,14 @@ extern "C" int dna_embed_ln_fwd(const int64_t* ids, const float* word_emb, const
   return DNA_OK;
 }
 
-extern "C" int dna_embed_ln_bwd(const float* dy, const void* dy_bf16, const int64_t* ids,
-                                const float* word_emb, const float* type_row, const float* gamma,
-                                const float* mean, const float* rstd, int rows, int cols,
-                                int vocab, int padding_idx, float p_drop, uint64_t seed,
-                                uint64_t offset, float* dword_emb, float* dtype_row,
-                                float* dgamma, float* dbeta, void* workspace,
-                                size_t workspace_bytes, void* stream) {
-  DNA_CHECK_ARG(ids && word_emb && type_row && gamma && mean && rstd && dword_emb,
+static int embed_ln_bwd_impl(const float* dy, const void* dy_bf16, const int64_t* ids,
+                             const float* word_emb, const float* type_row, const float* gamma,
+                             const float* mean, const float* rstd, int rows, int cols, int vocab,
+                             int padding_idx, float p_drop, uint64_t seed, uint64_t offset,
+                             float* dword_emb, float* drows, float* dtype_row, float* dgamma,
+                             float* dbeta, void* workspace, size_t workspace_bytes,
+                             void* stream) {
+  DNA_CHECK_ARG(ids && word_emb && type_row && gamma && mean && rstd && (dword_emb || drows),
                 "dna_embed_ln_bwd: null pointer");
   if (rows == 0) return DNA_OK;
   DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
@@ -490,7 +497,7 @@ extern "C" int dna_embed_ln_bwd(const float* dy, const void* dy_bf16, const int6
   const int nb = bwd_blocks(rows);
   EmbBwdArgs a{dy, (const bf16*)dy_bf16, ids, word_emb, type_row, gamma, mean, rstd, rows, cols,
                vocab, padding_idx, p_drop, dropout_threshold(p_drop), 1.f / (1.f - p_drop), seed,
-               offset, dword_emb, (float*)workspace};
+               offset, dword_emb, (float*)workspace, drows};
   hipStream_t s = as_stream(stream);
   const size_t lds = (size_t)WAVES * 3 * cols * sizeof(float);
   int st = dispatch_cols(cols, [&](auto nv, auto vec) {
@@ -504,4 +511,28 @@ extern "C" int dna_embed_ln_bwd(const float* dy, const void* dy_bf16, const int6
                      (const float*)workspace, nb, cols, dgamma, dbeta, dtype_row);
   DNA_LAUNCH_CHECK("dna_embed_ln_bwd");
   return DNA_OK;
+}
+
+extern "C" int dna_embed_ln_bwd(const float* dy, const void* dy_bf16, const int64_t* ids,
+                                const float* word_emb, const float* type_row, const float* gamma,
+                                const float* mean, const float* rstd, int rows, int cols,
+                                int vocab, int padding_idx, float p_drop, uint64_t seed,
+                                uint64_t offset, float* dword_emb, float* dtype_row,
+                                float* dgamma, float* dbeta, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  return embed_ln_bwd_impl(dy, dy_bf16, ids, word_emb, type_row, gamma, mean, rstd, rows, cols,
+                           vocab, padding_idx, p_drop, seed, offset, dword_emb, nullptr,
+                           dtype_row, dgamma, dbeta, workspace, workspace_bytes, stream);
+}
+
+extern "C" int dna_embed_ln_bwd_rows(const float* dy, const void* dy_bf16, const int64_t* ids,
+                                     const float* word_emb, const float* type_row,
+                                     const float* gamma, const float* mean, const float* rstd,
+                                     int rows, int cols, int vocab, float p_drop, uint64_t seed,
+                                     uint64_t offset, float* drows, float* dtype_row,
+                                     float* dgamma, float* dbeta, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  return embed_ln_bwd_impl(dy, dy_bf16, ids, word_emb, type_row, gamma, mean, rstd, rows, cols,
+                           vocab, -1, p_drop, seed, offset, nullptr, drows, dtype_row, dgamma,
+                           dbeta, workspace, workspace_bytes, stream);
 }

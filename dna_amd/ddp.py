@@ -40,6 +40,8 @@ class GradBucketReducer:
         self._works = []
         self._fired = [False] * len(self.buckets)
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in flat.params]
+        for p in flat.params:  # contributions written directly by fused kernels report here
+            p._dna_notify = self._hook
         self.enabled = self.world > 1
 
     def _hook(self, p):

@@ -60,3 +60,10 @@ class FlatParams:
 
     def zero_grad(self):
         self.grad.zero_()
+
+    def enable_direct_grad(self, on=True):
+        """Let fused backward kernels accumulate weight gradients straight into the flat .grad
+        views (dna_amd.functional.Linear) instead of returning them to AccumulateGrad. Only valid
+        for loss.backward() into these .grad buffers (not torch.autograd.grad)."""
+        for p in self.params:
+            p._dna_direct = bool(on)

@@ -113,7 +113,6 @@ class EmbeddingLN(torch.autograd.Function):
         ids, E, tt, gamma, mean, rstd = ctx.saved_tensors
         _, p, seed, off = ctx.cfg
         T, (V, d) = ids.numel(), E.shape
-        dE = torch.zeros_like(E)
         dtt = torch.zeros_like(tt)
         dg = torch.empty_like(gamma)
         db = torch.empty_like(gamma)
@@ -121,10 +120,17 @@ class EmbeddingLN(torch.autograd.Function):
         ws = torch.empty(max(nws, 16), device=E.device, dtype=torch.uint8)
         dy = None if dy is None else dy.contiguous()
         dyb = None if dyb is None else dyb.contiguous()
-        N.call("dna_embed_ln_bwd", _p(dy), _p(dyb), ids.data_ptr(), E.data_ptr(),
-               tt[0].data_ptr(), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), T, d, V, 0,
-               p, seed, off, dE.data_ptr(), dtt[0].data_ptr(), dg.data_ptr(), db.data_ptr(),
+        # per-token row gradients, then an id-sorted segmented sum into the table (frequent
+        # tokens would otherwise serialise thousands of atomic row adds on one row)
+        drows = torch.empty(T, d, device=E.device, dtype=torch.float32)
+        N.call("dna_embed_ln_bwd_rows", _p(dy), _p(dyb), ids.data_ptr(), E.data_ptr(),
+               tt[0].data_ptr(), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), T, d, V,
+               p, seed, off, drows.data_ptr(), dtt[0].data_ptr(), dg.data_ptr(), db.data_ptr(),
                ws.data_ptr(), nws, N.stream_ptr())
+        sorted_ids, perm = torch.sort(ids)
+        dE = torch.zeros_like(E)
+        N.call("dna_embed_grad_segsum", drows.data_ptr(), sorted_ids.data_ptr(), perm.data_ptr(),
+               T, d, V, 0, dE.data_ptr(), N.stream_ptr())
         return None, dE, dtt, dg, db, None, None, None, None, None, None
 
 
@@ -278,6 +284,7 @@ class Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, w_lp, b):
         ctx.save_for_backward(x, w_lp)
+        ctx.weight = w
         ctx.has_b = b is not None
         flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
         with _timed("gemm", flops):
@@ -294,8 +301,18 @@ class Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             with _timed("gemm", flops):
                 dx = torch.mm(dy, w_lp)
+        w = ctx.weight
         with _timed("gemm", flops):
-            dw = wgrad(dy, x)
+            if getattr(w, "_dna_direct", False) and w.grad is not None and x.dtype != torch.float32:
+                # write straight into the flat fp32 gradient buffer (dna_amd.flat) and tell the
+                # gradient-bucket reducer, instead of returning dW to AccumulateGrad
+                wgrad_accumulate(dy, x, w.grad)
+                notify = getattr(w, "_dna_notify", None)
+                if notify is not None:
+                    notify(w)
+                dw = None
+            else:
+                dw = wgrad(dy, x)
         db = dy.sum(0, dtype=torch.float32) if ctx.has_b else None
         return dx, dw, None, db
 
@@ -324,6 +341,20 @@ def wgrad(dy, x):
     a = dy.view(s, rows // s, m).transpose(1, 2)
     b = x.view(s, rows // s, n)
     return torch.bmm(a, b, out_dtype=torch.float32).sum(0)
+
+
+def wgrad_accumulate(dy, x, grad):
+    """grad[m, n] += dy^T x: split-K partials from hipBLASLt folded in by one native pass."""
+    rows, m = dy.shape
+    n = x.shape[1]
+    assert grad.is_contiguous() and grad.dtype == torch.float32 and grad.shape == (m, n)
+    s = wgrad_splits(rows, m, n)
+    if s == 1:
+        parts = torch.mm(dy.t(), x, out_dtype=torch.float32)
+    else:
+        parts = torch.bmm(dy.view(s, rows // s, m).transpose(1, 2), x.view(s, rows // s, n),
+                          out_dtype=torch.float32)
+    N.call("dna_sum_slices_accum", parts.data_ptr(), s, m * n, grad.data_ptr(), N.stream_ptr())
 
 
 def linear(x, w, w_lp, b=None):

@@ -49,6 +49,7 @@ class MLMTrainer:
         self.model = model.to(device).train()
         self.device = device
         self.flat = FlatParams(self.model, device)
+        self.flat.enable_direct_grad(True)
         self.opt = FusedAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                               max_grad_norm=max_grad_norm)
         self.sched = None

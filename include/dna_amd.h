@@ -107,6 +107,26 @@ int dna_embed_ln_bwd(const float* dy, const void* dy_bf16, const int64_t* ids,
                      float* dword_emb, float* dtype_row, float* dgamma, float* dbeta,
                      void* workspace, size_t workspace_bytes, void* stream);
 
+/* Same backward, but instead of accumulating into the table it writes each token's embedding-row
+ * gradient to drows [rows, cols] fp32 (for dna_embed_grad_segsum). */
+int dna_embed_ln_bwd_rows(const float* dy, const void* dy_bf16, const int64_t* ids,
+                          const float* word_emb, const float* type_row, const float* gamma,
+                          const float* mean, const float* rstd, int rows, int cols, int vocab,
+                          float p_drop, uint64_t seed, uint64_t offset, float* drows,
+                          float* dtype_row, float* dgamma, float* dbeta, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
+/* dword_emb[id] += sum of drows[perm[p]] over the id-sorted positions p (sorted_ids ascending,
+ * perm = the argsort of ids); rows with id == padding_idx are skipped. Replaces the scatter-add
+ * of nn.Embedding backward (padding_idx=0, bert_layers.py:45-47). */
+int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_ids, const int64_t* perm,
+                          int rows, int cols, int vocab, int padding_idx, float* dword_emb,
+                          void* stream);
+
+/* out[i] += sum_{k<s} parts[k*n + i]: split-K partials of a weight gradient folded straight
+ * into the flat fp32 gradient buffer (16-byte aligned, n % 4 == 0). */
+int dna_sum_slices_accum(const float* parts, int s, size_t n, float* out, void* stream);
+
 /* ------------------------------------------------------------------ GeGLU (+ dropout)
  * a = dropout( gelu_erf(g[:, :inter]) * g[:, inter:] )   (bert_layers.py:292-296)
  *   g [rows, 2*inter] dtype -> a [rows, inter] dtype. */

@@ -145,3 +145,25 @@ def test_bf16_training_reduces_loss():
         losses.append(loss.item())
     assert all(math.isfinite(x) for x in losses)
     assert losses[-1] < losses[0] - 1.0, losses
+
+
+def test_direct_grad_accumulation_matches_autograd():
+    """Trainer path (weight grads written straight into the flat buffer by fused kernels) ==
+    plain autograd accumulation, bf16 mode, dropout off."""
+    from dna_amd.bert_layers import BertForMaskedLM, MLMIndex
+    from dna_amd.flat import FlatParams
+    z, cfg = _golden("cfgA")
+    ids, mask, labels = _batch(z)
+    idx = MLMIndex.build(ids, labels)
+    grads = []
+    for direct in (False, True):
+        torch.manual_seed(0)
+        m = BertForMaskedLM(cfg, precision="bf16").to(DEV).eval()
+        flat = FlatParams(m, DEV)
+        flat.enable_direct_grad(direct)
+        flat.zero_grad()
+        loss, _ = m.mlm_loss(ids, mask, idx)
+        loss.backward()
+        grads.append(flat.grad.clone())
+    scale = grads[0].abs().max().item()
+    assert (grads[0] - grads[1]).abs().max().item() < 1e-3 * scale
