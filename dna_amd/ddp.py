@@ -39,13 +39,14 @@ class GradBucketReducer:
         self._pending = [0] * len(self.buckets)
         self._works = []
         self._fired = [False] * len(self.buckets)
+        self._sync = True
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in flat.params]
         for p in flat.params:  # contributions written directly by fused kernels report here
             p._dna_notify = self._hook
         self.enabled = self.world > 1
 
     def _hook(self, p):
-        if not self.enabled:
+        if not self.enabled or not self._sync:
             return
         pid = id(p)
         self._seen[pid] = self._seen.get(pid, 0) + 1
@@ -63,8 +64,12 @@ class GradBucketReducer:
         self._works.append(dist.all_reduce(self.flat.grad[s:e], op=dist.ReduceOp.SUM,
                                            group=self.group, async_op=True))
 
-    def prepare(self):
-        """Call before each backward."""
+    def prepare(self, sync=True):
+        """Call before each backward; sync=False for accumulation micro-batches (no collective,
+        gradients keep accumulating locally, like DDP's no_sync())."""
+        self._sync = sync
+        if not sync:
+            return
         self._seen = {}
         self._works = []
         self._fired = [False] * len(self.buckets)
@@ -77,7 +82,7 @@ class GradBucketReducer:
 
     def finish(self):
         """Call after backward: launch what did not fire, wait for all collectives."""
-        if not self.enabled:
+        if not self.enabled or not self._sync:
             return
         if self.expected is None:
             self.expected = dict(self._seen)

@@ -65,15 +65,25 @@ class MLMTrainer:
         self.model.dropout_rng.seed = (self.model.dropout_rng.seed * 1000003 + rank) & (2 ** 63 - 1)
         self.global_step = 0
 
-    def step(self, batch: DeviceBatch) -> torch.Tensor:
+    def step(self, batch) -> torch.Tensor:
+        """One optimizer step over one micro-batch or a list of them (accumulate_grad_batches:
+        each micro-batch loss is divided by their number, like Lightning; gradients are
+        all-reduced only during the last micro-batch's backward, like DDP no_sync)."""
+        micro = batch if isinstance(batch, (list, tuple)) else [batch]
         self.opt.zero_grad()
-        self.reducer.prepare()
-        loss, _ = self.model.mlm_loss(batch.masked_ids, batch.mask, batch.index, batch.n_mask,
-                                      batch.n_unk_masked)
-        loss.backward()
+        total = None
+        for i, mb in enumerate(micro):
+            last = i == len(micro) - 1
+            self.reducer.prepare(sync=last)
+            loss, _ = self.model.mlm_loss(mb.masked_ids, mb.mask, mb.index, mb.n_mask,
+                                          mb.n_unk_masked)
+            if len(micro) > 1:
+                loss = loss / len(micro)
+            loss.backward()
+            total = loss.detach() if total is None else total + loss.detach()
         self.reducer.finish()
         self.opt.step(grad_scale=self.reducer.grad_scale)
         if self.sched is not None:
             self.sched.step()
         self.global_step += 1
-        return loss.detach()
+        return total

@@ -1,0 +1,226 @@
+#!/usr/bin/env python
+"""`python train.py experiment=dnabert2/dnabert2_hg38_pretrain key=value ...` on MI355X.
+
+Mirrors the reference entry point (train.py:699-711: Hydra main over configs/config.yaml, then
+train() :668-694 -> Lightning fit) for the DNABERT-2 MLM path, without Hydra or Lightning:
+  * config: dna_amd.compose (defaults lists, @package, overrides, eval/div_up resolvers);
+    `--config-dir` may point at the reference's own configs/ tree, which composes unchanged;
+  * registries: model "dnabert2" -> dna_amd.bert_layers.BertForMaskedLM (src/utils/registry.py:39),
+    dataset "bert_hg38" -> dna_amd.hg38.BertHG38, task "hg38" + loss "bert_cross_entropy";
+  * loop: MLMTrainer steps (fused loss, bucketed RCCL all-reduce, clip + AdamW, LR schedule per
+    optimizer step, `accumulate_grad_batches`), DistributedSampler sharding across ranks
+    (one process per GPU, torch.distributed.run), metrics train/loss, trainer/loss,
+    train/perplexity, train/num_tokens, timer/step;
+  * checkpoints in Lightning's layout ({"state_dict": {"model.<key>": ...}, ...}) so
+    `train.pretrained_model_path` / `trainer.resume_from_checkpoint` interoperate; a missing
+    resume path (the reference configs carry cluster paths) is a warning, not a crash.
+The product path is GPU-only: `trainer.accelerator=cpu` is rejected (no CPU fallback).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+import warnings
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from dna_amd.compose import compose  # noqa: E402
+
+MODEL_REGISTRY = {"dnabert2": "dna_amd.bert_layers.BertForMaskedLM"}
+
+
+def _import(path):
+    mod, name = path.rsplit(".", 1)
+    return getattr(__import__(mod, fromlist=[name]), name)
+
+
+def _precision(p):
+    p = str(p)
+    if p in ("bf16", "bf16-mixed", "bfloat16"):
+        return "bf16"
+    if p in ("32", "32-true", "fp32", "float32"):
+        return "fp32"
+    raise ValueError(f"trainer.precision={p!r}: bf16 or 32")
+
+
+def build_dataset(cfg):
+    from dna_amd.hg38 import SequenceDataset
+    kw = {k: v for k, v in cfg.dataset.to_container().items()
+          if k != "_name_" and not k.startswith("__")}  # process_config drops "__" keys
+    ds = SequenceDataset.registry[cfg.dataset._name_](**kw)
+    return ds
+
+
+def load_lightning_state(model, path, strict):
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    sd = ck.get("state_dict", ck)
+    sd = {k[len("model."):] if k.startswith("model.") else k: v for k, v in sd.items()}
+    missing, unexpected = model.load_state_dict(sd, strict=strict)
+    return missing, unexpected
+
+
+def save_checkpoint(path, trainer, epoch):
+    m = trainer.model
+    sd = {"model." + k: v.detach().cpu() for k, v in m.state_dict().items()}
+    torch.save({"state_dict": sd, "epoch": epoch, "global_step": trainer.global_step,
+                "optimizer_states": [{k: (v.cpu() if torch.is_tensor(v) else v)
+                                      for k, v in trainer.opt.state_dict().items()}],
+                "lr_schedulers": [trainer.sched.state_dict()] if trainer.sched else []}, path)
+
+
+def train(cfg, dry_run=False, out=sys.stdout):
+    from dna_amd.bert_layers import BertForMaskedLM  # noqa: F401
+    from dna_amd.trainer import DeviceBatch, MLMTrainer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    seed = cfg.train.get("seed")
+    if seed is not None:
+        torch.manual_seed(int(seed) + rank)
+
+    tr = cfg.trainer
+    if str(tr.get("accelerator", "gpu")) not in ("gpu", "cuda", "auto"):
+        raise RuntimeError(f"trainer.accelerator={tr.accelerator!r}: dna_amd runs the hot path "
+                           "on MI355X GPUs only (no CPU fallback)")
+    model_cls = _import(MODEL_REGISTRY[cfg.model._name_])
+    model = model_cls(config=cfg.model.config.to_container(),
+                      precision=_precision(tr.get("precision", "bf16")))
+    pre = cfg.train.get("pretrained_model_path")
+    if pre:
+        if os.path.exists(pre):
+            load_lightning_state(model, pre, bool(cfg.train.get("pretrained_model_strict_load", True)))
+        else:
+            warnings.warn(f"train.pretrained_model_path {pre} not found; starting from init")
+    ds = build_dataset(cfg)
+    ds.setup()
+    task = _import("dna_amd.tasks.registry")[cfg.task._name_]
+    task = task(loss=cfg.task.loss, torchmetrics=cfg.task.get("torchmetrics"))
+    sched = None
+    if "scheduler" in cfg and cfg.scheduler is not None:
+        sc = {k: v for k, v in cfg.scheduler.to_container().items() if k != "_name_"}
+        if cfg.scheduler._name_ != "linear_warmup":
+            raise NotImplementedError(f"scheduler {cfg.scheduler._name_!r} (linear_warmup only)")
+        sched = sc
+    opt = cfg.optimizer
+    if dry_run:
+        print(json.dumps({"dry_run": True, "model_params": sum(p.numel() for p in model.parameters()),
+                          "train_windows": len(ds.dataset_train), "task": task.loss_name,
+                          "scheduler": sched, "optimizer": opt.to_container()}), file=out)
+        return None
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    trainer = MLMTrainer(model, device, lr=float(opt.lr),
+                         weight_decay=float(opt.get("weight_decay", 0.0)),
+                         betas=tuple(opt.get("betas", (0.9, 0.999))),
+                         max_grad_norm=float(tr.get("gradient_clip_val", 0.0) or 0.0),
+                         scheduler=sched)
+    resume = tr.get("resume_from_checkpoint") or cfg.train.get("ckpt")
+    start_epoch = 0
+    if resume:
+        if os.path.exists(resume):
+            ck = torch.load(resume, map_location="cpu", weights_only=True)
+            load_lightning_state(model, resume, True)
+            trainer.flat.refresh_shadow()
+            if ck.get("optimizer_states"):
+                trainer.opt.load_state_dict(ck["optimizer_states"][0])
+            if ck.get("lr_schedulers") and trainer.sched:
+                trainer.sched.load_state_dict(ck["lr_schedulers"][0])
+            trainer.global_step = int(ck.get("global_step", 0))
+            start_epoch = int(ck.get("epoch", 0))
+        else:
+            warnings.warn(f"resume checkpoint {resume} not found; training from scratch")
+
+    sampler = None
+    if world > 1:
+        sampler = torch.utils.data.distributed.DistributedSampler(
+            ds.dataset_train, num_replicas=world, rank=rank, shuffle=True,
+            seed=int(seed or 0))
+    loader = ds.train_dataloader(sampler=sampler)
+    accum = int(tr.get("accumulate_grad_batches", 1) or 1)
+    max_steps = cfg.train.get("max_steps") or tr.get("max_steps")
+    max_epochs = int(tr.get("max_epochs", 1) or 1)
+    log_every = int(tr.get("log_every_n_steps", 10) or 10)
+    limit = tr.get("limit_train_batches", 1.0)
+    pad_id = getattr(ds.tokenizer, "pad_token_id", 3)
+    ppl_sum, ppl_cnt, num_tokens = 0.0, 0, 0
+    t_last = time.perf_counter()
+    done = False
+    for epoch in range(start_epoch, max_epochs):
+        if sampler is not None:
+            sampler.set_epoch(epoch)
+        n_batches = len(loader)
+        if isinstance(limit, float) and limit <= 1.0:
+            n_batches = max(1, int(n_batches * limit))
+        elif limit:
+            n_batches = min(n_batches, int(limit))
+        micro = []
+        for bi, ((masked, mask, labels), target) in enumerate(loader):
+            if bi >= n_batches:
+                break
+            micro.append(DeviceBatch.from_host(masked, mask, labels, target, device, pad_id))
+            num_tokens += target.numel()
+            if len(micro) < accum:
+                continue
+            loss = trainer.step(micro)
+            micro = []
+            step = trainer.global_step
+            if step % log_every == 0 or step == 1:
+                lv = float(loss.item())
+                ppl_sum += lv
+                ppl_cnt += 1
+                now = time.perf_counter()
+                if rank == 0:
+                    print(json.dumps({"step": step, "epoch": epoch, "train/loss": round(lv, 5),
+                                      "trainer/loss": round(lv, 5),
+                                      "train/perplexity": round(math.exp(ppl_sum / ppl_cnt), 4),
+                                      "train/num_tokens": num_tokens * world,
+                                      "trainer/lr": trainer.opt.param_groups[0]["lr"],
+                                      "timer/step": round((now - t_last) / (log_every if step > 1 else 1), 5)}),
+                          file=out, flush=True)
+                t_last = now
+            if max_steps and step >= int(max_steps):
+                done = True
+                break
+        if done:
+            break
+    ck_cfg = cfg.get("callbacks", {}) or {}
+    mc = ck_cfg.get("model_checkpoint") if ck_cfg else None
+    if rank == 0 and mc is not None:
+        d = mc.get("dirpath", "checkpoints/")
+        os.makedirs(d, exist_ok=True)
+        save_checkpoint(os.path.join(d, "last.ckpt"), trainer, epoch)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return trainer
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--config-dir", default=os.environ.get("DNA_CONFIG_DIR",
+                                                           os.path.join(ROOT, "configs")))
+    ap.add_argument("--config-name", default="config")
+    ap.add_argument("--dry-run", action="store_true", help="compose + build, no training")
+    ap.add_argument("--print-config", action="store_true")
+    ap.add_argument("overrides", nargs="*")
+    a = ap.parse_args(argv)
+    cfg = compose(a.config_dir, a.config_name, a.overrides)
+    if a.print_config:
+        print(json.dumps(cfg.to_container(skip_errors=True), indent=1, default=str))
+    return train(cfg, dry_run=a.dry_run)
+
+
+if __name__ == "__main__":
+    main()
