@@ -32,11 +32,17 @@ constexpr float PAD_BIAS = -10000.0f;  // bert_layers.py:424
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 
-// element offset of (row, col) in a [64][64] bf16 tile with 16-byte chunks XOR-swizzled by row:
-// rows r and r+1 share a 256-byte bank row, so the swizzle key is (r>>1)&7 -> conflict-free
-// ds_read_b128 for 16 lanes reading 16 consecutive rows at one chunk.
+// element offset of (row, col) in a [64][64] bf16 tile (128-B rows) with 16-byte chunks
+// XOR-swizzled by row. Rows r, r+1 share a 256-B bank row, so the key depends on r>>1:
+//  * row reads (ds_read_b128, 16 lanes = 16 consecutive rows, one chunk): any bijection of
+//    (r>>1)&7 spreads the 8 row pairs over 8 chunk slots -> conflict-free;
+//  * transposed reads (ds_read_b64_tr_b16, a 32-lane half reads rows r0..r0+3, 4 chunks): rows r0
+//    and r0+2 must land in different chunk halves, i.e. their keys differ in bit 2 -- so the key
+//    is the bit-reversal of (r>>1)&7.
 __device__ __forceinline__ int swz(int r, int c) {
-  return r * D + ((((c >> 3) ^ (r >> 1)) & 7) << 3) + (c & 7);
+  const int k = (r >> 1) & 7;
+  const int key = ((k & 1) << 2) | (k & 2) | ((k >> 2) & 1);
+  return r * D + ((((c >> 3) ^ key) & 7) << 3) + (c & 7);
 }
 
 __device__ __forceinline__ bf16x4 tr_read(const bf16* lds_elem_ptr) {
@@ -67,6 +73,26 @@ __device__ __forceinline__ float alibi_b(float slope2, float h4) {
   return fmaf(slope2, (float)(KH * 32 + (R & 3) + 8 * (R >> 2)), h4);
 }
 
+
+// Block -> (tile, head, batch). Blocks are dealt round-robin over the 8 XCDs (each with its own
+// L2); all tiles of one (batch, head) read the same K/V (or Q/dO) rows, so map them to blocks with
+// equal blockIdx % 8 (speed only -- placement is not guaranteed; any mapping is correct).
+__device__ __forceinline__ void decode_block(int ntile, int H, int& tile, int& h, int& b) {
+  const int L = blockIdx.x;
+  const int nbh = gridDim.x / ntile;
+  int bh;
+  if ((nbh & 7) == 0) {
+    const int r = L >> 3;
+    tile = r % ntile;
+    bh = (r / ntile) * 8 + (L & 7);
+  } else {
+    tile = L % ntile;
+    bh = L / ntile;
+  }
+  h = bh % H;
+  b = bh / H;
+}
+
 // ----------------------------------------------------------------------------- bf16 forward
 struct TileRegs {
   bf16x8 k[2], v[2];
@@ -80,15 +106,16 @@ __global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ 
                                                         float* __restrict__ lse) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Ks = reinterpret_cast<bf16*>(smem);            // [2][64*64] swizzled
-  bf16* Vs = Ks + 2 * BK * D;                           // [2][64*64] plain
+  bf16* Vs = Ks + 2 * BK * D;                           // [2][64*64] swizzled
   float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);  // [2][64] pad bias (log2 units)
 
-  const int h = blockIdx.y, b = blockIdx.z;
+  int qblk, h, b;
+  decode_block((S + BQ - 1) / BQ, H, qblk, h, b);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int ql = lane & 31, hh = lane >> 5;
   const int ld = 3 * H * D;
   const bf16* base = qkv + (size_t)b * S * ld;
-  const int q0 = blockIdx.x * BQ + wave * 32;
+  const int q0 = qblk * BQ + wave * 32;
   const int qi = q0 + ql;
   const int qrow = min(qi, S - 1);
   const float slope2 = slopes[h] * LOG2E;
@@ -115,7 +142,7 @@ __global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ 
     for (int i = 0; i < 2; ++i) {
       int c = tid + i * 256, r = c >> 3, ch = c & 7;
       *reinterpret_cast<bf16x8*>(Ks + buf * BK * D + swz(r, ch * 8)) = t.k[i];
-      *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + r * D + ch * 8) = t.v[i];
+      *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + swz(r, ch * 8)) = t.v[i];
     }
     if (tid < BK) kb[buf * BK + tid] = bias;
   };
@@ -126,7 +153,7 @@ __global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ 
   float m = -INFINITY, l = 0.f;
 
   const int nt = S / BK;
-  const int kt0 = (blockIdx.x * BQ / BK) % nt;  // diagonal tiles first: the max settles early
+  const int kt0 = (qblk * BQ / BK) % nt;  // diagonal tiles first: the max settles early
   {
     TileRegs t; float bias;
     load_tile(kt0, t, bias);
@@ -238,7 +265,7 @@ __global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ 
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
           const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
-          bf16x8 a = cat(tr_read(V + krow * D + dcol), tr_read(V + (krow + 8) * D + dcol));
+          bf16x8 a = cat(tr_read(V + swz(krow, dcol)), tr_read(V + swz(krow + 8, dcol)));
           oacc[dt] = mfma(a, pbf, oacc[dt]);
         }
       }
@@ -292,12 +319,13 @@ __global__ __launch_bounds__(256) void dq_bf16_kernel(
   bf16* Vs = Ks + 2 * BK * D;                    // [2][64*64] swizzled
   float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);
 
-  const int h = blockIdx.y, b = blockIdx.z;
+  int qblk, h, b;
+  decode_block((S + BQ - 1) / BQ, H, qblk, h, b);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int ql = lane & 31, hh = lane >> 5;
   const int ld = 3 * H * D;
   const bf16* base = qkv + (size_t)b * S * ld;
-  const int qi = blockIdx.x * BQ + wave * 32 + ql;
+  const int qi = qblk * BQ + wave * 32 + ql;
   const int qrow = min(qi, S - 1);
   const float slope2 = slopes[h] * LOG2E;
   const float lse2 = lse[((size_t)b * H + h) * S + qrow] * LOG2E;
@@ -350,7 +378,7 @@ __global__ __launch_bounds__(256) void dq_bf16_kernel(
   __syncthreads();
   const int g16 = lane >> 4, i16 = lane & 15;
 
-  const int q0 = blockIdx.x * BQ + wave * 32;
+  const int q0 = qblk * BQ + wave * 32;
   const float h4 = slope2 * 4.f * hh;
   for (int kt = 0; kt < nt; ++kt) {
     const int buf = kt & 1;
@@ -451,13 +479,14 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
   float* ls = reinterpret_cast<float*>(Os + 2 * BQT * D);  // [2][64] lse (log2)
   float* ds = ls + 2 * BQT;                                 // [2][64] delta
 
-  const int h = blockIdx.y, b = blockIdx.z;
+  int kblk, h, b;
+  decode_block((S + BKW - 1) / BKW, H, kblk, h, b);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int kl = lane & 31, hh = lane >> 5;
   const int ld = 3 * H * D;
   const bf16* base = qkv + (size_t)b * S * ld;
   const bf16* obase = dout + (size_t)b * S * (H * D);
-  const int kj = blockIdx.x * BKW + wave * 32 + kl;
+  const int kj = kblk * BKW + wave * 32 + kl;
   const int krow = min(kj, S - 1);
   const float slope2 = slopes[h] * LOG2E;
   const float kbias = (key_valid && !key_valid[(size_t)b * S + krow]) ? PAD_BIAS * LOG2E : 0.f;
@@ -515,7 +544,7 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
     const float* L = ls + buf * BQT;
     const float* DL = ds + buf * BQT;
     const int qbase = qt * BQT;
-    const int kw0 = blockIdx.x * BKW + wave * 32;
+    const int kw0 = kblk * BKW + wave * 32;
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
       const int qb = qbase + qh * 32;
@@ -776,7 +805,7 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
   DNA_CHECK_ARG(out && lse, "dna_attn_fwd: null output");
   hipStream_t s = as_stream(stream);
   if (dtype == DNA_BF16) {
-    dim3 grid((seqlen + BQ - 1) / BQ, heads, batch);
+    dim3 grid(((seqlen + BQ - 1) / BQ) * heads * batch);
     hipLaunchKernelGGL(fwd_bf16_kernel, grid, dim3(256), FWD_LDS, s, (const bf16*)qkv, key_valid,
                        slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
   } else {
@@ -800,11 +829,11 @@ extern "C" int dna_attn_bwd(const void* qkv, const void* out, const void* dout, 
   const int nd = (rows * heads + 255) / 256;
   if (dtype == DNA_BF16) {
     // dQ kernel also produces delta = rowsum(dO*O), consumed by the dK/dV kernel after it
-    hipLaunchKernelGGL(dq_bf16_kernel, dim3((seqlen + BQ - 1) / BQ, heads, batch), dim3(256),
+    hipLaunchKernelGGL(dq_bf16_kernel, dim3(((seqlen + BQ - 1) / BQ) * heads * batch), dim3(256),
                        FWD_LDS, s, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
                        delta_ws, key_valid, slopes, seqlen, heads, softmax_scale * LOG2E,
                        softmax_scale, (bf16*)dqkv);
-    hipLaunchKernelGGL(dkdv_bf16_kernel, dim3((seqlen + BKW - 1) / BKW, heads, batch), dim3(256),
+    hipLaunchKernelGGL(dkdv_bf16_kernel, dim3(((seqlen + BKW - 1) / BKW) * heads * batch), dim3(256),
                        DKDV_LDS, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws, key_valid,
                        slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv);
   } else {
