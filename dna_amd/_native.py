@@ -41,6 +41,11 @@ _SIGS = {
     "dna_sum_slices_accum": (_i, [_vp, _i, _sz, _vp, _vp]),
     "dna_geglu_fwd": (_i, [_vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_geglu_bwd": (_i, [_vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
+    "dna_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
+    "dna_linear_dgrad": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
+    "dna_linear_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "dna_geglu_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
+    "dna_geglu_linear_dgrad": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_xent_fwd": (_i, [_vp, _i, _vp, _i, _i, _vp, _vp, _vp]),
     "dna_xent_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _f, _i, _i, _vp, _vp]),
     "dna_sumsq_workspace": (_sz, [_sz]),

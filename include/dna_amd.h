@@ -135,6 +135,31 @@ int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, float p_drop, u
 int dna_geglu_bwd(const void* da, const void* g, int dtype, int rows, int inter, float p_drop,
                   uint64_t seed, uint64_t offset, void* dg, void* stream);
 
+/* ------------------------------------------------------------------ projections (MFMA GEMM)
+ * The encoder's nn.Linear layers (bert_layers.py:158 Wqkv, :214 attention dense, :292
+ * gated_layers, :297 wo, :560 MLM transform) and their backward, bf16 in / fp32 accumulate.
+ * Row-major everywhere; w is the [N, K] nn.Linear weight (bf16 copy of the fp32 master).
+ *   fwd    y[M,N]  = x[M,K] . w^T + bias      (bias fp32 [N] or NULL; K % 64 == 0, N % 8 == 0)
+ *   dgrad  dx[M,K] = dy[M,N] . w             (N % 64 == 0, K % 8 == 0)
+ *   wgrad  partials[s][N][K] = dy[rows_s]^T . x[rows_s]  for s < splits over equal row slices
+ *          (M % (64*splits) == 0); reduce with dna_sum_slices_accum into the fp32 .grad. */
+int dna_linear_fwd(const void* x, const void* w, const float* bias, int M, int N, int K, void* y,
+                   void* stream);
+int dna_linear_dgrad(const void* dy, const void* w, int M, int N, int K, void* dx, void* stream);
+int dna_linear_wgrad(const void* dy, const void* x, int M, int N, int K, int splits,
+                     float* partials, void* stream);
+/* gated_layers + GeGLU + dropout in one launch (bert_layers.py:292-296):
+ *   g[M, 2F] = x[M,K] . wg^T + bias (bias fp32 [2F] or NULL),
+ *   out[M, F] = dropout(gelu_erf(g[:, :F]) * g[:, F:])   -- same Philox mask as dna_geglu_fwd.
+ * K % 64 == 0, F % 128 == 0. */
+int dna_geglu_linear_fwd(const void* x, const void* wg, const float* bias, int M, int F, int K,
+                         float p_drop, uint64_t seed, uint64_t offset, void* g, void* out,
+                         void* stream);
+/* wo dgrad + GeGLU backward in one launch: da = dy[M,N] . wo ([N, F]), then
+ * dg[M, 2F] = dna_geglu_bwd(da, g). N % 64 == 0, F % 8 == 0. */
+int dna_geglu_linear_dgrad(const void* dy, const void* wo, const void* g, int M, int F, int N,
+                           float p_drop, uint64_t seed, uint64_t offset, void* dg, void* stream);
+
 /* ------------------------------------------------------------------ masked-LM cross entropy
  * Per-row CE over the masked rows only (the model computes logits only for labels>0 rows,
  * bert_layers.py:795,:820-824; task loss bert_cross_entropy, src/tasks/metrics.py:268-273).

@@ -261,3 +261,65 @@ def test_embedding_grad_skewed_ids():
                                         (cols,), gm.detach(), bt.detach(), 1e-12)
     (yr * dy).sum().backward()
     assert (E.grad - E2.grad).abs().max().item() < 1e-3 * E2.grad.abs().max().item()
+
+
+# ------------------------------------------------------------------ MFMA GEMM (gemm.hip)
+def _gemm_call(name, *args):
+    from dna_amd import _native as N
+    N.call(name, *args, N.stream_ptr())
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm())
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 2304, 768), (1000, 768, 768), (512, 768, 3072),
+                                   (300, 4096, 768)])
+def test_gemm_linear_fwd_dgrad_wgrad(M, N, K):
+    """dna_linear_{fwd,dgrad,wgrad} vs fp32 torch on the same bf16 operands (bf16 rounding of
+    the output only: rel. Frobenius error < 1e-2; fp32 wgrad partials < 1e-5)."""
+    g = torch.Generator(device="cpu").manual_seed(N + K)
+    x = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV).bfloat16()
+    b = torch.randn(N, generator=g).to(DEV)
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_linear_fwd", x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, y.data_ptr())
+    assert _rel(y, x.float() @ w.float().t() + b) < 1e-2
+    dy = torch.randn(M, N, generator=g).to(DEV).bfloat16()
+    dx = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_linear_dgrad", dy.data_ptr(), w.data_ptr(), M, N, K, dx.data_ptr())
+    assert _rel(dx, dy.float() @ w.float()) < 1e-2
+    if M % 128 == 0:
+        s = 2
+        part = torch.empty(s, N, K, device=DEV)
+        _gemm_call("dna_linear_wgrad", dy.data_ptr(), x.data_ptr(), M, N, K, s, part.data_ptr())
+        assert _rel(part.sum(0), dy.float().t() @ x.float()) < 1e-5
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_geglu_fused_equals_unfused(p):
+    """Fused gated_layers+GeGLU fwd and wo-dgrad+GeGLU bwd give bit-identical results to the
+    unfused kernels on the GEMM outputs (same Philox dropout mask)."""
+    M, H, F = 1024, 768, 3072
+    g0 = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(M, H, generator=g0).to(DEV).bfloat16()
+    wg = (torch.randn(2 * F, H, generator=g0) * 0.05).to(DEV).bfloat16()
+    bg = (torch.randn(2 * F, generator=g0) * 0.1).to(DEV)
+    g = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    a = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_geglu_linear_fwd", x.data_ptr(), wg.data_ptr(), bg.data_ptr(), M, F, H, p, 11, 5,
+               g.data_ptr(), a.data_ptr())
+    assert _rel(g, x.float() @ wg.float().t() + bg) < 1e-2
+    a2 = torch.empty_like(a)
+    _gemm_call("dna_geglu_fwd", g.data_ptr(), 1, M, F, p, 11, 5, a2.data_ptr())
+    assert torch.equal(a, a2)
+    dy = torch.randn(M, H, generator=g0).to(DEV).bfloat16()
+    wo = (torch.randn(H, F, generator=g0) * 0.05).to(DEV).bfloat16()
+    dg = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_geglu_linear_dgrad", dy.data_ptr(), wo.data_ptr(), g.data_ptr(), M, F, H, p, 11, 5,
+               dg.data_ptr())
+    da = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_linear_dgrad", dy.data_ptr(), wo.data_ptr(), M, H, F, da.data_ptr())
+    dg2 = torch.empty_like(dg)
+    _gemm_call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, M, F, p, 11, 5, dg2.data_ptr())
+    assert torch.equal(dg, dg2)
