@@ -38,6 +38,20 @@ PEAK_HBM_GBS = 8000.0
 TRAIN_FLOP_PER_SEQ = 3.586e11  # 3 x fwd FLOPs at S=512 incl. last-layer subset
 
 
+def load_traffic():
+    """HBM bytes per launch of each timed op family from the newest profiles/r*/traffic.json
+    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench, FETCH_SIZE doubled per the
+    gfx950 correction; scripts/traffic_from_pmc.py). {} when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")))
+    if not files:
+        return {}
+    with open(files[-1]) as f:
+        d = json.load(f)
+    rel = os.path.relpath(files[-1], ROOT)
+    return {k: dict(v, source=rel) for k, v in d.get("families", {}).items()}
+
+
 def make_batches(n_batches, batch, rank, device):
     from dna_amd.hg38 import bert_mask_fast
     from dna_amd.synthetic import random_windows
@@ -163,18 +177,34 @@ def main():
     roofline, kernels = None, {}
     if timer:
         summ = timer.summary()
-        total_ms = {k: n * ms for k, (n, ms, u) in summ.items()}
-        for k, (n, ms, units) in summ.items():
-            tf = units / (ms * 1e-3) / 1e12
+        total_ms = {k: v[0] * v[1] for k, v in summ.items()}
+        traffic = load_traffic()
+        for k, (n, ms, units, kind) in summ.items():
+            rate = units / (ms * 1e-3)
             kernels[k] = {"launches_per_step": n / args.steps, "avg_ms": round(ms, 4),
-                          "share_of_step": round(total_ms[k] / (elapsed * 1e3), 4),
-                          "achieved_tflops": round(tf, 1)}
+                          "share_of_step": round(total_ms[k] / (elapsed * 1e3), 4)}
+            if kind == "flop":
+                kernels[k].update(bound="mfma", achieved_tflops=round(rate / 1e12, 1),
+                                  frac=round(rate / 1e12 / PEAK_BF16_TFLOPS, 4))
+            else:
+                kernels[k].update(bound="hbm", achieved_gbs=round(rate / 1e9, 1),
+                                  frac=round(rate / 1e9 / PEAK_HBM_GBS, 4))
+            if k in traffic:
+                kernels[k]["traffic"] = traffic[k]["bytes_per_launch"]
         dom = max(total_ms, key=total_ms.get)
-        n, ms, units = summ[dom]
-        ach = units / (ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 1),
-                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None}
+        n, ms, units, kind = summ[dom]
+        rate = units / (ms * 1e-3)
+        if kind == "flop":
+            roofline = {"bound": "mfma", "achieved": round(rate / 1e12, 1), "peak": PEAK_BF16_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(rate / 1e12 / PEAK_BF16_TFLOPS, 4)}
+        else:
+            roofline = {"bound": "hbm", "achieved": round(rate / 1e9, 1), "peak": PEAK_HBM_GBS,
+                        "unit": "GB/s", "frac": round(rate / 1e9 / PEAK_HBM_GBS, 4)}
+        roofline["traffic"] = traffic.get(dom, {}).get("bytes_per_launch")
+        roofline["kernel"] = dom
+        roofline["algorithmic_per_launch"] = units
+        if dom in traffic:
+            roofline["traffic_source"] = traffic[dom]["source"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

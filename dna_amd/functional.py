@@ -47,19 +47,20 @@ class OpTimer:
         OpTimer.active = None
 
     def summary(self):
-        """{name: (launches, mean_ms, units_per_launch)} after a device synchronize."""
+        """{name: (launches, mean_ms, units_per_launch, kind)} after a device synchronize;
+        kind "flop" (MFMA-bound: algorithmic FLOPs) or "byte" (HBM-bound: algorithmic bytes)."""
         acc = {}
-        for name, units, a, b in self.pending:
-            n, t, u = acc.get(name, (0, 0.0, 0.0))
-            acc[name] = (n + 1, t + a.elapsed_time(b), u + units)
-        return {k: (n, t / n, u / n) for k, (n, t, u) in acc.items()}
+        for name, units, kind, a, b in self.pending:
+            n, t, u, _ = acc.get(name, (0, 0.0, 0.0, kind))
+            acc[name] = (n + 1, t + a.elapsed_time(b), u + units, kind)
+        return {k: (n, t / n, u / n, kind) for k, (n, t, u, kind) in acc.items()}
 
 
 class _timed:
-    __slots__ = ("name", "units", "t", "a")
+    __slots__ = ("name", "units", "kind", "t", "a")
 
-    def __init__(self, name, units):
-        self.name, self.units, self.t = name, units, OpTimer.active
+    def __init__(self, name, units, kind="flop"):
+        self.name, self.units, self.kind, self.t = name, units, kind, OpTimer.active
 
     def __enter__(self):
         if self.t is not None:
@@ -70,7 +71,7 @@ class _timed:
         if self.t is not None:
             b = torch.cuda.Event(enable_timing=True)
             b.record()
-            self.t.pending.append((self.name, self.units, self.a, b))
+            self.t.pending.append((self.name, self.units, self.kind, self.a, b))
 
 
 class DropoutRNG:
@@ -152,9 +153,13 @@ class FusedLayerNorm(torch.autograd.Function):
         mean = torch.empty(n, device=x.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         residual = None if residual is None else residual.contiguous()
-        N.call("dna_ln_fwd", x.data_ptr(), _dt(x), _p(bias), act, p, seed, off, _p(residual),
-               gamma.data_ptr(), beta.data_ptr(), n, d, eps, _p(y), _p(yb), mean.data_ptr(),
-               rstd.data_ptr(), N.stream_ptr())
+        es = x.element_size()
+        nbytes = n * (d * (es + (4 if residual is not None else 0) + (4 if want_f32 else 0)
+                           + (2 if want_bf16 else 0)) + 8)
+        with _timed("ln_fwd", nbytes, "byte"):
+            N.call("dna_ln_fwd", x.data_ptr(), _dt(x), _p(bias), act, p, seed, off, _p(residual),
+                   gamma.data_ptr(), beta.data_ptr(), n, d, eps, _p(y), _p(yb), mean.data_ptr(),
+                   rstd.data_ptr(), N.stream_ptr())
         ctx.save_for_backward(x, bias, residual, gamma, mean, rstd)
         ctx.cfg = (act, p, seed, off)
         return y, yb
@@ -173,10 +178,14 @@ class FusedLayerNorm(torch.autograd.Function):
         ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
         dy = None if dy is None else dy.contiguous()
         dyb = None if dyb is None else dyb.contiguous()
-        N.call("dna_ln_bwd", _p(dy), _p(dyb), x.data_ptr(), _dt(x), _p(bias), act, p, seed, off,
-               _p(residual), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, d, _p(dres),
-               dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _p(dbias), ws.data_ptr(), nws,
-               N.stream_ptr())
+        es = x.element_size()
+        nbytes = n * (d * ((4 if dy is not None else 0) + (2 if dyb is not None else 0) + 2 * es
+                           + (4 if residual is not None else 0)) + 8)
+        with _timed("ln_bwd", nbytes, "byte"):
+            N.call("dna_ln_bwd", _p(dy), _p(dyb), x.data_ptr(), _dt(x), _p(bias), act, p, seed,
+                   off, _p(residual), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, d,
+                   _p(dres), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _p(dbias), ws.data_ptr(),
+                   nws, N.stream_ptr())
         return dx, dbias, dres, dg, db, None, None, None, None, None, None, None
 
 
@@ -229,8 +238,9 @@ class GeGLU(torch.autograd.Function):
         g = g.contiguous()
         n, F2 = g.shape
         a = torch.empty(n, F2 // 2, device=g.device, dtype=g.dtype)
-        N.call("dna_geglu_fwd", g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off, a.data_ptr(),
-               N.stream_ptr())
+        with _timed("geglu_fwd", n * F2 // 2 * 3 * g.element_size(), "byte"):
+            N.call("dna_geglu_fwd", g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off, a.data_ptr(),
+                   N.stream_ptr())
         ctx.save_for_backward(g)
         ctx.cfg = (p, seed, off)
         return a
@@ -242,8 +252,9 @@ class GeGLU(torch.autograd.Function):
         n, F2 = g.shape
         dg = torch.empty_like(g)
         da = da.contiguous()
-        N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off,
-               dg.data_ptr(), N.stream_ptr())
+        with _timed("geglu_bwd", n * F2 // 2 * 5 * g.element_size(), "byte"):
+            N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off,
+                   dg.data_ptr(), N.stream_ptr())
         return dg, None, None, None
 
 

@@ -1,0 +1,82 @@
+#!/usr/bin/env python
+"""HBM traffic per op launch from two rocprofv3 --pmc passes over the same bench command.
+
+    python scripts/traffic_from_pmc.py FETCH_DIR WRITE_DIR OUT.json
+
+FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB per dispatch. Per
+MI355X_MICROARCH.md (HBM section) FETCH_SIZE reports exactly half the bytes of 16-B/lane
+streaming reads on gfx950, so it is doubled; WRITE_SIZE is taken as is. Both count
+Infinity-Cache (MALL) hits as well as HBM. Kernels are grouped into the op families bench.py
+times (dna_amd.functional._timed names); bytes_per_launch = family bytes / op launches."""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+# family -> (regex selecting its kernels, regex selecting the one kernel counted per op launch)
+FAMILIES = {
+    "gemm": (r"Cijk_|sum_slices_kernel", r"Cijk_"),
+    "attn_fwd": (r"attn::fwd_bf16_kernel|attn4fwd_bf16", r"attn::fwd_bf16_kernel|attn4fwd_bf16"),
+    "attn_bwd": (r"attn::(dq|dkdv)_bf16_kernel|attn(2dq|4dkdv)_bf16", r"attn::dq_bf16_kernel|attn2dq_bf16"),
+    "geglu_fwd": (r"geglu10fwd_kernel|geglu::fwd_kernel", r"geglu10fwd_kernel|geglu::fwd_kernel"),
+    "geglu_bwd": (r"geglu10bwd_kernel|geglu::bwd_kernel", r"geglu10bwd_kernel|geglu::bwd_kernel"),
+    "ln_fwd": (r"2ln10fwd_kernel|ln::fwd_kernel", r"2ln10fwd_kernel|ln::fwd_kernel"),
+    "ln_bwd": (r"2ln10bwd_kernel|ln::bwd_kernel|ln::reduce_partials|2ln15reduce_partials",
+               r"2ln10bwd_kernel|ln::bwd_kernel"),
+}
+
+
+def per_dispatch(path, counter):
+    """{dispatch_id: (kernel_name, value)} summed over the rows of one dispatch."""
+    out = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter:
+                continue
+            d = row["Dispatch_Id"]
+            name, v = out.get(d, (row["Kernel_Name"], 0.0))
+            out[d] = (name, v + float(row["Counter_Value"]))
+    return out
+
+
+def families(disp, scale):
+    tot = collections.defaultdict(float)
+    cnt = collections.Counter()
+    for name, v in disp.values():
+        for fam, (sel, one) in FAMILIES.items():
+            if re.search(sel, name):
+                tot[fam] += v * scale
+                if re.search(one, name):
+                    cnt[fam] += 1
+    return tot, cnt
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    fetch = per_dispatch(os.path.join(fdir, "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_dispatch(os.path.join(wdir, "run_counter_collection.csv"), "WRITE_SIZE")
+    ft, fc = families(fetch, 2 * 1024.0)   # KiB, x2 gfx950 FETCH_SIZE correction
+    wt, wc = families(write, 1024.0)
+    res = {}
+    for fam in FAMILIES:
+        n = fc.get(fam) or wc.get(fam)
+        if not n:
+            continue
+        res[fam] = {"bytes_per_launch": int((ft[fam] / fc[fam] if fc.get(fam) else 0)
+                                            + (wt[fam] / wc[fam] if wc.get(fam) else 0)),
+                    "read_bytes_per_launch": int(ft[fam] / fc[fam]) if fc.get(fam) else None,
+                    "write_bytes_per_launch": int(wt[fam] / wc[fam]) if wc.get(fam) else None,
+                    "launches_profiled": int(n)}
+    doc = {"method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate "
+                     "passes) over `python bench.py --steps 6 --warmup 2 --no-cpu-baseline`; "
+                     "FETCH_SIZE x2 (gfx950 correction), KiB->bytes; includes Infinity-Cache hits",
+           "families": res}
+    with open(out, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    main()
