@@ -342,20 +342,34 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(EmbBwdArgs a) {
   block_partials<NV, VEC>(acc_g, acc_b, acc_t, a.cols, a.part);
 }
 
-// sum partials over blocks: out_q[c] = sum_b part[b][q][c]. Block = 64 columns x 4 row
-// groups (coalesced 256-B rows), fixed summation order (deterministic).
-__global__ __launch_bounds__(256) void reduce_partials(const float* __restrict__ part, int nblocks,
-                                                       int cols, float* o0, float* o1, float* o2) {
-  __shared__ float red[4][64];
+// sum partials over blocks: out_q[c] = sum_b part[b][q][c]. Block = 64 columns x 16 row
+// groups (coalesced 256-B rows), 8 independent loads in flight per thread, fixed summation
+// order (deterministic).
+constexpr int RP_GROUPS = 16;
+__global__ __launch_bounds__(64 * RP_GROUPS) void reduce_partials(const float* __restrict__ part,
+                                                                  int nblocks, int cols,
+                                                                  float* o0, float* o1, float* o2) {
+  __shared__ float red[RP_GROUPS][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + tx;
+  const size_t ld = (size_t)3 * cols;
   float s = 0.f;
-  if (i < 3 * cols)
-    for (int b = ty; b < nblocks; b += 4) s += part[(size_t)b * 3 * cols + i];
+  if (i < 3 * cols) {
+    float v[8];
+    int b = ty;
+    for (; b + 7 * RP_GROUPS < nblocks; b += 8 * RP_GROUPS) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + u * RP_GROUPS) * ld + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < nblocks; b += RP_GROUPS) s += part[(size_t)b * ld + i];
+  }
   red[ty][tx] = s;
   __syncthreads();
   if (ty == 0 && i < 3 * cols) {
-    s = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+#pragma unroll
+    for (int g = 1; g < RP_GROUPS; ++g) s += red[g][tx];
     const int q = i / cols, c = i % cols;
     float* o = q == 0 ? o0 : (q == 1 ? o1 : o2);
     if (o) o[c] = s;
@@ -452,7 +466,7 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
       hipLaunchKernelGGL((bwd_kernel<float, NV, VEC>), dim3(nb), dim3(256), lds, s, a);
   });
   if (st) return st;
-  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(256), 0, s,
+  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
                      (const float*)workspace, nb, cols, dgamma, dbeta, dbias);
   DNA_LAUNCH_CHECK("dna_ln_bwd");
   return DNA_OK;
@@ -507,7 +521,7 @@ static int embed_ln_bwd_impl(const float* dy, const void* dy_bf16, const int64_t
   });
   if (st) return st;
   // partial slots: 0 dgamma, 1 dbeta, 2 d(type_row)
-  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(256), 0, s,
+  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
                      (const float*)workspace, nb, cols, dgamma, dbeta, dtype_row);
   DNA_LAUNCH_CHECK("dna_embed_ln_bwd");
   return DNA_OK;
