@@ -1,0 +1,87 @@
+"""GPU: the HIP FFT long convolution (dna_amd.hyena.fftconv) against the reference fixtures
+(fftconv_ref outputs/grads in fp64) and the numpy oracle at HyenaDNA sizes (L = 65536).
+Tolerances: fp32 in/out -- relative max error 2e-5 of the output scale (fp32 FFT of size 2L);
+bf16 in/out -- 1e-2 (bf16 rounding of inputs and outputs)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hyena_ref as H
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "fftconv_golden.npz")
+
+
+def _cases():
+    z = np.load(GOLD)
+    for c in range(int(z["ncases"])):
+        p = f"c{c}_"
+        B, D, L, bi = (int(v) for v in z[p + "shape"])
+        yield c, B, D, L, bool(bi), {k[len(p):]: z[k] for k in z.files if k.startswith(p)}
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+@pytest.mark.parametrize("case", list(_cases()), ids=lambda c: f"c{c[0]}_B{c[1]}D{c[2]}L{c[3]}bi{int(c[4])}")
+def test_fftconv_matches_reference_fixture(case):
+    from dna_amd.hyena import fftconv
+    _, B, D, L, bi, f = case
+    u = torch.tensor(f["u"], device=DEV, requires_grad=True)          # [B,1,D,1,L] as HyenaOperator
+    k = torch.tensor(f["k"], device=DEV, requires_grad=True)
+    bias = torch.tensor(f["bias"], device=DEV, requires_grad=True)    # [1,D,1]
+    y = fftconv(u, k, bias, bidirectional=bi)
+    assert y.shape == u.shape and y.dtype == u.dtype
+    assert _rel(y.detach().cpu(), f["y64"]) < 2e-5
+    y.backward(torch.tensor(f["dy"], device=DEV))
+    assert _rel(u.grad.cpu(), f["du"]) < 2e-5
+    assert _rel(k.grad.cpu(), f["dk"]) < 2e-5
+    assert _rel(bias.grad.cpu(), f["dbias"]) < 2e-5
+
+
+@pytest.mark.parametrize("bi", [False, True])
+def test_fftconv_hyena_size_vs_oracle(bi):
+    """L = 65536 (BASELINE config D length), odd batch (an unpaired row), fp32 and bf16."""
+    from dna_amd.hyena import fftconv
+    B, D, L = 3, 2, 65536
+    g = torch.Generator().manual_seed(3)
+    u = torch.randn(B, D, L, generator=g)
+    k = torch.randn(D, L, generator=g) * torch.exp(-torch.linspace(0, 6, L))[None]
+    bias = torch.randn(D, 1, generator=g)
+    ref = H.fftconv_fwd(u.numpy(), k.numpy(), bias.numpy(), bi)
+    y = fftconv(u.to(DEV), k.to(DEV), bias.to(DEV), bidirectional=bi)
+    assert _rel(y.cpu(), ref) < 2e-5
+    yb = fftconv(u.to(DEV).bfloat16(), k.to(DEV), bias.to(DEV), bidirectional=bi)
+    assert yb.dtype == torch.bfloat16 and _rel(yb.float().cpu(), ref) < 1e-2
+    dy = torch.randn(B, D, L, generator=g)
+    du, dk, db = H.fftconv_bwd(dy.numpy(), u.numpy(), k.numpy(), bias.numpy(), bi)
+    ut = u.to(DEV).requires_grad_(True)
+    kt = k.to(DEV).requires_grad_(True)
+    bt = bias.to(DEV).requires_grad_(True)
+    fftconv(ut, kt, bt, bidirectional=bi).backward(dy.to(DEV))
+    assert _rel(ut.grad.cpu(), du) < 2e-5
+    assert _rel(kt.grad.cpu(), dk) < 5e-5
+    assert _rel(bt.grad.cpu(), db) < 2e-5
+
+
+def test_fftconv_linearity_and_errors():
+    from dna_amd.hyena import fftconv
+    g = torch.Generator().manual_seed(5)
+    u1, u2 = torch.randn(2, 4, 1024, generator=g).to(DEV), torch.randn(2, 4, 1024, generator=g).to(DEV)
+    k = torch.randn(4, 1024, generator=g).to(DEV)
+    b = torch.zeros(4, device=DEV)
+    lhs = fftconv(2.0 * u1 - 3.0 * u2, k, b)
+    rhs = 2.0 * fftconv(u1, k, b) - 3.0 * fftconv(u2, k, b)
+    assert (lhs - rhs).abs().max().item() < 1e-4 * rhs.abs().max().item()
+    with pytest.raises(NotImplementedError):
+        fftconv(u1, k, b, gelu=True)
+    with pytest.raises(Exception):
+        fftconv(u1[..., :1000], k[..., :1000], b)  # L not a power of 2
+    with pytest.raises(RuntimeError):
+        fftconv(u1.cpu(), k.cpu(), b.cpu())       # GPU only, no fallback
