@@ -5,18 +5,21 @@
 // for rows r = (b, d) of u [B, D, L]; u~ is u zero-padded to N (causal: at offset 0,
 // bidirectional: at offset pad_before = L/2 -- the reference's F.pad then rfft(n=2L)).
 //
-// Layout and passes. N = M1 * M2 (M2 = 256 for N >= 512, M1 <= 1024). Two rows with the same
+// Layout and passes. N = M1 * M2 (M2 = 512 for N >= 1024, M1 <= 512). Two rows with the same
 // filter (batches b, b+1 of channel d) are packed into ONE complex sequence z = u~_b + i u~_{b+1};
 // since the filter is real, IFFT(Z * K) = (u~_b * k) + i (u~_{b+1} * k) -- no separation step.
 // With n = n1*M2 + n2 and k = k1 + M1*k2 (four-step / Bailey):
-//   A  column pass: for each column n2, FFT-M1 over n1 (LDS-staged, CW columns per block so the
-//      global reads/writes are CW*8-byte row segments), times W_N^(n2*k1) -> T[k1][n2]
+//   A  column pass: for each column n2, FFT-M1 over n1 (LDS-staged, 8192/M1 columns per block so
+//      the global reads/writes are row segments of 32 columns at M1 = 256), times W_N^(n2*k1)
+//      -> T[k1][n2]
 //   B  row pass:    for each row k1, FFT-M2 over n2 -> spectrum Z[k1 + M1*k2], times the filter
 //      spectrum (stored in the same [k1][k2] order, 1/N folded in), inverse FFT-M2 -> T'[k1][n2]
 //   C  column pass: times W_N^-(n2*k1), inverse FFT-M1 over k1 -> z[n1*M2 + n2]; epilogue adds
 //      bias*u and writes rows b, b+1 (real, imaginary part) for t < L.
-// FFTs are radix-2 in LDS with an LDS twiddle table (W_M^m, m < M/2, from sincospi); the
-// inter-pass twiddles W_N^(n2*k1) come from sincospi of an exactly-representable argument.
+// FFTs are autosort Stockham passes in LDS with radix-8/4/2 register butterflies (16 points per
+// thread per pass) and an LDS twiddle table W_M^m; the inter-pass twiddles W_N^(n2*k1) come
+// from a two-level LDS table (W_N^(m & 511) * W_N^(512*(m >> 9))), all built with sincospi of
+// exactly representable arguments.
 // Backward: du runs the same three passes on dy (offset 0) with conj(K) and reads the output at
 // offset pad_before; dk = Re IFFT(sum_pairs conj(Z_u) Z_dy) / N (the packed pair's cross terms are
 // purely imaginary after the inverse transform), j < L; dbias = sum_{b,t} dy u.
@@ -44,57 +47,149 @@ __device__ __forceinline__ cf twiddle(uint32_t m, int logN) {
   return make_float2(c, s);
 }
 
-__device__ __forceinline__ int brev(int i, int bits) { return (int)(__brev((unsigned)i) >> (32 - bits)); }
+// ------------------------------------------------------------------ register butterflies
+// multiply by W_4^1 = -i (forward) / +i (inverse)
+template <bool INV> __device__ __forceinline__ cf mul_w4(cf a) {
+  return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+}
+// multiply by W_8^1 = (1 -/+ i)/sqrt(2)
+template <bool INV> __device__ __forceinline__ cf mul_w8(cf a) {
+  const float r = 0.70710678118654752f;
+  return INV ? make_float2((a.x - a.y) * r, (a.x + a.y) * r) : make_float2((a.x + a.y) * r, (a.y - a.x) * r);
+}
+template <bool INV> __device__ __forceinline__ void dft2(cf* x) {
+  const cf t = x[0];
+  x[0] = cadd(t, x[1]);
+  x[1] = csub(t, x[1]);
+}
+template <bool INV> __device__ __forceinline__ void dft4(cf* x) {
+  const cf a0 = cadd(x[0], x[2]), a1 = csub(x[0], x[2]);
+  const cf a2 = cadd(x[1], x[3]), a3 = mul_w4<INV>(csub(x[1], x[3]));
+  x[0] = cadd(a0, a2);
+  x[2] = csub(a0, a2);
+  x[1] = cadd(a1, a3);
+  x[3] = csub(a1, a3);
+}
+template <bool INV> __device__ __forceinline__ void dft8(cf* x) {
+  cf e[4] = {x[0], x[2], x[4], x[6]}, o[4] = {x[1], x[3], x[5], x[7]};
+  dft4<INV>(e);
+  dft4<INV>(o);
+  o[1] = mul_w8<INV>(o[1]);
+  o[2] = mul_w4<INV>(o[2]);
+  o[3] = mul_w4<INV>(mul_w8<INV>(o[3]));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    x[k] = cadd(e[k], o[k]);
+    x[k + 4] = csub(e[k], o[k]);
+  }
+}
+template <int R, bool INV> __device__ __forceinline__ void dft(cf* x) {
+  if constexpr (R == 8) dft8<INV>(x);
+  else if constexpr (R == 4) dft4<INV>(x);
+  else dft2<INV>(x);
+}
 
-// LDS twiddle table tw[m] = W_M^m, m < M/2.
+// ------------------------------------------------------------------ LDS Stockham FFT
+// A block transforms G sequences of length M = 2^logM held in LDS at buf[g*S + i], with
+// G*M = PTS points (PTS/NTH = 16 per thread per pass, whatever the radix). Autosort Stockham
+// (Govindaraju et al. 2008): natural order in and out, in place (each pass reads its 16
+// points into registers, barrier, writes them, barrier). Twiddles from the LDS table
+// twM[m] = W_M^m (m < M). Unscaled; INV conjugates all twiddles.
+constexpr int NTH = 512;
+constexpr int PTS = 8192;
+constexpr int PPT = PTS / NTH;  // points per thread per pass
+// 8 waves per block, 2 blocks per CU (LDS ~78 KB each): 4 waves per SIMD, <= 128 VGPRs.
+#define FFT_BOUNDS __launch_bounds__(NTH, 4)  // HIP: 2nd argument = min waves per SIMD
+
+// LDS address of point i of sequence g: one pad slot every 16 points (the stride-R writes of
+// the first Stockham passes then spread over all banks) and a caller-chosen sequence stride S.
+__device__ __forceinline__ int lds_at(int g, int i, int S) { return g * S + i + (i >> 4); }
+// sequence stride for length M: padded length (+1 for column buffers, whose transposing
+// global<->LDS copies walk across sequences)
+__host__ __device__ __forceinline__ int seq_stride(int logM, bool col) {
+  return (1 << logM) + ((1 << logM) >> 4) + (col ? 1 : 0);
+}
+
+template <int R, int LOGR, bool INV>
+__device__ __forceinline__ void stockham_pass(cf* buf, int G, int logM, int S, int logNs, const cf* twM) {
+  constexpr int IPT = PPT / R;  // butterflies per thread
+  const int M = 1 << logM;
+  const int lognbf = logM - LOGR;
+  const int items = G << lognbf;
+  const int Ns = 1 << logNs;
+  const int logtstep = logM - logNs - LOGR;
+  cf x[IPT][R];
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    const int w = threadIdx.x + it * NTH;
+    if (w < items) {
+      const int g = w >> lognbf, j = w & ((1 << lognbf) - 1);
+      const int k = j & (Ns - 1);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        cf v = buf[lds_at(g, j + (r << lognbf), S)];
+        if (r > 0 && logNs > 0) {
+          cf t = twM[((r * k) << logtstep) & (M - 1)];
+          if (INV) t.y = -t.y;
+          v = cmul(v, t);
+        }
+        x[it][r] = v;
+      }
+      dft<R, INV>(x[it]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    const int w = threadIdx.x + it * NTH;
+    if (w < items) {
+      const int g = w >> lognbf, j = w & ((1 << lognbf) - 1);
+      const int k = j & (Ns - 1);
+      const int base = ((j - k) << LOGR) + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) buf[lds_at(g, base + (r << logNs), S)] = x[it][r];
+    }
+  }
+  __syncthreads();
+}
+
+template <bool INV>
+__device__ void fft_lds(cf* buf, int G, int logM, int S, const cf* twM) {
+  int logNs = 0, left = logM;
+  while (left >= 3) {
+    stockham_pass<8, 3, INV>(buf, G, logM, S, logNs, twM);
+    logNs += 3;
+    left -= 3;
+  }
+  if (left == 2) stockham_pass<4, 2, INV>(buf, G, logM, S, logNs, twM);
+  else if (left == 1) stockham_pass<2, 1, INV>(buf, G, logM, S, logNs, twM);
+}
+
+// LDS twiddle table tw[m] = W_M^m, m < M.
 __device__ __forceinline__ void make_table(cf* tw, int logM) {
-  const int half = 1 << (logM - 1);
-  for (int m = threadIdx.x; m < half; m += blockDim.x) tw[m] = twiddle(m, logM);
+  const int M = 1 << logM;
+  for (int m = threadIdx.x; m < M; m += blockDim.x) tw[m] = twiddle(m, logM);
 }
 
-// G independent in-place radix-2 FFTs of length M = 2^logM on buf[g*stride + i].
-// DIT: input in bit-reversed order, output natural. INV uses conj twiddles (unscaled).
-template <bool INV>
-__device__ void fft_dit(cf* buf, int G, int logM, const cf* tw, int stride) {
-  const int M = 1 << logM, halfM = M >> 1;
-  const int nb = G * halfM;
-  for (int s = 0; s < logM; ++s) {
-    const int h = 1 << s;
-    const int tstep = logM - 1 - s;  // twiddle index = pos << tstep
-    for (int idx = threadIdx.x; idx < nb; idx += blockDim.x) {
-      const int g = idx >> (logM - 1), j = idx & (halfM - 1);
-      const int pos = j & (h - 1), grp = j >> s;
-      const int i0 = g * stride + (grp << (s + 1)) + pos, i1 = i0 + h;
-      cf w = tw[pos << tstep];
-      if (INV) w.y = -w.y;
-      const cf a = buf[i0], b = cmul(buf[i1], w);
-      buf[i0] = cadd(a, b);
-      buf[i1] = csub(a, b);
-    }
-    __syncthreads();
+// Two-level table for W_N^m, m < N <= 2^18: lo[m & (2^lb - 1)] * hi[m >> lb], lb = logN/2.
+struct BigTwiddle {
+  cf* lo;  // [2^lb]
+  cf* hi;  // [2^(logN - lb)]
+  int lb;
+  __device__ __forceinline__ void init(int logN) {
+    lb = logN >> 1;
+    hi = lo + (1 << lb);
+    const uint32_t mask = (1u << logN) - 1;
+    for (int m = threadIdx.x; m < (1 << lb); m += blockDim.x) lo[m] = twiddle((uint32_t)m, logN);
+    for (int m = threadIdx.x; m < (1 << (logN - lb)); m += blockDim.x)
+      hi[m] = twiddle(((uint32_t)m << lb) & mask, logN);
   }
-}
-
-// DIF: input natural order, output bit-reversed.
-template <bool INV>
-__device__ void fft_dif(cf* buf, int G, int logM, const cf* tw, int stride) {
-  const int M = 1 << logM, halfM = M >> 1;
-  const int nb = G * halfM;
-  for (int s = logM - 1; s >= 0; --s) {
-    const int h = 1 << s;
-    const int tstep = logM - 1 - s;
-    for (int idx = threadIdx.x; idx < nb; idx += blockDim.x) {
-      const int g = idx >> (logM - 1), j = idx & (halfM - 1);
-      const int pos = j & (h - 1), grp = j >> s;
-      const int i0 = g * stride + (grp << (s + 1)) + pos, i1 = i0 + h;
-      cf w = tw[pos << tstep];
-      if (INV) w.y = -w.y;
-      const cf a = buf[i0], b = buf[i1];
-      buf[i0] = cadd(a, b);
-      buf[i1] = cmul(csub(a, b), w);
-    }
-    __syncthreads();
+  __device__ __forceinline__ cf operator()(uint32_t m) const {
+    return cmul(lo[m & ((1u << lb) - 1)], hi[m >> lb]);
   }
+};
+__host__ __device__ __forceinline__ int big_twiddle_elems(int logN) {
+  return (1 << (logN >> 1)) + (1 << (logN - (logN >> 1)));
 }
 
 template <typename T> __device__ __forceinline__ float ld(const T* p, size_t i) { return to_f32(p[i]); }
@@ -114,46 +209,64 @@ struct Geo {
   int L, logN, logM1, logM2;  // N = 2L = M1 * M2
 };
 
-constexpr int CW = 16;      // columns per block in the column passes
-constexpr int NTH = 256;
+// Column passes: G = PTS / M1 columns per block (16 at M1 = 512), column stride M1 + 1 (the
+// transposing global<->LDS copies then spread over the banks). Row pass: G = PTS / M2 rows.
+__host__ __device__ __forceinline__ int log_col_group(const Geo& g) {
+  return (13 - g.logM1) < g.logM2 ? (13 - g.logM1) : g.logM2;  // log2(min(PTS/M1, M2)), PTS = 2^13
+}
+__host__ __device__ __forceinline__ int log_row_group(const Geo& g) {
+  return (13 - g.logM2) < g.logM1 ? (13 - g.logM2) : g.logM1;      // log2(min(PTS/M2, M1))
+}
 
 // ---------------------------------------------------------------- A: column FFT over n1
 // src rows [.][L] (dtype T); z[n] = x_a[n - off] + i x_b[n - off] (zero outside [0, L)).
 template <typename T>
-__global__ __launch_bounds__(NTH) void col_fwd_kernel(const T* __restrict__ x, Pairing pr, Geo g,
+__global__ FFT_BOUNDS void col_fwd_kernel(const T* __restrict__ x, Pairing pr, Geo g,
                                                       int off, cf* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M1 = 1 << g.logM1, M2 = 1 << g.logM2;
-  const int cw = min(CW, M2);
-  const int S = M1 + 1;                    // padded column stride (bank spread)
-  cf* buf = reinterpret_cast<cf*>(smem);  // [cw][S]
-  cf* tw = buf + cw * S;                   // [M1/2]
+  const int lcw = log_col_group(g), cw = 1 << lcw;
+  const int S = seq_stride(g.logM1, true);
+  cf* buf = reinterpret_cast<cf*>(smem);  // [cw][S] padded
+  cf* tw = buf + cw * S;                   // [M1]
+  BigTwiddle bt{tw + M1};
   const int n20 = blockIdx.x * cw;
   const int p = blockIdx.y;
   int d, ra, rb;
   pr.rows(p, d, ra, rb);
   make_table(tw, g.logM1);
+  bt.init(g.logN);
   const T* xa = x + (size_t)ra * g.L;
   const T* xb = rb >= 0 ? x + (size_t)rb * g.L : nullptr;
-  for (int e = threadIdx.x; e < cw * M1; e += NTH) {
-    const int n1 = e / cw, c = e - n1 * cw;
-    const int i = n1 * M2 + n20 + c - off;
-    cf v = make_float2(0.f, 0.f);
-    if (i >= 0 && i < g.L) {
-      v.x = ld(xa, i);
-      if (xb) v.y = ld(xb, i);
+  {
+    // all PPT loads in flight before the LDS stores (a plain strided loop serialises them)
+    cf v[PPT];
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      const int n1 = e >> lcw, c = e & (cw - 1);
+      const int i = n1 * M2 + n20 + c - off;
+      v[it] = make_float2(0.f, 0.f);
+      if (e < cw * M1 && i >= 0 && i < g.L) {
+        v[it].x = ld(xa, i);
+        if (xb) v[it].y = ld(xb, i);
+      }
     }
-    buf[c * S + brev(n1, g.logM1)] = v;
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      const int n1 = e >> lcw, c = e & (cw - 1);
+      if (e < cw * M1) buf[lds_at(c, n1, S)] = v[it];
+    }
   }
   __syncthreads();
-  fft_dit<false>(buf, cw, g.logM1, tw, S);
-  cf* out = ws + ((size_t)p << (g.logM1 + g.logM2));
-  const int logN = g.logM1 + g.logM2;
+  fft_lds<false>(buf, cw, g.logM1, S, tw);
+  cf* out = ws + ((size_t)p << g.logN);
+  const uint32_t mask = (1u << g.logN) - 1;
   for (int e = threadIdx.x; e < cw * M1; e += NTH) {
-    const int k1 = e / cw, c = e - k1 * cw;
+    const int k1 = e >> lcw, c = e & (cw - 1);
     const int n2 = n20 + c;
-    const uint32_t m = ((uint32_t)n2 * (uint32_t)k1) & ((1u << logN) - 1);
-    out[(size_t)k1 * M2 + n2] = cmul(buf[c * S + k1], twiddle(m, logN));
+    out[(size_t)k1 * M2 + n2] = cmul(buf[lds_at(c, k1, S)], bt(((uint32_t)n2 * (uint32_t)k1) & mask));
   }
 }
 
@@ -163,30 +276,38 @@ enum RowMode { ROW_SPEC = 0, ROW_MUL = 1, ROW_MULCONJ = 2, ROW_INV = 3, ROW_INV_
 // inverse FFT, store. ROW_INV: input is a spectrum (natural k2): inverse FFT, store.
 // ROW_INV_MULCONJ: input is a spectrum: times conj kspec[d], inverse FFT, store.
 template <int MODE>
-__global__ __launch_bounds__(NTH) void row_kernel(cf* __restrict__ ws, const cf* __restrict__ kspec,
+__global__ FFT_BOUNDS void row_kernel(cf* __restrict__ ws, const cf* __restrict__ kspec,
                                                   Pairing pr, Geo g) {
   constexpr bool FWD = MODE == ROW_SPEC || MODE == ROW_MUL || MODE == ROW_MULCONJ;
   constexpr bool MUL = MODE == ROW_MUL || MODE == ROW_MULCONJ || MODE == ROW_INV_MULCONJ;
   constexpr bool CONJK = MODE == ROW_MULCONJ || MODE == ROW_INV_MULCONJ;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int M1 = 1 << g.logM1, M2 = 1 << g.logM2;
-  const int rw = max(1, 2048 >> g.logM2);  // rows per block
-  cf* buf = reinterpret_cast<cf*>(smem);   // [rw][M2]
-  cf* tw = buf + rw * M2;
+  const int M2 = 1 << g.logM2;
+  const int lrw = log_row_group(g), rw = 1 << lrw;
+  const int S = seq_stride(g.logM2, false);
+  cf* buf = reinterpret_cast<cf*>(smem);  // [rw][S] padded
+  cf* tw = buf + rw * S;
   const int k10 = blockIdx.x * rw;
   const int p = blockIdx.y;
-  const int nrow = min(rw, M1 - k10);
   make_table(tw, g.logM2);
-  cf* base = ws + ((size_t)p << (g.logM1 + g.logM2)) + (size_t)k10 * M2;
-  for (int e = threadIdx.x; e < nrow * M2; e += NTH) {
-    const int r = e >> g.logM2, n = e & (M2 - 1);
-    const int dst = FWD ? brev(n, g.logM2) : n;
-    buf[r * M2 + dst] = base[e];
+  cf* base = ws + ((size_t)p << g.logN) + (size_t)k10 * M2;
+  {
+    cf v[PPT];
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      if (e < rw * M2) v[it] = base[e];
+    }
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      if (e < rw * M2) buf[lds_at(e >> g.logM2, e & (M2 - 1), S)] = v[it];
+    }
   }
   __syncthreads();
-  if (FWD) fft_dit<false>(buf, nrow, g.logM2, tw, M2);
+  if (FWD) fft_lds<false>(buf, rw, g.logM2, S, tw);
   if (MODE == ROW_SPEC) {
-    for (int e = threadIdx.x; e < nrow * M2; e += NTH) base[e] = buf[e];
+    for (int e = threadIdx.x; e < rw * M2; e += NTH) base[e] = buf[lds_at(e >> g.logM2, e & (M2 - 1), S)];
     return;
   }
   if (MUL) {
@@ -195,19 +316,23 @@ __global__ __launch_bounds__(NTH) void row_kernel(cf* __restrict__ ws, const cf*
       int ra, rb;
       pr.rows(p, d, ra, rb);
     }
-    const cf* ks = kspec + ((size_t)d << (g.logM1 + g.logM2)) + (size_t)k10 * M2;
-    for (int e = threadIdx.x; e < nrow * M2; e += NTH) {
-      cf kv = ks[e];
-      if (CONJK) kv = cconj(kv);
-      buf[e] = cmul(buf[e], kv);
+    const cf* ks = kspec + ((size_t)d << g.logN) + (size_t)k10 * M2;
+    cf kv[PPT];
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      if (e < rw * M2) kv[it] = ks[e];
+    }
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      const int a = lds_at(e >> g.logM2, e & (M2 - 1), S);
+      if (e < rw * M2) buf[a] = cmul(buf[a], CONJK ? cconj(kv[it]) : kv[it]);
     }
     __syncthreads();
   }
-  fft_dif<true>(buf, nrow, g.logM2, tw, M2);
-  for (int e = threadIdx.x; e < nrow * M2; e += NTH) {
-    const int r = e >> g.logM2, n = e & (M2 - 1);
-    base[e] = buf[r * M2 + brev(n, g.logM2)];
-  }
+  fft_lds<true>(buf, rw, g.logM2, S, tw);
+  for (int e = threadIdx.x; e < rw * M2; e += NTH) base[e] = buf[lds_at(e >> g.logM2, e & (M2 - 1), S)];
 }
 
 // ---------------------------------------------------------------- C: inverse column FFT over k1
@@ -215,51 +340,74 @@ enum OutMode { OUT_PAIR = 0, OUT_REAL = 1 };
 // OUT_PAIR: rows ra/rb of y get Re/Im at i = n - off for i in [0, L), plus bias[d] * aux[i].
 // OUT_REAL: row p (= channel) of outf gets Re * scale at i = n for i < L.
 template <typename T, int MODE>
-__global__ __launch_bounds__(NTH) void col_inv_kernel(const cf* __restrict__ ws, Pairing pr, Geo g,
+__global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr, Geo g,
                                                       int off, const float* __restrict__ bias,
                                                       const T* __restrict__ aux, T* __restrict__ y,
                                                       float* __restrict__ outf, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M1 = 1 << g.logM1, M2 = 1 << g.logM2;
-  const int cw = min(CW, M2);
-  const int S = M1 + 1;
+  const int lcw = log_col_group(g), cw = 1 << lcw;
+  const int S = seq_stride(g.logM1, true);
   cf* buf = reinterpret_cast<cf*>(smem);
   cf* tw = buf + cw * S;
+  BigTwiddle bt{tw + M1};
   const int n20 = blockIdx.x * cw;
   const int p = blockIdx.y;
-  const int logN = g.logM1 + g.logM2;
   make_table(tw, g.logM1);
-  const cf* src = ws + ((size_t)p << logN);
-  for (int e = threadIdx.x; e < cw * M1; e += NTH) {
-    const int k1 = e / cw, c = e - k1 * cw;
-    const int n2 = n20 + c;
-    const uint32_t m = ((uint32_t)n2 * (uint32_t)k1) & ((1u << logN) - 1);
-    buf[c * S + brev(k1, g.logM1)] = cmul(src[(size_t)k1 * M2 + n2], cconj(twiddle(m, logN)));
+  bt.init(g.logN);
+  __syncthreads();
+  const cf* src = ws + ((size_t)p << g.logN);
+  const uint32_t mask = (1u << g.logN) - 1;
+  {
+    cf v[PPT];
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      const int k1 = e >> lcw, c = e & (cw - 1);
+      if (e < cw * M1) v[it] = src[(size_t)k1 * M2 + n20 + c];
+    }
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      const int k1 = e >> lcw, c = e & (cw - 1);
+      const int n2 = n20 + c;
+      if (e < cw * M1) buf[lds_at(c, k1, S)] = cmul(v[it], cconj(bt(((uint32_t)n2 * (uint32_t)k1) & mask)));
+    }
   }
   __syncthreads();
-  fft_dit<true>(buf, cw, g.logM1, tw, S);
+  fft_lds<true>(buf, cw, g.logM1, S, tw);
   if (MODE == OUT_PAIR) {
     int d, ra, rb;
     pr.rows(p, d, ra, rb);
     const float bd = bias ? bias[d] : 0.f;
-    for (int e = threadIdx.x; e < cw * M1; e += NTH) {
-      const int n1 = e / cw, c = e - n1 * cw;
+    float xa[PPT], xb[PPT];
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      const int n1 = e >> lcw, c = e & (cw - 1);
       const int i = n1 * M2 + n20 + c - off;
-      if (i < 0 || i >= g.L) continue;
-      const cf v = buf[c * S + n1];
-      const size_t ia = (size_t)ra * g.L + i;
-      y[ia] = from_f32<T>(v.x + bd * (aux ? to_f32(aux[ia]) : 0.f));
-      if (rb >= 0) {
-        const size_t ib = (size_t)rb * g.L + i;
-        y[ib] = from_f32<T>(v.y + bd * (aux ? to_f32(aux[ib]) : 0.f));
+      xa[it] = xb[it] = 0.f;
+      if (aux && e < cw * M1 && i >= 0 && i < g.L) {
+        xa[it] = to_f32(aux[(size_t)ra * g.L + i]);
+        if (rb >= 0) xb[it] = to_f32(aux[(size_t)rb * g.L + i]);
       }
+    }
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      const int n1 = e >> lcw, c = e & (cw - 1);
+      const int i = n1 * M2 + n20 + c - off;
+      if (e >= cw * M1 || i < 0 || i >= g.L) continue;
+      const cf v = buf[lds_at(c, n1, S)];
+      y[(size_t)ra * g.L + i] = from_f32<T>(v.x + bd * xa[it]);
+      if (rb >= 0) y[(size_t)rb * g.L + i] = from_f32<T>(v.y + bd * xb[it]);
     }
   } else {
     for (int e = threadIdx.x; e < cw * M1; e += NTH) {
-      const int n1 = e / cw, c = e - n1 * cw;
+      const int n1 = e >> lcw, c = e & (cw - 1);
       const int i = n1 * M2 + n20 + c;
       if (i >= g.L) continue;
-      outf[(size_t)p * g.L + i] = buf[c * S + n1].x * scale;
+      outf[(size_t)p * g.L + i] = buf[lds_at(c, n1, S)].x * scale;
     }
   }
 }
@@ -305,16 +453,32 @@ __global__ __launch_bounds__(NTH) void dkspec_kernel(const cf* __restrict__ zu, 
   }
 }
 
-// dbias[d] = sum_{b,t} dy[b,d,t] u[b,d,t]   (one block per channel, fixed order)
+// dbias[d] = sum_{b,t} dy[b,d,t] u[b,d,t]: blockIdx.x = channel, blockIdx.y = one of DB_CHUNKS
+// slices of the (b, t) range -> partials[d][chunk]; dbias_final sums them in fixed order.
+constexpr int DB_CHUNKS = 32;
 template <typename T>
 __global__ __launch_bounds__(NTH) void dbias_kernel(const T* __restrict__ dy, const T* __restrict__ u,
-                                                    int B, int D, int L, float* __restrict__ dbias) {
+                                                    int B, int D, int L, float* __restrict__ part) {
   __shared__ float red[NTH / 64];
-  const int d = blockIdx.x;
+  const int d = blockIdx.x, ch = blockIdx.y;
+  const size_t tot = (size_t)B * L;
+  const size_t per = (tot + DB_CHUNKS - 1) / DB_CHUNKS;
+  const size_t beg = ch * per, end = min(tot, beg + per);
   float s = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const size_t o = ((size_t)b * D + d) * L;
-    for (int t = threadIdx.x; t < L; t += NTH) s += to_f32(dy[o + t]) * to_f32(u[o + t]);
+  for (size_t q = beg + threadIdx.x; q < end; q += 4 * NTH) {
+    float a[4], b[4];
+#pragma unroll
+    for (int u4 = 0; u4 < 4; ++u4) {
+      const size_t qq = q + (size_t)u4 * NTH;
+      a[u4] = b[u4] = 0.f;
+      if (qq < end) {
+        const size_t o = ((qq / L) * D + d) * (size_t)L + qq % L;
+        a[u4] = to_f32(dy[o]);
+        b[u4] = to_f32(u[o]);
+      }
+    }
+#pragma unroll
+    for (int u4 = 0; u4 < 4; ++u4) s += a[u4] * b[u4];
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -322,8 +486,16 @@ __global__ __launch_bounds__(NTH) void dbias_kernel(const T* __restrict__ dy, co
   if (threadIdx.x == 0) {
     float t = 0.f;
     for (int w = 0; w < NTH / 64; ++w) t += red[w];
-    dbias[d] = t;
+    part[d * DB_CHUNKS + ch] = t;
   }
+}
+
+__global__ void dbias_final(const float* __restrict__ part, int D, float* __restrict__ dbias) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float t = 0.f;
+  for (int c = 0; c < DB_CHUNKS; ++c) t += part[d * DB_CHUNKS + c];
+  dbias[d] = t;
 }
 
 inline bool geometry(int L, Geo& g) {
@@ -333,27 +505,20 @@ inline bool geometry(int L, Geo& g) {
   if (logN > 18) return false;
   g.L = L;
   g.logN = logN;
-  g.logM2 = logN - 1 < 8 ? logN - 1 : 8;
+  g.logM2 = logN - 1 < 9 ? logN - 1 : 9;  // N = 2^17 -> 256 x 512
   g.logM1 = logN - g.logM2;
   return true;
 }
 
 inline size_t col_lds(const Geo& g) {
-  const int cw = (1 << g.logM2) < CW ? (1 << g.logM2) : CW;
-  return ((size_t)cw * ((1u << g.logM1) + 1) + (1u << (g.logM1 - 1))) * sizeof(cf);
+  return ((size_t)(1 << log_col_group(g)) * seq_stride(g.logM1, true) + (1u << g.logM1) +
+          big_twiddle_elems(g.logN)) * sizeof(cf);
 }
 inline size_t row_lds(const Geo& g) {
-  const int rw = (2048 >> g.logM2) > 1 ? (2048 >> g.logM2) : 1;
-  return ((size_t)rw * (1u << g.logM2) + (1u << (g.logM2 - 1))) * sizeof(cf);
+  return ((size_t)(1 << log_row_group(g)) * seq_stride(g.logM2, false) + (1u << g.logM2)) * sizeof(cf);
 }
-inline dim3 col_grid(const Geo& g, int P) {
-  const int cw = (1 << g.logM2) < CW ? (1 << g.logM2) : CW;
-  return dim3((1 << g.logM2) / cw, P);
-}
-inline dim3 row_grid(const Geo& g, int P) {
-  const int rw = (2048 >> g.logM2) > 1 ? (2048 >> g.logM2) : 1;
-  return dim3(((1 << g.logM1) + rw - 1) / rw, P);
-}
+inline dim3 col_grid(const Geo& g, int P) { return dim3(1 << (g.logM2 - log_col_group(g)), P); }
+inline dim3 row_grid(const Geo& g, int P) { return dim3(1 << (g.logM1 - log_row_group(g)), P); }
 
 template <typename Kern>
 inline void allow_lds(Kern k, size_t bytes) {
@@ -487,8 +652,13 @@ static void bwd_impl(const void* dy, const void* u, const cf* kspec, const float
     launch_row<ROW_INV_MULCONJ>(zy, kspec, pr, g, P, s);
     launch_col_inv<T, OUT_PAIR>(zy, pr, g, pb, bias, dy, du, nullptr, 1.f, P, s);
   }
-  if (dbias) hipLaunchKernelGGL(dbias_kernel<T>, dim3(D), dim3(NTH), 0, s, (const T*)dy, (const T*)u, B, D,
-                                g.L, dbias);
+  if (dbias) {
+    // partials live after the dk spectra in the workspace
+    float* part = reinterpret_cast<float*>(ws + (2 * (size_t)P + D) * N);
+    hipLaunchKernelGGL(dbias_kernel<T>, dim3(D, DB_CHUNKS), dim3(NTH), 0, s, (const T*)dy, (const T*)u, B,
+                       D, g.L, part);
+    hipLaunchKernelGGL(dbias_final, dim3((D + 255) / 256), dim3(256), 0, s, (const float*)part, D, dbias);
+  }
 }
 
 extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec,
@@ -499,7 +669,8 @@ extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const v
   DNA_CHECK_ARG(B > 0 && D > 0 && geometry(L, g), "dna_fftconv_bwd: L=%d must be a power of 2 in [64, 131072]", L);
   const size_t N = (size_t)1 << g.logN;
   const size_t P = (size_t)((B + 1) / 2) * D;
-  DNA_CHECK_ARG(ws_bytes >= (2 * P + (size_t)D) * N * sizeof(cf), "dna_fftconv_bwd: workspace too small");
+  DNA_CHECK_ARG(ws_bytes >= (2 * P + (size_t)D) * N * sizeof(cf) + (size_t)D * DB_CHUNKS * sizeof(float),
+                "dna_fftconv_bwd: workspace too small");
   const int pb = pad_before(L, bidirectional);
   hipStream_t s = as_stream(stream);
   if (dtype == DNA_BF16)
