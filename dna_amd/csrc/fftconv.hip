@@ -14,8 +14,9 @@
 //      -> T[k1][n2]
 //   B  row pass:    for each row k1, FFT-M2 over n2 -> spectrum Z[k1 + M1*k2], times the filter
 //      spectrum (stored in the same [k1][k2] order, 1/N folded in), inverse FFT-M2 -> T'[k1][n2]
-//   C  column pass: times W_N^-(n2*k1), inverse FFT-M1 over k1 -> z[n1*M2 + n2]; epilogue adds
-//      bias*u and writes rows b, b+1 (real, imaginary part) for t < L.
+//   C  column pass: times W_N^-(n2*k1), inverse FFT-M1 over k1 -> z[n1*M2 + n2]; writes rows
+//      b, b+1 (real, imaginary part) for t < L. The bias term bias*u is a filter tap at
+//      (N - pad_before) mod N folded into the filter spectrum, so no epilogue read of u.
 // FFTs are autosort Stockham passes in LDS with radix-8/4/2 register butterflies (16 points per
 // thread per pass) and an LDS twiddle table W_M^m; the inter-pass twiddles W_N^(n2*k1) come
 // from a two-level LDS table (W_N^(m & 511) * W_N^(512*(m >> 9))), all built with sincospi of
@@ -317,17 +318,20 @@ __global__ FFT_BOUNDS void row_kernel(cf* __restrict__ ws, const cf* __restrict_
       pr.rows(p, d, ra, rb);
     }
     const cf* ks = kspec + ((size_t)d << g.logN) + (size_t)k10 * M2;
-    cf kv[PPT];
+#pragma unroll 1
+    for (int c0 = 0; c0 < PPT; c0 += 8) {  // 8 spectrum loads in flight (register budget)
+      cf kv[8];
 #pragma unroll
-    for (int it = 0; it < PPT; ++it) {
-      const int e = threadIdx.x + it * NTH;
-      if (e < rw * M2) kv[it] = ks[e];
-    }
+      for (int it = 0; it < 8; ++it) {
+        const int e = threadIdx.x + (c0 + it) * NTH;
+        if (e < rw * M2) kv[it] = ks[e];
+      }
 #pragma unroll
-    for (int it = 0; it < PPT; ++it) {
-      const int e = threadIdx.x + it * NTH;
-      const int a = lds_at(e >> g.logM2, e & (M2 - 1), S);
-      if (e < rw * M2) buf[a] = cmul(buf[a], CONJK ? cconj(kv[it]) : kv[it]);
+      for (int it = 0; it < 8; ++it) {
+        const int e = threadIdx.x + (c0 + it) * NTH;
+        const int a = lds_at(e >> g.logM2, e & (M2 - 1), S);
+        if (e < rw * M2) buf[a] = cmul(buf[a], CONJK ? cconj(kv[it]) : kv[it]);
+      }
     }
     __syncthreads();
   }
@@ -337,13 +341,11 @@ __global__ FFT_BOUNDS void row_kernel(cf* __restrict__ ws, const cf* __restrict_
 
 // ---------------------------------------------------------------- C: inverse column FFT over k1
 enum OutMode { OUT_PAIR = 0, OUT_REAL = 1 };
-// OUT_PAIR: rows ra/rb of y get Re/Im at i = n - off for i in [0, L), plus bias[d] * aux[i].
+// OUT_PAIR: rows ra/rb of y get Re/Im at i = n - off for i in [0, L).
 // OUT_REAL: row p (= channel) of outf gets Re * scale at i = n for i < L.
 template <typename T, int MODE>
-__global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr, Geo g,
-                                                      int off, const float* __restrict__ bias,
-                                                      const T* __restrict__ aux, T* __restrict__ y,
-                                                      float* __restrict__ outf, float scale) {
+__global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr, Geo g, int off,
+                                          T* __restrict__ y, float* __restrict__ outf, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M1 = 1 << g.logM1, M2 = 1 << g.logM2;
   const int lcw = log_col_group(g), cw = 1 << lcw;
@@ -379,28 +381,15 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
   if (MODE == OUT_PAIR) {
     int d, ra, rb;
     pr.rows(p, d, ra, rb);
-    const float bd = bias ? bias[d] : 0.f;
-    float xa[PPT], xb[PPT];
-#pragma unroll
-    for (int it = 0; it < PPT; ++it) {
-      const int e = threadIdx.x + it * NTH;
+    T* ya = y + (size_t)ra * g.L;
+    T* yb = rb >= 0 ? y + (size_t)rb * g.L : nullptr;
+    for (int e = threadIdx.x; e < cw * M1; e += NTH) {
       const int n1 = e >> lcw, c = e & (cw - 1);
       const int i = n1 * M2 + n20 + c - off;
-      xa[it] = xb[it] = 0.f;
-      if (aux && e < cw * M1 && i >= 0 && i < g.L) {
-        xa[it] = to_f32(aux[(size_t)ra * g.L + i]);
-        if (rb >= 0) xb[it] = to_f32(aux[(size_t)rb * g.L + i]);
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < PPT; ++it) {
-      const int e = threadIdx.x + it * NTH;
-      const int n1 = e >> lcw, c = e & (cw - 1);
-      const int i = n1 * M2 + n20 + c - off;
-      if (e >= cw * M1 || i < 0 || i >= g.L) continue;
+      if (i < 0 || i >= g.L) continue;
       const cf v = buf[lds_at(c, n1, S)];
-      y[(size_t)ra * g.L + i] = from_f32<T>(v.x + bd * xa[it]);
-      if (rb >= 0) y[(size_t)rb * g.L + i] = from_f32<T>(v.y + bd * xb[it]);
+      ya[i] = from_f32<T>(v.x);
+      if (yb) yb[i] = from_f32<T>(v.y);
     }
   } else {
     for (int e = threadIdx.x; e < cw * M1; e += NTH) {
@@ -414,25 +403,37 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
 
 // ---------------------------------------------------------------- filter spectrum separation
 // Z = FFT(k_{2q} + i k_{2q+1}) in [k1][k2] order -> kspec rows 2q, 2q+1 (scaled 1/N):
-//   K_a[k] = (Z[k] + conj Z[N-k]) / 2,   K_b[k] = (Z[k] - conj Z[N-k]) / (2i)
-__global__ __launch_bounds__(NTH) void separate_kernel(const cf* __restrict__ ws, int D, Geo g,
-                                                       cf* __restrict__ kspec) {
+//   K_a[f] = (Z[f] + conj Z[N-f]) / 2,   K_b[f] = (Z[f] - conj Z[N-f]) / (2i)
+// plus the bias folded in as a filter tap: bias * u[t] = bias * u~[(t + pad) mod N] is tap
+// (N - pad) mod N of the circular convolution, i.e. + bias * W_N^(-f * pad) in the spectrum.
+__global__ __launch_bounds__(256) void separate_kernel(const cf* __restrict__ ws, const float* __restrict__ bias,
+                                                       int D, int pad, Geo g, cf* __restrict__ kspec) {
   const int M1 = 1 << g.logM1, M2 = 1 << g.logM2;
   const int logN = g.logM1 + g.logM2;
   const size_t N = (size_t)1 << logN;
+  const uint32_t mask = (uint32_t)N - 1;
   const int q = blockIdx.y;
   const float s = 0.5f / (float)N;
+  const float ba = bias ? bias[2 * q] / (float)N : 0.f;
+  const float bb = (bias && 2 * q + 1 < D) ? bias[2 * q + 1] / (float)N : 0.f;
   const cf* z = ws + ((size_t)q << logN);
-  for (size_t pos = (size_t)blockIdx.x * NTH + threadIdx.x; pos < N; pos += (size_t)gridDim.x * NTH) {
+  for (size_t pos = (size_t)blockIdx.x * 256 + threadIdx.x; pos < N; pos += (size_t)gridDim.x * 256) {
     const int k1 = (int)(pos >> g.logM2), k2 = (int)(pos & (M2 - 1));
     const int k1m = k1 == 0 ? 0 : M1 - k1;
     const int k2m = k1 == 0 ? ((M2 - k2) & (M2 - 1)) : (M2 - 1 - k2);
     const cf a = z[pos], b = cconj(z[((size_t)k1m << g.logM2) + k2m]);
-    kspec[((size_t)(2 * q) << logN) + pos] = make_float2((a.x + b.x) * s, (a.y + b.y) * s);
+    cf sh = make_float2(1.f, 0.f);
+    if (pad) {
+      const uint32_t f = (uint32_t)k1 + ((uint32_t)k2 << g.logM1);
+      sh = cconj(twiddle((f * (uint32_t)pad) & mask, logN));
+    }
+    kspec[((size_t)(2 * q) << logN) + pos] =
+        make_float2((a.x + b.x) * s + ba * sh.x, (a.y + b.y) * s + ba * sh.y);
     if (2 * q + 1 < D) {
       // (a - b) / (2i) = (-i/2)(a - b)
       const cf dlt = csub(a, b);
-      kspec[((size_t)(2 * q + 1) << logN) + pos] = make_float2(dlt.y * s, -dlt.x * s);
+      kspec[((size_t)(2 * q + 1) << logN) + pos] =
+          make_float2(dlt.y * s + bb * sh.x, -dlt.x * s + bb * sh.y);
     }
   }
 }
@@ -541,12 +542,11 @@ void launch_row(cf* ws, const cf* kspec, Pairing pr, const Geo& g, int P, hipStr
 }
 
 template <typename T, int MODE>
-void launch_col_inv(const cf* ws, Pairing pr, const Geo& g, int off, const float* bias, const void* aux,
-                    void* y, float* outf, float scale, int P, hipStream_t s) {
+void launch_col_inv(const cf* ws, Pairing pr, const Geo& g, int off, void* y, float* outf, float scale,
+                    int P, hipStream_t s) {
   auto k = col_inv_kernel<T, MODE>;
   allow_lds(k, col_lds(g));
-  hipLaunchKernelGGL(k, col_grid(g, P), dim3(NTH), col_lds(g), s, ws, pr, g, off, bias,
-                     (const T*)aux, (T*)y, outf, scale);
+  hipLaunchKernelGGL(k, col_grid(g, P), dim3(NTH), col_lds(g), s, ws, pr, g, off, (T*)y, outf, scale);
 }
 
 inline int pad_before(int L, int bidirectional) {
@@ -576,8 +576,8 @@ extern "C" size_t dna_fftconv_kspec_elems(int L) {
   return (size_t)2 << g.logN;  // floats per channel (complex N)
 }
 
-extern "C" int dna_fftconv_filter(const float* k, int D, int L, void* kspec, void* ws,
-                                  size_t ws_bytes, void* stream) {
+extern "C" int dna_fftconv_filter(const float* k, const float* bias, int D, int L, int bidirectional,
+                                  void* kspec, void* ws, size_t ws_bytes, void* stream) {
   Geo g;
   DNA_CHECK_ARG(k && kspec && ws, "dna_fftconv_filter: null pointer");
   DNA_CHECK_ARG(D > 0 && geometry(L, g), "dna_fftconv_filter: L=%d must be a power of 2 in [64, 131072]", L);
@@ -589,15 +589,15 @@ extern "C" int dna_fftconv_filter(const float* k, int D, int L, void* kspec, voi
   cf* w = (cf*)ws;
   launch_col_fwd<float>(k, pr, g, 0, w, Q, s);
   launch_row<ROW_SPEC>(w, nullptr, pr, g, Q, s);
-  const int bx = (int)((N + NTH - 1) / NTH) < 1024 ? (int)((N + NTH - 1) / NTH) : 1024;
-  hipLaunchKernelGGL(separate_kernel, dim3(bx, Q), dim3(NTH), 0, s, (const cf*)w, D, g, (cf*)kspec);
+  const int bx = (int)((N + 255) / 256) < 1024 ? (int)((N + 255) / 256) : 1024;
+  hipLaunchKernelGGL(separate_kernel, dim3(bx, Q), dim3(256), 0, s, (const cf*)w, bias, D,
+                     pad_before(L, bidirectional), g, (cf*)kspec);
   DNA_LAUNCH_CHECK("dna_fftconv_filter");
   return DNA_OK;
 }
 
-extern "C" int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, const float* bias,
-                               int B, int D, int L, int bidirectional, void* y, void* ws,
-                               size_t ws_bytes, void* stream) {
+extern "C" int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, int B, int D, int L,
+                               int bidirectional, void* y, void* ws, size_t ws_bytes, void* stream) {
   Geo g;
   DNA_CHECK_ARG(u && kspec && y && ws, "dna_fftconv_fwd: null pointer");
   DNA_CHECK_ARG(B > 0 && D > 0 && geometry(L, g), "dna_fftconv_fwd: L=%d must be a power of 2 in [64, 131072]", L);
@@ -611,11 +611,11 @@ extern "C" int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, cons
   if (dtype == DNA_BF16) {
     launch_col_fwd<bf16>(u, pr, g, pb, w, P, s);
     launch_row<ROW_MUL>(w, (const cf*)kspec, pr, g, P, s);
-    launch_col_inv<bf16, OUT_PAIR>(w, pr, g, 0, bias, u, y, nullptr, 1.f, P, s);
+    launch_col_inv<bf16, OUT_PAIR>(w, pr, g, 0, y, nullptr, 1.f, P, s);
   } else if (dtype == DNA_F32) {
     launch_col_fwd<float>(u, pr, g, pb, w, P, s);
     launch_row<ROW_MUL>(w, (const cf*)kspec, pr, g, P, s);
-    launch_col_inv<float, OUT_PAIR>(w, pr, g, 0, bias, u, y, nullptr, 1.f, P, s);
+    launch_col_inv<float, OUT_PAIR>(w, pr, g, 0, y, nullptr, 1.f, P, s);
   } else {
     DNA_CHECK_ARG(false, "dna_fftconv_fwd: bad dtype");
   }
@@ -624,8 +624,8 @@ extern "C" int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, cons
 }
 
 template <typename T>
-static void bwd_impl(const void* dy, const void* u, const cf* kspec, const float* bias, int B, int D,
-                     const Geo& g, int pb, void* du, float* dk, float* dbias, cf* ws, hipStream_t s) {
+static void bwd_impl(const void* dy, const void* u, const cf* kspec, int B, int D, const Geo& g, int pb,
+                     void* du, float* dk, float* dbias, cf* ws, hipStream_t s) {
   const size_t N = (size_t)1 << g.logN;
   const int BP = (B + 1) / 2, P = BP * D;
   Pairing pr{B, D, BP};
@@ -645,12 +645,12 @@ static void bwd_impl(const void* dy, const void* u, const cf* kspec, const float
                        g.logN, pk);
     Pairing one{D, 1, 0};  // BP = 0: row index is the channel
     launch_row<ROW_INV>(pk, nullptr, one, g, D, s);
-    launch_col_inv<float, OUT_REAL>(pk, one, g, 0, nullptr, nullptr, nullptr, dk, 1.f / (float)N, D, s);
+    launch_col_inv<float, OUT_REAL>(pk, one, g, 0, nullptr, dk, 1.f / (float)N, D, s);
   }
   if (du) {
-    // du~ = IFFT(DY * conj(K)); du = du~[pb : pb + L] + bias * dy   (zy is consumed in place)
+    // du~ = IFFT(DY * conj(K')) with the bias tap in K'; du = du~[pb : pb + L]  (zy consumed in place)
     launch_row<ROW_INV_MULCONJ>(zy, kspec, pr, g, P, s);
-    launch_col_inv<T, OUT_PAIR>(zy, pr, g, pb, bias, dy, du, nullptr, 1.f, P, s);
+    launch_col_inv<T, OUT_PAIR>(zy, pr, g, pb, du, nullptr, 1.f, P, s);
   }
   if (dbias) {
     // partials live after the dk spectra in the workspace
@@ -661,9 +661,9 @@ static void bwd_impl(const void* dy, const void* u, const cf* kspec, const float
   }
 }
 
-extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec,
-                               const float* bias, int B, int D, int L, int bidirectional, void* du,
-                               float* dk, float* dbias, void* ws, size_t ws_bytes, void* stream) {
+extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec, int B,
+                               int D, int L, int bidirectional, void* du, float* dk, float* dbias,
+                               void* ws, size_t ws_bytes, void* stream) {
   Geo g;
   DNA_CHECK_ARG(dy && u && kspec && ws, "dna_fftconv_bwd: null pointer");
   DNA_CHECK_ARG(B > 0 && D > 0 && geometry(L, g), "dna_fftconv_bwd: L=%d must be a power of 2 in [64, 131072]", L);
@@ -674,9 +674,9 @@ extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const v
   const int pb = pad_before(L, bidirectional);
   hipStream_t s = as_stream(stream);
   if (dtype == DNA_BF16)
-    bwd_impl<bf16>(dy, u, (const cf*)kspec, bias, B, D, g, pb, du, dk, dbias, (cf*)ws, s);
+    bwd_impl<bf16>(dy, u, (const cf*)kspec, B, D, g, pb, du, dk, dbias, (cf*)ws, s);
   else if (dtype == DNA_F32)
-    bwd_impl<float>(dy, u, (const cf*)kspec, bias, B, D, g, pb, du, dk, dbias, (cf*)ws, s);
+    bwd_impl<float>(dy, u, (const cf*)kspec, B, D, g, pb, du, dk, dbias, (cf*)ws, s);
   else
     DNA_CHECK_ARG(false, "dna_fftconv_bwd: bad dtype");
   DNA_LAUNCH_CHECK("dna_fftconv_bwd");

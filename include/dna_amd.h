@@ -166,19 +166,20 @@ int dna_geglu_linear_dgrad(const void* dy, const void* wo, const void* g, int M,
  * u, y [B, D, L] (dtype: DNA_F32 / DNA_BF16), k [D, L] fp32, bias [D] fp32 or NULL; u~ = u
  * zero-padded to 2L at offset 0 (causal) or pad_before = L/2 (bidirectional, :68-74).
  * L must be a power of two in [64, 131072]. Internally fp32 (four-step FFT of size 2L).
- * kspec: the filter spectrum, dna_fftconv_kspec_elems(L) floats per channel, written by
- * dna_fftconv_filter (its workspace: ceil(D/2) * 4L complex64 = dna_fftconv_workspace(1, D, L) is enough). */
+ * kspec: dna_fftconv_kspec_elems(L) floats per channel, written by dna_fftconv_filter: the
+ * spectrum of k with the bias folded in as the filter tap that reproduces bias*u (so fwd and bwd
+ * take no bias). Its workspace: ceil(D/2) * 2L complex64; dna_fftconv_workspace(1, D, L) is enough. */
 size_t dna_fftconv_workspace(int B, int D, int L);
 size_t dna_fftconv_kspec_elems(int L);
-int dna_fftconv_filter(const float* k, int D, int L, void* kspec, void* ws, size_t ws_bytes,
-                       void* stream);
-int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, const float* bias, int B, int D,
-                    int L, int bidirectional, void* y, void* ws, size_t ws_bytes, void* stream);
+int dna_fftconv_filter(const float* k, const float* bias, int D, int L, int bidirectional,
+                       void* kspec, void* ws, size_t ws_bytes, void* stream);
+int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, int B, int D, int L,
+                    int bidirectional, void* y, void* ws, size_t ws_bytes, void* stream);
 /* Gradients of sum(dy * y): du (like u, may be NULL), dk [D, L] fp32 (may be NULL),
  * dbias [D] fp32 (may be NULL). ws: dna_fftconv_workspace(B, D, L) bytes. */
-int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec, const float* bias,
-                    int B, int D, int L, int bidirectional, void* du, float* dk, float* dbias,
-                    void* ws, size_t ws_bytes, void* stream);
+int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec, int B, int D,
+                    int L, int bidirectional, void* du, float* dk, float* dbias, void* ws,
+                    size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------ masked-LM cross entropy
  * Per-row CE over the masked rows only (the model computes logits only for labels>0 rows,
