@@ -49,8 +49,8 @@ _SIGS = {
     "dna_fftconv_workspace": (_sz, [_i, _i, _i]),
     "dna_fftconv_kspec_elems": (_sz, [_i]),
     "dna_fftconv_filter": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _sz, _vp]),
-    "dna_fftconv_fwd": (_i, [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
-    "dna_fftconv_bwd": (_i, [_vp, _vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dna_fftconv_fwd": (_i, [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _sz, _vp]),
+    "dna_fftconv_bwd": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dna_xent_fwd": (_i, [_vp, _i, _vp, _i, _i, _vp, _vp, _vp]),
     "dna_xent_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _f, _i, _i, _vp, _vp]),
     "dna_sumsq_workspace": (_sz, [_sz]),

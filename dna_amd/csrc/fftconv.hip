@@ -278,7 +278,7 @@ enum RowMode { ROW_SPEC = 0, ROW_MUL = 1, ROW_MULCONJ = 2, ROW_INV = 3, ROW_INV_
 // ROW_INV_MULCONJ: input is a spectrum: times conj kspec[d], inverse FFT, store.
 template <int MODE>
 __global__ FFT_BOUNDS void row_kernel(cf* __restrict__ ws, const cf* __restrict__ kspec,
-                                                  Pairing pr, Geo g) {
+                                      Pairing pr, Geo g, cf* __restrict__ zsave) {
   constexpr bool FWD = MODE == ROW_SPEC || MODE == ROW_MUL || MODE == ROW_MULCONJ;
   constexpr bool MUL = MODE == ROW_MUL || MODE == ROW_MULCONJ || MODE == ROW_INV_MULCONJ;
   constexpr bool CONJK = MODE == ROW_MULCONJ || MODE == ROW_INV_MULCONJ;
@@ -310,6 +310,10 @@ __global__ FFT_BOUNDS void row_kernel(cf* __restrict__ ws, const cf* __restrict_
   if (MODE == ROW_SPEC) {
     for (int e = threadIdx.x; e < rw * M2; e += NTH) base[e] = buf[lds_at(e >> g.logM2, e & (M2 - 1), S)];
     return;
+  }
+  if (MODE == ROW_MUL && zsave) {  // keep the input spectrum for the backward's dk (no barrier needed)
+    cf* zs = zsave + ((size_t)p << g.logN) + (size_t)k10 * M2;
+    for (int e = threadIdx.x; e < rw * M2; e += NTH) zs[e] = buf[lds_at(e >> g.logM2, e & (M2 - 1), S)];
   }
   if (MUL) {
     int d = p;
@@ -535,10 +539,11 @@ int launch_col_fwd(const void* x, Pairing pr, const Geo& g, int off, cf* ws, int
 }
 
 template <int MODE>
-void launch_row(cf* ws, const cf* kspec, Pairing pr, const Geo& g, int P, hipStream_t s) {
+void launch_row(cf* ws, const cf* kspec, Pairing pr, const Geo& g, int P, hipStream_t s,
+                cf* zsave = nullptr) {
   auto k = row_kernel<MODE>;
   allow_lds(k, row_lds(g));
-  hipLaunchKernelGGL(k, row_grid(g, P), dim3(NTH), row_lds(g), s, ws, kspec, pr, g);
+  hipLaunchKernelGGL(k, row_grid(g, P), dim3(NTH), row_lds(g), s, ws, kspec, pr, g, zsave);
 }
 
 template <typename T, int MODE>
@@ -597,7 +602,8 @@ extern "C" int dna_fftconv_filter(const float* k, const float* bias, int D, int 
 }
 
 extern "C" int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, int B, int D, int L,
-                               int bidirectional, void* y, void* ws, size_t ws_bytes, void* stream) {
+                               int bidirectional, void* y, void* uspec, void* ws, size_t ws_bytes,
+                               void* stream) {
   Geo g;
   DNA_CHECK_ARG(u && kspec && y && ws, "dna_fftconv_fwd: null pointer");
   DNA_CHECK_ARG(B > 0 && D > 0 && geometry(L, g), "dna_fftconv_fwd: L=%d must be a power of 2 in [64, 131072]", L);
@@ -610,11 +616,11 @@ extern "C" int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, int 
   const int pb = pad_before(L, bidirectional);
   if (dtype == DNA_BF16) {
     launch_col_fwd<bf16>(u, pr, g, pb, w, P, s);
-    launch_row<ROW_MUL>(w, (const cf*)kspec, pr, g, P, s);
+    launch_row<ROW_MUL>(w, (const cf*)kspec, pr, g, P, s, (cf*)uspec);
     launch_col_inv<bf16, OUT_PAIR>(w, pr, g, 0, y, nullptr, 1.f, P, s);
   } else if (dtype == DNA_F32) {
     launch_col_fwd<float>(u, pr, g, pb, w, P, s);
-    launch_row<ROW_MUL>(w, (const cf*)kspec, pr, g, P, s);
+    launch_row<ROW_MUL>(w, (const cf*)kspec, pr, g, P, s, (cf*)uspec);
     launch_col_inv<float, OUT_PAIR>(w, pr, g, 0, y, nullptr, 1.f, P, s);
   } else {
     DNA_CHECK_ARG(false, "dna_fftconv_fwd: bad dtype");
@@ -624,8 +630,8 @@ extern "C" int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, int 
 }
 
 template <typename T>
-static void bwd_impl(const void* dy, const void* u, const cf* kspec, int B, int D, const Geo& g, int pb,
-                     void* du, float* dk, float* dbias, cf* ws, hipStream_t s) {
+static void bwd_impl(const void* dy, const void* u, const cf* kspec, const cf* uspec, int B, int D,
+                     const Geo& g, int pb, void* du, float* dk, float* dbias, cf* ws, hipStream_t s) {
   const size_t N = (size_t)1 << g.logN;
   const int BP = (B + 1) / 2, P = BP * D;
   Pairing pr{B, D, BP};
@@ -633,15 +639,16 @@ static void bwd_impl(const void* dy, const void* u, const cf* kspec, int B, int 
   cf* zy = ws + (size_t)P * N;
   cf* pk = ws + (size_t)2 * P * N;
   // spectra of u~ and of dy (padded at the end)
-  if (dk) {
+  if (dk && !uspec) {
     launch_col_fwd<T>(u, pr, g, pb, zu, P, s);
     launch_row<ROW_SPEC>(zu, nullptr, pr, g, P, s);
   }
+  const cf* zuc = uspec ? uspec : zu;
   launch_col_fwd<T>(dy, pr, g, 0, zy, P, s);
   launch_row<ROW_SPEC>(zy, nullptr, pr, g, P, s);
   if (dk) {
     const int bx = (int)((N + NTH - 1) / NTH) < 512 ? (int)((N + NTH - 1) / NTH) : 512;
-    hipLaunchKernelGGL(dkspec_kernel, dim3(bx, D), dim3(NTH), 0, s, (const cf*)zu, (const cf*)zy, BP,
+    hipLaunchKernelGGL(dkspec_kernel, dim3(bx, D), dim3(NTH), 0, s, zuc, (const cf*)zy, BP,
                        g.logN, pk);
     Pairing one{D, 1, 0};  // BP = 0: row index is the channel
     launch_row<ROW_INV>(pk, nullptr, one, g, D, s);
@@ -661,9 +668,9 @@ static void bwd_impl(const void* dy, const void* u, const cf* kspec, int B, int 
   }
 }
 
-extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec, int B,
-                               int D, int L, int bidirectional, void* du, float* dk, float* dbias,
-                               void* ws, size_t ws_bytes, void* stream) {
+extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec,
+                               const void* uspec, int B, int D, int L, int bidirectional, void* du,
+                               float* dk, float* dbias, void* ws, size_t ws_bytes, void* stream) {
   Geo g;
   DNA_CHECK_ARG(dy && u && kspec && ws, "dna_fftconv_bwd: null pointer");
   DNA_CHECK_ARG(B > 0 && D > 0 && geometry(L, g), "dna_fftconv_bwd: L=%d must be a power of 2 in [64, 131072]", L);
@@ -674,9 +681,9 @@ extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const v
   const int pb = pad_before(L, bidirectional);
   hipStream_t s = as_stream(stream);
   if (dtype == DNA_BF16)
-    bwd_impl<bf16>(dy, u, (const cf*)kspec, B, D, g, pb, du, dk, dbias, (cf*)ws, s);
+    bwd_impl<bf16>(dy, u, (const cf*)kspec, (const cf*)uspec, B, D, g, pb, du, dk, dbias, (cf*)ws, s);
   else if (dtype == DNA_F32)
-    bwd_impl<float>(dy, u, (const cf*)kspec, B, D, g, pb, du, dk, dbias, (cf*)ws, s);
+    bwd_impl<float>(dy, u, (const cf*)kspec, (const cf*)uspec, B, D, g, pb, du, dk, dbias, (cf*)ws, s);
   else
     DNA_CHECK_ARG(false, "dna_fftconv_bwd: bad dtype");
   DNA_LAUNCH_CHECK("dna_fftconv_bwd");

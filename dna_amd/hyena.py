@@ -47,18 +47,22 @@ class FFTConv(torch.autograd.Function):
         wsz = lib.dna_fftconv_workspace(B, D, L)
         ws = torch.empty(wsz, device=u.device, dtype=torch.uint8)
         y = torch.empty_like(u)
+        # keep the input spectrum for dk when the filter needs a gradient
+        uspec = (torch.empty(((B + 1) // 2) * D, nk, device=u.device, dtype=torch.float32)
+                 if ctx.needs_input_grad[1] else None)
         with _timed("fftconv_fwd", B * D * L * 2 * _bytes_per_elem(u), "byte"):
             N.call("dna_fftconv_filter", kf.data_ptr(), _p(b32), D, L, int(bool(bidirectional)),
                    kspec.data_ptr(), ws.data_ptr(), wsz, N.stream_ptr())
             N.call("dna_fftconv_fwd", u.data_ptr(), _dt(u), kspec.data_ptr(), B, D, L,
-                   int(bool(bidirectional)), y.data_ptr(), ws.data_ptr(), wsz, N.stream_ptr())
-        ctx.save_for_backward(u, kspec)
+                   int(bool(bidirectional)), y.data_ptr(), _p(uspec), ws.data_ptr(), wsz,
+                   N.stream_ptr())
+        ctx.save_for_backward(u, kspec, uspec)
         ctx.cfg = (B, D, L, bool(bidirectional), bias is not None, k.dtype, None if bias is None else bias.shape)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        u, kspec = ctx.saved_tensors
+        u, kspec, uspec = ctx.saved_tensors
         B, D, L, bi, has_bias, kdtype, bshape = ctx.cfg
         dy = dy.contiguous().to(u.dtype)
         need_u, need_k, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
@@ -69,8 +73,9 @@ class FFTConv(torch.autograd.Function):
         wsz = lib.dna_fftconv_workspace(B, D, L)
         ws = torch.empty(wsz, device=u.device, dtype=torch.uint8)
         with _timed("fftconv_bwd", B * D * L * 3 * _bytes_per_elem(u), "byte"):
-            N.call("dna_fftconv_bwd", dy.data_ptr(), u.data_ptr(), _dt(u), kspec.data_ptr(), B, D, L,
-                   int(bi), _p(du), _p(dk), _p(db), ws.data_ptr(), wsz, N.stream_ptr())
+            N.call("dna_fftconv_bwd", dy.data_ptr(), u.data_ptr(), _dt(u), kspec.data_ptr(),
+                   _p(uspec), B, D, L, int(bi), _p(du), _p(dk), _p(db), ws.data_ptr(), wsz,
+                   N.stream_ptr())
         return (du, None if dk is None else dk.to(kdtype),
                 None if db is None else db.reshape(bshape), None)
 

@@ -173,13 +173,17 @@ size_t dna_fftconv_workspace(int B, int D, int L);
 size_t dna_fftconv_kspec_elems(int L);
 int dna_fftconv_filter(const float* k, const float* bias, int D, int L, int bidirectional,
                        void* kspec, void* ws, size_t ws_bytes, void* stream);
+/* uspec (may be NULL): receives the spectrum of the padded input, ceil(B/2)*D*4L floats, for
+ * dna_fftconv_bwd to reuse (saves recomputing it for dk). */
 int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, int B, int D, int L,
-                    int bidirectional, void* y, void* ws, size_t ws_bytes, void* stream);
+                    int bidirectional, void* y, void* uspec, void* ws, size_t ws_bytes,
+                    void* stream);
 /* Gradients of sum(dy * y): du (like u, may be NULL), dk [D, L] fp32 (may be NULL),
- * dbias [D] fp32 (may be NULL). ws: dna_fftconv_workspace(B, D, L) bytes. */
-int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec, int B, int D,
-                    int L, int bidirectional, void* du, float* dk, float* dbias, void* ws,
-                    size_t ws_bytes, void* stream);
+ * dbias [D] fp32 (may be NULL). uspec: the forward's saved input spectrum or NULL (recomputed).
+ * ws: dna_fftconv_workspace(B, D, L) bytes. */
+int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec, const void* uspec,
+                    int B, int D, int L, int bidirectional, void* du, float* dk, float* dbias,
+                    void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------ masked-LM cross entropy
  * Per-row CE over the masked rows only (the model computes logits only for labels>0 rows,
