@@ -108,3 +108,27 @@ def test_train_config_a_runs_on_gpu(data_root, monkeypatch, tmp_path):
                     "train.max_steps=8", "trainer.accumulate_grad_batches=2"])
     tr2 = train.train(cfg2, out=io.StringIO())
     assert tr2.global_step == 8
+
+
+@pytest.mark.parametrize("cdir", [os.path.join(ROOT, "configs"), REF_CONFIGS])
+def test_text_corpus_experiment_builds(cdir, tmp_path, monkeypatch):
+    """experiment=dnabert2/dnabert2_pretrain (text corpus) composes from our
+    configs and, when mounted here, the reference's, and builds the dnabert2_pretrain data module."""
+    if not os.path.isdir(cdir):
+        pytest.skip("reference configs not mounted")
+    import numpy as np
+    import train
+    from dna_amd.compose import compose
+    z = np.load(os.path.join(ROOT, "tests", "golden", "corpus_golden.npz"))
+    d = tmp_path / "dnabert2"
+    d.mkdir()
+    for split in ("train", "dev"):
+        (d / f"{split}.txt").write_text("\n".join(str(s) for s in z["lines"]) + "\n")
+    cfg = compose(cdir, "config", ["experiment=dnabert2/dnabert2_pretrain", "trainer.devices=1",
+                                   "dataset.num_workers=0", "wandb=null",
+                                   "trainer.resume_from_checkpoint=null", f"dataset.text_file={d}"])
+    buf = io.StringIO()
+    train.train(cfg, dry_run=True, out=buf)
+    res = json.loads(buf.getvalue())
+    assert res["train_windows"] == len(z["lines"]) and cfg.dataset.max_length == 128
+    assert list(cfg.optimizer.betas) == [0.9, 0.98] and cfg.scheduler.warmup_t == 60000

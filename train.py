@@ -6,7 +6,8 @@ train() :668-694 -> Lightning fit) for the DNABERT-2 MLM path, without Hydra or 
   * config: dna_amd.compose (defaults lists, @package, overrides, eval/div_up resolvers);
     `--config-dir` may point at the reference's own configs/ tree, which composes unchanged;
   * registries: model "dnabert2" -> dna_amd.bert_layers.BertForMaskedLM (src/utils/registry.py:39),
-    dataset "bert_hg38" -> dna_amd.hg38.BertHG38, task "hg38" + loss "bert_cross_entropy";
+    dataset "bert_hg38" -> dna_amd.hg38.BertHG38, "dnabert2_pretrain" (text corpus) ->
+    dna_amd.corpus.DNABERT2Pretrain, task "hg38" + loss "bert_cross_entropy";
   * loop: MLMTrainer steps (fused loss, bucketed RCCL all-reduce, clip + AdamW, LR schedule per
     optimizer step, `accumulate_grad_batches`), DistributedSampler sharding across ranks
     (one process per GPU, torch.distributed.run), metrics train/loss, trainer/loss,
@@ -50,6 +51,7 @@ def _precision(p):
 
 
 def build_dataset(cfg):
+    import dna_amd.corpus  # noqa: F401  (registers "dnabert2_pretrain")
     from dna_amd.hg38 import SequenceDataset
     kw = {k: v for k, v in cfg.dataset.to_container().items()
           if k != "_name_" and not k.startswith("__")}  # process_config drops "__" keys
