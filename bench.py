@@ -74,11 +74,12 @@ def make_batches(n_batches, batch, rank, device):
     return out
 
 
-def cpu_baseline(seconds_budget=20.0):
+def cpu_baseline(seconds_budget=20.0, threads=None):
     """Oracle restatement (PyTorch CPU fp32, oracle/bert_ref.py, pinned to the reference) timing
     the same step (fwd + bert_cross_entropy + bwd + clip + AdamW, dropout 0.1) on a bounded sample."""
     from oracle import bert_ref
-    threads = min(os.cpu_count() or 1, 16)
+    threads = threads or min(os.cpu_count() or 1, 16)
+    prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     cfg = dict(MODEL_CFG)
@@ -112,6 +113,7 @@ def cpu_baseline(seconds_budget=20.0):
         step(b)
         t_used += time.perf_counter() - t0
         n_seq += b
+    torch.set_num_threads(prev_threads)
     return {"value": round(n_seq / t_used, 4), "unit": "sequences/s", "cores": threads,
             "kind": "port",
             "sample": f"{n_seq} sequences (batches of {b}) of DNABERT-2-117M S=512 fp32 train steps "
@@ -123,7 +125,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("DNA_BENCH_BATCH", 128)))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DNA_BENCH_BATCH", 256)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
@@ -145,7 +147,13 @@ def main():
     torch.manual_seed(2222)
     model = BertForMaskedLM(MODEL_CFG, precision="bf16")
     trainer = MLMTrainer(model, device, lr=5e-4, weight_decay=1e-5, max_grad_norm=1.0)
+    t_data = time.perf_counter()
     batches = make_batches(4, args.batch, rank, device)
+    t_data = time.perf_counter() - t_data
+    data_pipeline = {"seq_per_s": round(4 * args.batch / t_data, 1),
+                     "threads": min(16, os.cpu_count() or 1),
+                     "what": "host tokenize (native BPE, multithreaded) + BERT masking + H2D copy of "
+                             "4096-bp windows, timed before the GPU region (not part of value)"}
 
     for i in range(args.warmup):
         trainer.step(batches[i % len(batches)])
@@ -209,6 +217,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
+        one = cpu_baseline(seconds_budget=12.0, threads=1)  # the reference forces OMP_NUM_THREADS=1
+        cpu["single_thread"] = {"value": one["value"], "cores": 1, "sample": one["sample"]}
 
     if rank == 0:
         line = {
@@ -224,6 +234,7 @@ def main():
             "model_mfu": round(value / world * TRAIN_FLOP_PER_SEQ / 1e12 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(final_loss, 4),
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
+            "data_pipeline": data_pipeline,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
