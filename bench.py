@@ -38,17 +38,23 @@ PEAK_HBM_GBS = 8000.0
 TRAIN_FLOP_PER_SEQ = 3.586e11  # 3 x fwd FLOPs at S=512 incl. last-layer subset
 
 
-def load_traffic():
+def load_traffic(batch):
     """HBM bytes per launch of each timed op family from the newest profiles/r*/traffic.json
-    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench, FETCH_SIZE doubled per the
-    gfx950 correction; scripts/traffic_from_pmc.py). {} when absent."""
+    measured at this per-GPU batch (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this
+    bench, FETCH_SIZE doubled per the gfx950 correction; scripts/traffic_from_pmc.py). {} when
+    there is none for this batch."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")))
-    if not files:
+    d = None
+    for fn in reversed(files):
+        with open(fn) as f:
+            cand = json.load(f)
+        if cand.get("batch") == batch:
+            d = cand
+            break
+    if d is None:
         return {}
-    with open(files[-1]) as f:
-        d = json.load(f)
-    rel = os.path.relpath(files[-1], ROOT)
+    rel = os.path.relpath(fn, ROOT)
     return {k: dict(v, source=rel) for k, v in d.get("families", {}).items()}
 
 
@@ -186,7 +192,7 @@ def main():
     if timer:
         summ = timer.summary()
         total_ms = {k: v[0] * v[1] for k, v in summ.items()}
-        traffic = load_traffic()
+        traffic = load_traffic(args.batch)
         for k, (n, ms, units, kind) in summ.items():
             rate = units / (ms * 1e-3)
             kernels[k] = {"launches_per_step": n / args.steps, "avg_ms": round(ms, 4),

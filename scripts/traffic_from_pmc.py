@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """HBM traffic per op launch from two rocprofv3 --pmc passes over the same bench command.
 
-    python scripts/traffic_from_pmc.py FETCH_DIR WRITE_DIR OUT.json
+    python scripts/traffic_from_pmc.py FETCH_DIR WRITE_DIR OUT.json [BATCH]
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB per dispatch. Per
 MI355X_MICROARCH.md (HBM section) FETCH_SIZE reports exactly half the bytes of 16-B/lane
@@ -55,6 +55,7 @@ def families(disp, scale):
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
+    batch = int(sys.argv[4]) if len(sys.argv) > 4 else None
     fetch = per_dispatch(os.path.join(fdir, "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_dispatch(os.path.join(wdir, "run_counter_collection.csv"), "WRITE_SIZE")
     ft, fc = families(fetch, 2 * 1024.0)   # KiB, x2 gfx950 FETCH_SIZE correction
@@ -70,9 +71,9 @@ def main():
                     "write_bytes_per_launch": int(wt[fam] / wc[fam]) if wc.get(fam) else None,
                     "launches_profiled": int(n)}
     doc = {"method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate "
-                     "passes) over `python bench.py --steps 6 --warmup 2 --no-cpu-baseline`; "
+                     "passes) over `python bench.py --steps 6 --warmup 2 --no-cpu-baseline --batch B`; "
                      "FETCH_SIZE x2 (gfx950 correction), KiB->bytes; includes Infinity-Cache hits",
-           "families": res}
+           "batch": batch, "families": res}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps(doc, indent=1))
