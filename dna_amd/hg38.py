@@ -188,8 +188,11 @@ class BertHG38Dataset(torch.utils.data.Dataset):
             seq = seq - 7
             m = (seq >= 4) | (seq < 0)
             seq[m] = 4
-        if self.replace_N_token:
-            raise NotImplementedError("replace_N_token (char tokenizer only in the reference)")
+        if self.replace_N_token:  # hg38_dataset.py:388-390 (needs the char vocab)
+            vocab = getattr(self.tokenizer, "_vocab_str_to_int", None)
+            if vocab is None:
+                raise AttributeError("replace_N_token needs the char tokenizer (_vocab_str_to_int)")
+            seq = torch.where(seq == vocab["N"], torch.full_like(seq, self.tokenizer.pad_token_id), seq)
         data, target = seq.clone(), seq.clone()
         tok = self.tokenizer
         if self.objective == "stdmlm":
@@ -248,8 +251,14 @@ class BertHG38(SequenceDataset):
     def setup(self, stage=None):
         if self.tokenizer_name == "bpe":
             self.tokenizer = DNABertTokenizer(self.tokenizer_path)
+        elif self.tokenizer_name == "char":  # genomics.py:1132-1138
+            from .tokenizer import CharacterTokenizer
+            self.tokenizer = CharacterTokenizer(characters=["A", "C", "G", "T", "N"],
+                                                model_max_length=self.max_length + 2)
         else:
-            raise NotImplementedError(f"tokenizer_name={self.tokenizer_name!r}: bpe only (SURVEY §8f)")
+            raise NotImplementedError(f"tokenizer_name={self.tokenizer_name!r}: bpe / char "
+                                      "(kmer cannot produce items in the reference's "
+                                      "BertHG38Dataset either, hg38_dataset.py:358-375)")
         self.vocab_size = len(self.tokenizer)
         self.init_datasets()
 
