@@ -51,6 +51,9 @@ _SIGS = {
     "dna_fftconv_filter": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "dna_fftconv_fwd": (_i, [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "dna_fftconv_bwd": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dna_selective_scan_states": (_sz, [_i, _i, _i, _i]),
+    "dna_selective_scan_fwd": (_i, [_vp] * 8 + [_i] * 6 + [_vp] * 4),
+    "dna_selective_scan_bwd": (_i, [_vp] * 8 + [_i] * 6 + [_vp] * 11),
     "dna_xent_fwd": (_i, [_vp, _i, _vp, _i, _i, _vp, _vp, _vp]),
     "dna_xent_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _f, _i, _i, _vp, _vp]),
     "dna_sumsq_workspace": (_sz, [_sz]),

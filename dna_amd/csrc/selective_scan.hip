@@ -1,0 +1,386 @@
+// Mamba selective scan (Caduceus BiMamba, reference src/models/caduceus/modeling_caduceus.py:68-121
+// -> mamba_ssm Mamba.forward -> selective_scan_fn), forward and backward, gfx950.
+//
+//   delta = softplus(delta + delta_bias)                              (optional)
+//   x_t[n] = exp(delta_t A[d,n]) x_{t-1}[n] + delta_t B[b,n,t] u_t     per channel (b, d)
+//   y_t = sum_n C[b,n,t] x_t[n] + D[d] u_t ;   out = y * silu(z)       (z optional)
+//
+// One wave per channel (b, d) walks the sequence in chunks of 64 lanes x 8 positions. For each
+// state n, a lane scans its 8 positions as a product of affine maps x -> a x + b, the wave
+// combines the lanes' (P, S) pairs with a 6-step shuffle scan (earlier map first:
+// (P1,S1) then (P2,S2) = (P1 P2, S1 P2 + S2)), applies the chunk's carry-in state and
+// accumulates y. The forward stores the state at every chunk start (N floats per 512
+// positions) so the backward can recompute the states of one chunk at a time.
+// Backward, chunks in reverse: recompute x within the chunk, then the reverse recurrence of
+// h_t = a_t g_t (g_t = dL/dx_t = C_t dy_t + h_{t+1}) as a suffix scan of the same affine maps,
+// and accumulate du, ddelta, dz, dD, ddelta_bias, dA (per wave, then atomics over the batch) and
+// dB, dC (shared by all channels of a batch: fp32 atomics).
+// Everything in fp32; u/delta/z/B/C/out in fp32 or bf16.
+#include <math.h>
+
+#include "common.h"
+
+namespace dna {
+namespace ssm {
+
+constexpr int ITEMS = 8;
+constexpr int CHUNK = 64 * ITEMS;
+constexpr int WPB = 4;  // waves (channels) per block
+
+struct Args {
+  const void* u; const void* delta; const float* A; const void* B; const void* C;
+  const float* D; const void* z; const float* delta_bias; int softplus;
+  int batch, dim, len;
+  void* out; float* states; float* last_state;
+  // backward
+  const void* dout; void* du; void* ddelta; void* dz; float* dA; float* dB; float* dC;
+  float* dD; float* ddelta_bias;
+};
+
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, int pos, int len, float (&v)[ITEMS]) {
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) v[i] = (pos + i < len) ? to_f32(p[pos + i]) : 0.f;
+}
+template <>
+__device__ __forceinline__ void load8<bf16>(const bf16* p, int pos, int len, float (&v)[ITEMS]) {
+  if (pos + ITEMS <= len && (reinterpret_cast<uintptr_t>(p + pos) & 15) == 0) {
+    const bf16x8 w = *reinterpret_cast<const bf16x8*>(p + pos);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) v[i] = (float)w[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) v[i] = (pos + i < len) ? (float)p[pos + i] : 0.f;
+  }
+}
+template <>
+__device__ __forceinline__ void load8<float>(const float* p, int pos, int len, float (&v)[ITEMS]) {
+  if (pos + ITEMS <= len && (reinterpret_cast<uintptr_t>(p + pos) & 15) == 0) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p + pos);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(p + pos + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[i] = a[i]; v[i + 4] = b[i]; }
+  } else {
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) v[i] = (pos + i < len) ? p[pos + i] : 0.f;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* p, int pos, int len, const float (&v)[ITEMS]) {
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i)
+    if (pos + i < len) p[pos + i] = from_f32<T>(v[i]);
+}
+
+__device__ __forceinline__ float softplus(float x) { return x <= 20.f ? log1pf(__expf(x)) : x; }
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float siluf(float x) { return x * sigmoidf(x); }
+
+// Inclusive wave scan of affine maps (P, S), earlier lanes applied first.
+__device__ __forceinline__ void scan_fwd(float& P, float& S, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float Po = __shfl_up(P, off, 64), So = __shfl_up(S, off, 64);
+    if (lane >= off) {
+      S = fmaf(So, P, S);
+      P = Po * P;
+    }
+  }
+}
+// Inclusive suffix scan (later lanes applied first).
+__device__ __forceinline__ void scan_rev(float& P, float& S, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float Po = __shfl_down(P, off, 64), So = __shfl_down(S, off, 64);
+    if (lane + off < 64) {
+      S = fmaf(So, P, S);
+      P = Po * P;
+    }
+  }
+}
+
+// delta after bias + softplus for one lane's 8 positions (invalid positions -> 0: identity map)
+__device__ __forceinline__ void prep_delta(float (&dl)[ITEMS], float bias, int sp, int pos, int len) {
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    float v = dl[i] + bias;
+    if (sp) v = softplus(v);
+    dl[i] = (pos + i < len) ? v : 0.f;
+  }
+}
+
+template <typename T, int N>
+__global__ __launch_bounds__(64 * WPB) void fwd_kernel(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int ch = blockIdx.x * WPB + (threadIdx.x >> 6);  // b * dim + d
+  if (ch >= a.batch * a.dim) return;
+  const int b = ch / a.dim, d = ch - b * a.dim;
+  const T* u = (const T*)a.u + (size_t)ch * a.len;
+  const T* dlt = (const T*)a.delta + (size_t)ch * a.len;
+  const T* z = a.z ? (const T*)a.z + (size_t)ch * a.len : nullptr;
+  const T* Bm = (const T*)a.B + (size_t)b * N * a.len;
+  const T* Cm = (const T*)a.C + (size_t)b * N * a.len;
+  T* out = (T*)a.out + (size_t)ch * a.len;
+  // per-state scalars live lane-distributed: lane n holds A[d][n] and the carried state x[n]
+  const float Al = lane < N ? a.A[d * N + lane] : 0.f;
+  const float Dd = a.D ? a.D[d] : 0.f;
+  const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+  float xcl = 0.f;  // lane n: state entering the chunk
+  const int nch = (a.len + CHUNK - 1) / CHUNK;
+  for (int c = 0; c < nch; ++c) {
+    const int pos = c * CHUNK + lane * ITEMS;
+    if (a.states && lane < N) a.states[((size_t)ch * nch + c) * N + lane] = xcl;
+    float uu[ITEMS], dl[ITEMS], y[ITEMS];
+    load8(u, pos, a.len, uu);
+    load8(dlt, pos, a.len, dl);
+    prep_delta(dl, bias, a.softplus, pos, a.len);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) y[i] = 0.f;
+#pragma unroll 2
+    for (int n = 0; n < N; ++n) {
+      float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS];
+      load8(Bm + (size_t)n * a.len, pos, a.len, Bv);
+      load8(Cm + (size_t)n * a.len, pos, a.len, Cv);
+      const float An = __shfl(Al, n, 64);
+      float P = 1.f, S = 0.f;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        aa[i] = __expf(dl[i] * An);
+        bb[i] = dl[i] * Bv[i] * uu[i];
+        S = fmaf(aa[i], S, bb[i]);
+        P *= aa[i];
+      }
+      scan_fwd(P, S, lane);
+      // exclusive prefix = inclusive of the previous lane; lane 0 gets the identity
+      float Pe = __shfl_up(P, 1, 64), Se = __shfl_up(S, 1, 64);
+      if (lane == 0) { Pe = 1.f; Se = 0.f; }
+      float x = fmaf(Pe, __shfl(xcl, n, 64), Se);
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        x = fmaf(aa[i], x, bb[i]);
+        y[i] = fmaf(Cv[i], x, y[i]);
+      }
+      const float xe = __shfl(x, 63, 64);
+      if (lane == n) xcl = xe;
+    }
+    float o[ITEMS];
+    if (z) {
+      float zz[ITEMS];
+      load8(z, pos, a.len, zz);
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) o[i] = fmaf(Dd, uu[i], y[i]) * siluf(zz[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) o[i] = fmaf(Dd, uu[i], y[i]);
+    }
+    store8(out, pos, a.len, o);
+  }
+  if (a.last_state && lane < N) a.last_state[(size_t)ch * N + lane] = xcl;
+}
+
+template <typename T, int N>
+__global__ __launch_bounds__(64 * WPB) void bwd_kernel(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int ch = blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (ch >= a.batch * a.dim) return;
+  const int b = ch / a.dim, d = ch - b * a.dim;
+  const size_t off = (size_t)ch * a.len;
+  const T* u = (const T*)a.u + off;
+  const T* dlt = (const T*)a.delta + off;
+  const T* z = a.z ? (const T*)a.z + off : nullptr;
+  const T* dout = (const T*)a.dout + off;
+  const T* Bm = (const T*)a.B + (size_t)b * N * a.len;
+  const T* Cm = (const T*)a.C + (size_t)b * N * a.len;
+  float* dBm = a.dB + (size_t)b * N * a.len;
+  float* dCm = a.dC + (size_t)b * N * a.len;
+  const float Al = lane < N ? a.A[d * N + lane] : 0.f;  // lane-distributed per-state scalars
+  const float Dd = a.D ? a.D[d] : 0.f;
+  const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+  const int nch = (a.len + CHUNK - 1) / CHUNK;
+  float hcl = 0.f;    // lane n: h_{t1+1} entering the chunk from the right
+  float dAl = 0.f;    // lane n: dA[d][n] partial
+  float dDacc = 0.f, dbacc = 0.f;
+  for (int c = nch - 1; c >= 0; --c) {
+    const int pos = c * CHUNK + lane * ITEMS;
+    float uu[ITEMS], dr[ITEMS], dl[ITEMS], go[ITEMS], dy[ITEMS];
+    load8(u, pos, a.len, uu);
+    load8(dlt, pos, a.len, dr);
+    load8(dout, pos, a.len, go);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) dl[i] = dr[i];
+    prep_delta(dl, bias, a.softplus, pos, a.len);
+    // recompute y (needed for dz) alongside the states; dy = d(out)/d(y + D u)
+    float zz[ITEMS], sz[ITEMS];
+    if (z) {
+      load8(z, pos, a.len, zz);
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) { sz[i] = siluf(zz[i]); dy[i] = go[i] * sz[i]; }
+    } else {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) dy[i] = go[i];
+    }
+    float ddl[ITEMS], du[ITEMS], y[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) { ddl[i] = 0.f; du[i] = Dd * dy[i]; y[i] = 0.f; dDacc = fmaf(dy[i], uu[i], dDacc); }
+#pragma unroll 1
+    for (int n = 0; n < N; ++n) {
+      float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
+      load8(Bm + (size_t)n * a.len, pos, a.len, Bv);
+      load8(Cm + (size_t)n * a.len, pos, a.len, Cv);
+      const float An = __shfl(Al, n, 64);
+      // forward states within the chunk from the stored chunk-start state
+      float P = 1.f, S = 0.f;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        aa[i] = __expf(dl[i] * An);
+        bb[i] = dl[i] * Bv[i] * uu[i];
+        S = fmaf(aa[i], S, bb[i]);
+        P *= aa[i];
+      }
+      scan_fwd(P, S, lane);
+      float Pe = __shfl_up(P, 1, 64), Se = __shfl_up(S, 1, 64);
+      if (lane == 0) { Pe = 1.f; Se = 0.f; }
+      const float x0 = a.states[((size_t)ch * nch + c) * N + n];
+      float xprev = fmaf(Pe, x0, Se);  // x_{t-1} for the lane's first position
+      float x = xprev;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        x = fmaf(aa[i], x, bb[i]);
+        xs[i] = x;
+        y[i] = fmaf(Cv[i], x, y[i]);
+      }
+      // reverse: h_t = a_t (c_t + h_{t+1}), c_t = C_t dy_t; lane-local suffix map then wave suffix scan
+      float Pr = 1.f, Sr = 0.f;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) {
+        Sr = aa[i] * (Cv[i] * dy[i] + Sr);
+        Pr *= aa[i];
+      }
+      scan_rev(Pr, Sr, lane);
+      float Pn = __shfl_down(Pr, 1, 64), Sn = __shfl_down(Sr, 1, 64);
+      if (lane == 63) { Pn = 1.f; Sn = 0.f; }
+      float h = fmaf(Pn, __shfl(hcl, n, 64), Sn);  // h_{t+1} for the lane's last position
+      float dAn = 0.f;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) {
+        const float g = fmaf(Cv[i], dy[i], h);                 // dL/dx_t
+        const float xm1 = i > 0 ? xs[i - 1] : xprev;           // x_{t-1}
+        const float da = g * xm1 * aa[i];                      // dL/d(delta A) via a_t
+        ddl[i] = fmaf(da, An, ddl[i]);
+        dAn = fmaf(da, dl[i], dAn);
+        const float gb = g * dl[i];
+        ddl[i] = fmaf(g, Bv[i] * uu[i], ddl[i]);
+        du[i] = fmaf(gb, Bv[i], du[i]);
+        if (pos + i < a.len) {
+          atomicAdd(dBm + (size_t)n * a.len + pos + i, gb * uu[i]);
+          atomicAdd(dCm + (size_t)n * a.len + pos + i, dy[i] * xs[i]);
+        }
+        h = aa[i] * g;
+      }
+      const float dAs = wave_sum(dAn);
+      const float h0 = __shfl(h, 0, 64);
+      if (lane == n) { dAl += dAs; hcl = h0; }
+    }
+    // delta bias / softplus chain
+    float dd[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      float g = ddl[i];
+      if (a.softplus) g *= sigmoidf(dr[i] + bias);
+      dd[i] = (pos + i < a.len) ? g : 0.f;
+      dbacc += dd[i];
+    }
+    store8((T*)a.ddelta + off, pos, a.len, dd);
+    store8((T*)a.du + off, pos, a.len, du);
+    if (z && a.dz) {
+      float dzv[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const float s = sigmoidf(zz[i]);
+        const float pre = fmaf(Dd, uu[i], y[i]);
+        dzv[i] = go[i] * pre * s * (1.f + zz[i] * (1.f - s));
+      }
+      store8((T*)a.dz + off, pos, a.len, dzv);
+    }
+  }
+  // per-channel reductions over the wave, then over the batch (atomics)
+  if (lane < N) atomicAdd(a.dA + d * N + lane, dAl);
+  dDacc = wave_sum(dDacc);
+  dbacc = wave_sum(dbacc);
+  if (lane == 0) {
+    if (a.dD) atomicAdd(a.dD + d, dDacc);
+    if (a.ddelta_bias) atomicAdd(a.ddelta_bias + d, dbacc);
+  }
+}
+
+template <typename F>
+int dispatch(int dtype, int n, F&& f) {
+  if (dtype != DNA_F32 && dtype != DNA_BF16) return -1;
+  switch (n) {
+    case 4: dtype == DNA_F32 ? f(float(), std::integral_constant<int, 4>()) : f(bf16(), std::integral_constant<int, 4>()); return 0;
+    case 8: dtype == DNA_F32 ? f(float(), std::integral_constant<int, 8>()) : f(bf16(), std::integral_constant<int, 8>()); return 0;
+    case 16: dtype == DNA_F32 ? f(float(), std::integral_constant<int, 16>()) : f(bf16(), std::integral_constant<int, 16>()); return 0;
+    default: return -1;
+  }
+}
+
+}  // namespace ssm
+}  // namespace dna
+
+using namespace dna;
+using namespace dna::ssm;
+
+extern "C" size_t dna_selective_scan_states(int batch, int dim, int len, int d_state) {
+  if (batch <= 0 || dim <= 0 || len <= 0 || d_state <= 0) return 0;
+  return (size_t)batch * dim * ((len + CHUNK - 1) / CHUNK) * d_state;
+}
+
+extern "C" int dna_selective_scan_fwd(const void* u, const void* delta, const float* A, const void* B,
+                                      const void* C, const float* D, const void* z,
+                                      const float* delta_bias, int delta_softplus, int dtype,
+                                      int batch, int dim, int len, int d_state, void* out,
+                                      float* states, float* last_state, void* stream) {
+  DNA_CHECK_ARG(u && delta && A && B && C && out, "dna_selective_scan_fwd: null pointer");
+  DNA_CHECK_ARG(batch > 0 && dim > 0 && len > 0, "dna_selective_scan_fwd: bad shape");
+  Args a{};
+  a.u = u; a.delta = delta; a.A = A; a.B = B; a.C = C; a.D = D; a.z = z; a.delta_bias = delta_bias;
+  a.softplus = delta_softplus; a.batch = batch; a.dim = dim; a.len = len;
+  a.out = out; a.states = states; a.last_state = last_state;
+  const dim3 grid((batch * dim + WPB - 1) / WPB);
+  hipStream_t s = as_stream(stream);
+  const int st = dispatch(dtype, d_state, [&](auto t, auto n) {
+    hipLaunchKernelGGL((fwd_kernel<decltype(t), decltype(n)::value>), grid, dim3(64 * WPB), 0, s, a);
+  });
+  DNA_CHECK_ARG(st == 0, "dna_selective_scan_fwd: d_state %d / dtype %d unsupported (4, 8, 16; f32/bf16)",
+                d_state, dtype);
+  DNA_LAUNCH_CHECK("dna_selective_scan_fwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_selective_scan_bwd(const void* u, const void* delta, const float* A, const void* B,
+                                      const void* C, const float* D, const void* z,
+                                      const float* delta_bias, int delta_softplus, int dtype,
+                                      int batch, int dim, int len, int d_state, const float* states,
+                                      const void* dout, void* du, void* ddelta, float* dA, float* dB,
+                                      float* dC, float* dD, void* dz, float* ddelta_bias,
+                                      void* stream) {
+  DNA_CHECK_ARG(u && delta && A && B && C && states && dout && du && ddelta && dA && dB && dC,
+                "dna_selective_scan_bwd: null pointer");
+  DNA_CHECK_ARG(batch > 0 && dim > 0 && len > 0, "dna_selective_scan_bwd: bad shape");
+  DNA_CHECK_ARG(!z || dz, "dna_selective_scan_bwd: dz required with z");
+  Args a{};
+  a.u = u; a.delta = delta; a.A = A; a.B = B; a.C = C; a.D = D; a.z = z; a.delta_bias = delta_bias;
+  a.softplus = delta_softplus; a.batch = batch; a.dim = dim; a.len = len;
+  a.states = const_cast<float*>(states);
+  a.dout = dout; a.du = du; a.ddelta = ddelta; a.dz = dz; a.dA = dA; a.dB = dB; a.dC = dC;
+  a.dD = dD; a.ddelta_bias = ddelta_bias;
+  const dim3 grid((batch * dim + WPB - 1) / WPB);
+  hipStream_t s = as_stream(stream);
+  const int st = dispatch(dtype, d_state, [&](auto t, auto n) {
+    hipLaunchKernelGGL((bwd_kernel<decltype(t), decltype(n)::value>), grid, dim3(64 * WPB), 0, s, a);
+  });
+  DNA_CHECK_ARG(st == 0, "dna_selective_scan_bwd: d_state %d / dtype %d unsupported (4, 8, 16; f32/bf16)",
+                d_state, dtype);
+  DNA_LAUNCH_CHECK("dna_selective_scan_bwd");
+  return DNA_OK;
+}

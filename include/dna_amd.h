@@ -185,6 +185,29 @@ int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec,
                     int B, int D, int L, int bidirectional, void* du, float* dk, float* dbias,
                     void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------ Mamba selective scan (Caduceus)
+ * selective_scan_fn as called by mamba_ssm Mamba.forward inside Caduceus' BiMambaWrapper
+ * (src/models/caduceus/modeling_caduceus.py:68-121; mamba_ssm is external and not vendored):
+ *   delta = softplus(delta + delta_bias) (if delta_softplus; bias may be NULL)
+ *   x_t = exp(delta_t A) x_{t-1} + delta_t B_t u_t ;  out_t = (C_t . x_t + D u_t) * silu(z_t)
+ * u, delta, z, out [batch, dim, len] (dtype), A [dim, d_state] fp32, B, C [batch, d_state, len]
+ * (dtype), D, delta_bias [dim] fp32 (NULL allowed; z NULL = no gating). d_state in {4, 8, 16}.
+ * states: dna_selective_scan_states() floats, chunk-start states for the backward (NULL to skip);
+ * last_state [batch, dim, d_state] fp32 or NULL. */
+size_t dna_selective_scan_states(int batch, int dim, int len, int d_state);
+int dna_selective_scan_fwd(const void* u, const void* delta, const float* A, const void* B,
+                           const void* C, const float* D, const void* z, const float* delta_bias,
+                           int delta_softplus, int dtype, int batch, int dim, int len, int d_state,
+                           void* out, float* states, float* last_state, void* stream);
+/* Backward from the forward's states. du, ddelta, dz (dtype) are written; dA [dim, d_state],
+ * dB, dC [batch, d_state, len], dD, ddelta_bias [dim] (fp32) are ACCUMULATED (+=, zero them). */
+int dna_selective_scan_bwd(const void* u, const void* delta, const float* A, const void* B,
+                           const void* C, const float* D, const void* z, const float* delta_bias,
+                           int delta_softplus, int dtype, int batch, int dim, int len, int d_state,
+                           const float* states, const void* dout, void* du, void* ddelta,
+                           float* dA, float* dB, float* dC, float* dD, void* dz,
+                           float* ddelta_bias, void* stream);
+
 /* ------------------------------------------------------------------ masked-LM cross entropy
  * Per-row CE over the masked rows only (the model computes logits only for labels>0 rows,
  * bert_layers.py:795,:820-824; task loss bert_cross_entropy, src/tasks/metrics.py:268-273).
