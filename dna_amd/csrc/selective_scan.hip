@@ -313,6 +313,426 @@ __global__ __launch_bounds__(64 * WPB) void bwd_kernel(Args a) {
   }
 }
 
+// ------------------------------------------------------------------ chunk-parallel path
+// One wave per channel exposes only batch*dim waves, one per SIMD at Caduceus sizes, so the
+// shuffle scans above run latency-bound. When dim % 8 == 0 and a states buffer is given, the
+// chunk index becomes a grid dimension instead:
+//   1. summary   (b, chunk, group): per channel, Σδ over the chunk and, per state, the chunk's end
+//                state from a zero start  S = Σ_t exp(A (Δ_end - Δ_t)) δ_t B_t u_t
+//                (backward: R = Σ_t exp(A Δ_t) C_t dy_t, the chunk's h at its first position
+//                from a zero right boundary);
+//   2. carry     (channel, state), sequential over chunks, in place: x_c <- x at chunk c start
+//                (backward: h entering chunk c from the right), decay exp(A Σδ_c);
+//   3. chunk     (b, chunk, group): the per-chunk forward / backward above from those carries.
+// A block is 8 waves over a group of G = 8k channels of one batch row: B/C of the chunk are
+// staged in LDS once for all G channels, and the backward reduces dB/dC over the group in LDS
+// before one global atomic per element.
+// states buffer (dna_selective_scan_states floats): [x0: ch*nch*N][h: ch*nch*N][Σδ: ch*nch].
+constexpr int CW = 8;           // waves per block
+constexpr int CT = 64 * CW;     // threads per block
+
+struct Chunked {
+  int nch, groups, k;  // chunks, channel groups per batch row, channels per wave
+};
+
+// stage one [N][CHUNK] matrix slice (chunk c of the rows M[n*len ...]) into LDS
+template <typename T, int N>
+__device__ __forceinline__ void stage(T* lds, const T* M, int c, int len) {
+  constexpr int VE = 16 / sizeof(T);
+  constexpr int NV = N * CHUNK / VE;
+  for (int vi = threadIdx.x; vi < NV; vi += CT) {
+    const int e = vi * VE;
+    const int n = e / CHUNK, p = e - n * CHUNK;
+    const int gp = c * CHUNK + p;
+    const T* src = M + (size_t)n * len + gp;
+    uint4 v;
+    if (gp + VE <= len && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      v = *reinterpret_cast<const uint4*>(src);
+    } else {
+      T tmp[VE];
+#pragma unroll
+      for (int q = 0; q < VE; ++q) tmp[q] = (gp + q < len) ? src[q] : from_f32<T>(0.f);
+      v = *reinterpret_cast<const uint4*>(tmp);
+    }
+    *reinterpret_cast<uint4*>(lds + e) = v;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void lds8(const T* p, float (&v)[ITEMS]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 w = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) v[i] = (float)w[i];
+  } else {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+    const f32x4 y = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[i] = x[i]; v[i + 4] = y[i]; }
+  }
+}
+
+// lane-level sums of δ: exclusive prefix (lanes before) and exclusive suffix (lanes after),
+// each summed directly (no differences of large prefix sums), and the chunk total
+__device__ __forceinline__ void delta_sums(float tl, int lane, float& pre, float& suf, float& tot) {
+  float inc = tl, sinc = tl;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float a = __shfl_up(inc, off, 64), b = __shfl_down(sinc, off, 64);
+    if (lane >= off) inc += a;
+    if (lane + off < 64) sinc += b;
+  }
+  pre = inc - tl;     // exact enough: inc and tl are one lane's own values
+  suf = sinc - tl;
+  tot = __shfl(inc, 63, 64);
+}
+
+template <typename T, int N>
+__global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
+  __shared__ __attribute__((aligned(16))) T Bs[N * CHUNK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y, b = blockIdx.z;
+  const size_t nchN = (size_t)q.nch * N;
+  float* Sbuf = a.states;
+  float* dsum = a.states + 2 * (size_t)a.batch * a.dim * nchN;
+  stage<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
+  __syncthreads();
+  const int pos = c * CHUNK + lane * ITEMS;
+  for (int j = 0; j < q.k; ++j) {
+    const int d = blockIdx.x * CW * q.k + j * CW + w;
+    const int ch = b * a.dim + d;
+    const float Al = lane < N ? a.A[d * N + lane] : 0.f;
+    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    float uu[ITEMS], dl[ITEMS];
+    load8((const T*)a.u + (size_t)ch * a.len, pos, a.len, uu);
+    load8((const T*)a.delta + (size_t)ch * a.len, pos, a.len, dl);
+    prep_delta(dl, bias, a.softplus, pos, a.len);
+    float tl = 0.f;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) { tl += dl[i]; uu[i] *= dl[i]; }  // uu <- δ u
+    float pre, suf, tot;
+    delta_sums(tl, lane, pre, suf, tot);
+    float Sl = 0.f;
+#pragma unroll 4
+    for (int n = 0; n < N; ++n) {
+      float Bv[ITEMS];
+      lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
+      const float An = __shfl(Al, n, 64);
+      float x = 0.f;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) x = fmaf(__expf(dl[i] * An), x, uu[i] * Bv[i]);
+      const float S = wave_sum(x * __expf(An * suf));
+      if (lane == n) Sl = S;
+    }
+    if (lane < N) Sbuf[(size_t)ch * nchN + (size_t)c * N + lane] = Sl;
+    if (lane == 0) dsum[(size_t)ch * q.nch + c] = tot;
+  }
+}
+
+template <typename T, int N>
+__global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
+  __shared__ __attribute__((aligned(16))) T Cs[N * CHUNK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y, b = blockIdx.z;
+  const size_t nchN = (size_t)q.nch * N;
+  float* Rbuf = a.states + (size_t)a.batch * a.dim * nchN;
+  stage<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
+  __syncthreads();
+  const int pos = c * CHUNK + lane * ITEMS;
+  for (int j = 0; j < q.k; ++j) {
+    const int d = blockIdx.x * CW * q.k + j * CW + w;
+    const int ch = b * a.dim + d;
+    const float Al = lane < N ? a.A[d * N + lane] : 0.f;
+    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    float dl[ITEMS], dy[ITEMS];
+    load8((const T*)a.delta + (size_t)ch * a.len, pos, a.len, dl);
+    load8((const T*)a.dout + (size_t)ch * a.len, pos, a.len, dy);
+    prep_delta(dl, bias, a.softplus, pos, a.len);
+    if (a.z) {
+      float zz[ITEMS];
+      load8((const T*)a.z + (size_t)ch * a.len, pos, a.len, zz);
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) dy[i] *= siluf(zz[i]);
+    }
+    float tl = 0.f;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) tl += dl[i];
+    float pre, suf, tot;
+    delta_sums(tl, lane, pre, suf, tot);
+    float Rl = 0.f;
+#pragma unroll 4
+    for (int n = 0; n < N; ++n) {
+      float Cv[ITEMS];
+      lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
+      const float An = __shfl(Al, n, 64);
+      float r = 0.f;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) r = __expf(dl[i] * An) * fmaf(Cv[i], dy[i], r);
+      const float R = wave_sum(r * __expf(An * pre));
+      if (lane == n) Rl = R;
+    }
+    if (lane < N) Rbuf[(size_t)ch * nchN + (size_t)c * N + lane] = Rl;
+  }
+}
+
+// one thread per (channel, state): region <- carries, in place (read the summary, then write)
+template <int N>
+__global__ __launch_bounds__(256) void carry_kernel(Args a, Chunked q, int reverse) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= a.batch * a.dim * N) return;
+  const int ch = idx / N, n = idx - ch * N, d = ch % a.dim;
+  const size_t nchN = (size_t)q.nch * N;
+  float* buf = a.states + (reverse ? (size_t)a.batch * a.dim * nchN : 0) + (size_t)ch * nchN + n;
+  const float* dsum = a.states + 2 * (size_t)a.batch * a.dim * nchN + (size_t)ch * q.nch;
+  const float An = a.A[d * N + n];
+  float x = 0.f;
+  constexpr int U = 8;
+  for (int s0 = 0; s0 < q.nch; s0 += U) {
+    float sv[U], pv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = reverse ? q.nch - 1 - (s0 + u) : s0 + u;
+      const bool ok = s0 + u < q.nch;
+      sv[u] = ok ? buf[(size_t)c * N] : 0.f;
+      pv[u] = ok ? __expf(An * dsum[c]) : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = reverse ? q.nch - 1 - (s0 + u) : s0 + u;
+      if (s0 + u < q.nch) buf[(size_t)c * N] = x;
+      x = fmaf(pv[u], x, sv[u]);
+    }
+  }
+  if (!reverse && a.last_state) a.last_state[(size_t)ch * N + n] = x;
+}
+
+template <typename T, int N>
+__global__ __launch_bounds__(CT) void chunk_fwd_kernel(Args a, Chunked q) {
+  __shared__ __attribute__((aligned(16))) T Bs[N * CHUNK];
+  __shared__ __attribute__((aligned(16))) T Cs[N * CHUNK];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y, b = blockIdx.z;
+  const size_t nchN = (size_t)q.nch * N;
+  stage<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
+  stage<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
+  __syncthreads();
+  const int pos = c * CHUNK + lane * ITEMS;
+  for (int j = 0; j < q.k; ++j) {
+    const int d = blockIdx.x * CW * q.k + j * CW + w;
+    const int ch = b * a.dim + d;
+    const size_t off = (size_t)ch * a.len;
+    const float Al = lane < N ? a.A[d * N + lane] : 0.f;
+    const float Dd = a.D ? a.D[d] : 0.f;
+    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    const float xcl = lane < N ? a.states[(size_t)ch * nchN + (size_t)c * N + lane] : 0.f;
+    float uu[ITEMS], dl[ITEMS], y[ITEMS];
+    load8((const T*)a.u + off, pos, a.len, uu);
+    load8((const T*)a.delta + off, pos, a.len, dl);
+    prep_delta(dl, bias, a.softplus, pos, a.len);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) y[i] = 0.f;
+#pragma unroll 2
+    for (int n = 0; n < N; ++n) {
+      float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS];
+      lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
+      lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
+      const float An = __shfl(Al, n, 64);
+      float P = 1.f, S = 0.f;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        aa[i] = __expf(dl[i] * An);
+        bb[i] = dl[i] * Bv[i] * uu[i];
+        S = fmaf(aa[i], S, bb[i]);
+        P *= aa[i];
+      }
+      scan_fwd(P, S, lane);
+      float Pe = __shfl_up(P, 1, 64), Se = __shfl_up(S, 1, 64);
+      if (lane == 0) { Pe = 1.f; Se = 0.f; }
+      float x = fmaf(Pe, __shfl(xcl, n, 64), Se);
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        x = fmaf(aa[i], x, bb[i]);
+        y[i] = fmaf(Cv[i], x, y[i]);
+      }
+    }
+    float o[ITEMS];
+    if (a.z) {
+      float zz[ITEMS];
+      load8((const T*)a.z + off, pos, a.len, zz);
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) o[i] = fmaf(Dd, uu[i], y[i]) * siluf(zz[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) o[i] = fmaf(Dd, uu[i], y[i]);
+    }
+    store8((T*)a.out + off, pos, a.len, o);
+  }
+}
+
+template <typename T, int N>
+__global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // dB/dC partials of the group: [R copies][2 (dB, dC)][N][ITEMS][64] fp32; position
+  // lane*ITEMS+i lives at slot i*64+lane (each wave access = 64 consecutive words). No LDS
+  // atomics (ds_add_f32 runs ~4x slower than the whole rest of this kernel): in state step s
+  // wave w owns state (s + w) % N of copy w / N, and a barrier ends every step, so each
+  // accumulator slot has one writer at a time and is updated with a plain read-modify-write.
+  constexpr int R = CW > N ? CW / N : 1;
+  float* acc = reinterpret_cast<float*>(smem);
+  T* Bs = reinterpret_cast<T*>(acc + R * 2 * N * CHUNK);   // [N][CHUNK]
+  T* Cs = Bs + N * CHUNK;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y, b = blockIdx.z;
+  const size_t nchN = (size_t)q.nch * N;
+  const float* hbuf = a.states + (size_t)a.batch * a.dim * nchN;
+  for (int e = threadIdx.x; e < R * 2 * N * CHUNK; e += CT) acc[e] = 0.f;
+  float* accw = acc + (w / N) * 2 * N * CHUNK;
+  stage<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
+  stage<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
+  __syncthreads();
+  const int pos = c * CHUNK + lane * ITEMS;
+  for (int j = 0; j < q.k; ++j) {
+    const int d = blockIdx.x * CW * q.k + j * CW + w;
+    const int ch = b * a.dim + d;
+    const size_t off = (size_t)ch * a.len;
+    const float Al = lane < N ? a.A[d * N + lane] : 0.f;
+    const float Dd = a.D ? a.D[d] : 0.f;
+    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    const float xcl = lane < N ? a.states[(size_t)ch * nchN + (size_t)c * N + lane] : 0.f;
+    const float hcl = lane < N ? hbuf[(size_t)ch * nchN + (size_t)c * N + lane] : 0.f;
+    float uu[ITEMS], dr[ITEMS], dl[ITEMS], go[ITEMS], dy[ITEMS];
+    load8((const T*)a.u + off, pos, a.len, uu);
+    load8((const T*)a.delta + off, pos, a.len, dr);
+    load8((const T*)a.dout + off, pos, a.len, go);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) dl[i] = dr[i];
+    prep_delta(dl, bias, a.softplus, pos, a.len);
+    float zz[ITEMS];
+    if (a.z) {
+      load8((const T*)a.z + off, pos, a.len, zz);
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) dy[i] = go[i] * siluf(zz[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) dy[i] = go[i];
+    }
+    float ddl[ITEMS], du[ITEMS], y[ITEMS];
+    float dDacc = 0.f, dAl = 0.f;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) { ddl[i] = 0.f; du[i] = Dd * dy[i]; y[i] = 0.f; dDacc = fmaf(dy[i], uu[i], dDacc); }
+#pragma unroll 1
+    for (int st = 0; st < N; ++st) {
+      const int n = (st + w) % N;
+      float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
+      lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
+      lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
+      const float An = __shfl(Al, n, 64);
+      float P = 1.f, S = 0.f;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        aa[i] = __expf(dl[i] * An);
+        bb[i] = dl[i] * Bv[i] * uu[i];
+        S = fmaf(aa[i], S, bb[i]);
+        P *= aa[i];
+      }
+      scan_fwd(P, S, lane);
+      float Pe = __shfl_up(P, 1, 64), Se = __shfl_up(S, 1, 64);
+      if (lane == 0) { Pe = 1.f; Se = 0.f; }
+      const float xprev = fmaf(Pe, __shfl(xcl, n, 64), Se);
+      float x = xprev;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        x = fmaf(aa[i], x, bb[i]);
+        xs[i] = x;
+        y[i] = fmaf(Cv[i], x, y[i]);
+      }
+      float Pr = 1.f, Sr = 0.f;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) {
+        Sr = aa[i] * (Cv[i] * dy[i] + Sr);
+        Pr *= aa[i];
+      }
+      scan_rev(Pr, Sr, lane);
+      float Pn = __shfl_down(Pr, 1, 64), Sn = __shfl_down(Sr, 1, 64);
+      if (lane == 63) { Pn = 1.f; Sn = 0.f; }
+      float h = fmaf(Pn, __shfl(hcl, n, 64), Sn);
+      float dAn = 0.f;
+      float* aB = accw + n * CHUNK + lane;
+      float* aC = aB + N * CHUNK;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) {
+        const float g = fmaf(Cv[i], dy[i], h);
+        const float xm1 = i > 0 ? xs[i - 1] : xprev;
+        const float da = g * xm1 * aa[i];
+        ddl[i] = fmaf(da, An, ddl[i]);
+        dAn = fmaf(da, dl[i], dAn);
+        const float gb = g * dl[i];
+        ddl[i] = fmaf(g, Bv[i] * uu[i], ddl[i]);
+        du[i] = fmaf(gb, Bv[i], du[i]);
+        aB[i * 64] += gb * uu[i];   // exclusive this step (see the state rotation above)
+        aC[i * 64] += dy[i] * xs[i];
+        h = aa[i] * g;
+      }
+      const float dAs = wave_sum(dAn);
+      if (lane == n) dAl = dAs;
+      __syncthreads();
+    }
+    float dd[ITEMS], dbacc = 0.f;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      float g = ddl[i];
+      if (a.softplus) g *= sigmoidf(dr[i] + bias);
+      dd[i] = (pos + i < a.len) ? g : 0.f;
+      dbacc += dd[i];
+    }
+    store8((T*)a.ddelta + off, pos, a.len, dd);
+    store8((T*)a.du + off, pos, a.len, du);
+    if (a.z && a.dz) {
+      float dzv[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const float s = sigmoidf(zz[i]);
+        const float pre = fmaf(Dd, uu[i], y[i]);
+        dzv[i] = go[i] * pre * s * (1.f + zz[i] * (1.f - s));
+      }
+      store8((T*)a.dz + off, pos, a.len, dzv);
+    }
+    if (lane < N) atomicAdd(a.dA + d * N + lane, dAl);
+    dDacc = wave_sum(dDacc);
+    dbacc = wave_sum(dbacc);
+    if (lane == 0) {
+      if (a.dD) atomicAdd(a.dD + d, dDacc);
+      if (a.ddelta_bias) atomicAdd(a.ddelta_bias + d, dbacc);
+    }
+  }
+  __syncthreads();
+  float* dBm = a.dB + (size_t)b * N * a.len;
+  float* dCm = a.dC + (size_t)b * N * a.len;
+  for (int e = threadIdx.x; e < 2 * N * CHUNK; e += CT) {
+    const int mat = e / (N * CHUNK), rem = e - mat * (N * CHUNK);
+    const int n = rem / CHUNK, p = rem - n * CHUNK;  // p: position within the chunk
+    const int gp = c * CHUNK + p;
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v += acc[(r * 2 + mat) * N * CHUNK + n * CHUNK + (p % ITEMS) * 64 + p / ITEMS];
+    if (gp < a.len) atomicAdd((mat ? dCm : dBm) + (size_t)n * a.len + gp, v);
+  }
+}
+
+inline Chunked plan_chunks(int batch, int dim, int len) {
+  Chunked q;
+  q.nch = (len + CHUNK - 1) / CHUNK;
+  q.k = 8;
+  while (q.k > 1 && (dim % (CW * q.k) != 0 || (long)batch * q.nch * (dim / (CW * q.k)) < 2048)) q.k >>= 1;
+  q.groups = dim / (CW * q.k);
+  return q;
+}
+
+template <typename K>
+inline void allow_lds(K k, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 template <typename F>
 int dispatch(int dtype, int n, F&& f) {
   if (dtype != DNA_F32 && dtype != DNA_BF16) return -1;
@@ -332,7 +752,7 @@ using namespace dna::ssm;
 
 extern "C" size_t dna_selective_scan_states(int batch, int dim, int len, int d_state) {
   if (batch <= 0 || dim <= 0 || len <= 0 || d_state <= 0) return 0;
-  return (size_t)batch * dim * ((len + CHUNK - 1) / CHUNK) * d_state;
+  return (size_t)batch * dim * ((len + CHUNK - 1) / CHUNK) * (2 * d_state + 1);
 }
 
 extern "C" int dna_selective_scan_fwd(const void* u, const void* delta, const float* A, const void* B,
@@ -346,10 +766,21 @@ extern "C" int dna_selective_scan_fwd(const void* u, const void* delta, const fl
   a.u = u; a.delta = delta; a.A = A; a.B = B; a.C = C; a.D = D; a.z = z; a.delta_bias = delta_bias;
   a.softplus = delta_softplus; a.batch = batch; a.dim = dim; a.len = len;
   a.out = out; a.states = states; a.last_state = last_state;
-  const dim3 grid((batch * dim + WPB - 1) / WPB);
   hipStream_t s = as_stream(stream);
+  const bool chunked = states && dim % CW == 0;
+  const Chunked q = plan_chunks(batch, dim, len);
+  const dim3 cgrid(q.groups, q.nch, batch);
   const int st = dispatch(dtype, d_state, [&](auto t, auto n) {
-    hipLaunchKernelGGL((fwd_kernel<decltype(t), decltype(n)::value>), grid, dim3(64 * WPB), 0, s, a);
+    using T = decltype(t);
+    constexpr int NS = decltype(n)::value;
+    if (chunked) {
+      hipLaunchKernelGGL((sum_fwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
+      hipLaunchKernelGGL((carry_kernel<NS>), dim3((batch * dim * NS + 255) / 256), dim3(256), 0, s, a, q, 0);
+      hipLaunchKernelGGL((chunk_fwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
+    } else {
+      hipLaunchKernelGGL((fwd_kernel<T, NS>), dim3((batch * dim + WPB - 1) / WPB), dim3(64 * WPB),
+                         0, s, a);
+    }
   });
   DNA_CHECK_ARG(st == 0, "dna_selective_scan_fwd: d_state %d / dtype %d unsupported (4, 8, 16; f32/bf16)",
                 d_state, dtype);
@@ -360,7 +791,7 @@ extern "C" int dna_selective_scan_fwd(const void* u, const void* delta, const fl
 extern "C" int dna_selective_scan_bwd(const void* u, const void* delta, const float* A, const void* B,
                                       const void* C, const float* D, const void* z,
                                       const float* delta_bias, int delta_softplus, int dtype,
-                                      int batch, int dim, int len, int d_state, const float* states,
+                                      int batch, int dim, int len, int d_state, float* states,
                                       const void* dout, void* du, void* ddelta, float* dA, float* dB,
                                       float* dC, float* dD, void* dz, float* ddelta_bias,
                                       void* stream) {
@@ -371,13 +802,27 @@ extern "C" int dna_selective_scan_bwd(const void* u, const void* delta, const fl
   Args a{};
   a.u = u; a.delta = delta; a.A = A; a.B = B; a.C = C; a.D = D; a.z = z; a.delta_bias = delta_bias;
   a.softplus = delta_softplus; a.batch = batch; a.dim = dim; a.len = len;
-  a.states = const_cast<float*>(states);
+  a.states = states;
   a.dout = dout; a.du = du; a.ddelta = ddelta; a.dz = dz; a.dA = dA; a.dB = dB; a.dC = dC;
   a.dD = dD; a.ddelta_bias = ddelta_bias;
-  const dim3 grid((batch * dim + WPB - 1) / WPB);
   hipStream_t s = as_stream(stream);
+  const bool chunked = dim % CW == 0;
+  const Chunked q = plan_chunks(batch, dim, len);
+  const dim3 cgrid(q.groups, q.nch, batch);
   const int st = dispatch(dtype, d_state, [&](auto t, auto n) {
-    hipLaunchKernelGGL((bwd_kernel<decltype(t), decltype(n)::value>), grid, dim3(64 * WPB), 0, s, a);
+    using T = decltype(t);
+    constexpr int NS = decltype(n)::value;
+    if (chunked) {
+      constexpr int R = CW > NS ? CW / NS : 1;
+      const size_t bytes = (size_t)2 * NS * CHUNK * (R * sizeof(float) + sizeof(T));
+      allow_lds(chunk_bwd_kernel<T, NS>, bytes);
+      hipLaunchKernelGGL((sum_bwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
+      hipLaunchKernelGGL((carry_kernel<NS>), dim3((batch * dim * NS + 255) / 256), dim3(256), 0, s, a, q, 1);
+      hipLaunchKernelGGL((chunk_bwd_kernel<T, NS>), cgrid, dim3(CT), bytes, s, a, q);
+    } else {
+      hipLaunchKernelGGL((bwd_kernel<T, NS>), dim3((batch * dim + WPB - 1) / WPB), dim3(64 * WPB),
+                         0, s, a);
+    }
   });
   DNA_CHECK_ARG(st == 0, "dna_selective_scan_bwd: d_state %d / dtype %d unsupported (4, 8, 16; f32/bf16)",
                 d_state, dtype);

@@ -192,19 +192,22 @@ int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec,
  *   x_t = exp(delta_t A) x_{t-1} + delta_t B_t u_t ;  out_t = (C_t . x_t + D u_t) * silu(z_t)
  * u, delta, z, out [batch, dim, len] (dtype), A [dim, d_state] fp32, B, C [batch, d_state, len]
  * (dtype), D, delta_bias [dim] fp32 (NULL allowed; z NULL = no gating). d_state in {4, 8, 16}.
- * states: dna_selective_scan_states() floats, chunk-start states for the backward (NULL to skip);
+ * states: dna_selective_scan_states() floats (fp32): chunk-start states kept for the backward,
+ * chunk delta sums and the backward's reverse-carry scratch; NULL skips them (and the
+ * chunk-parallel kernels, which need the buffer as workspace).
  * last_state [batch, dim, d_state] fp32 or NULL. */
 size_t dna_selective_scan_states(int batch, int dim, int len, int d_state);
 int dna_selective_scan_fwd(const void* u, const void* delta, const float* A, const void* B,
                            const void* C, const float* D, const void* z, const float* delta_bias,
                            int delta_softplus, int dtype, int batch, int dim, int len, int d_state,
                            void* out, float* states, float* last_state, void* stream);
-/* Backward from the forward's states. du, ddelta, dz (dtype) are written; dA [dim, d_state],
+/* Backward from the forward's states (the buffer's reverse-carry region is rewritten; the
+ * forward's part is only read). du, ddelta, dz (dtype) are written; dA [dim, d_state],
  * dB, dC [batch, d_state, len], dD, ddelta_bias [dim] (fp32) are ACCUMULATED (+=, zero them). */
 int dna_selective_scan_bwd(const void* u, const void* delta, const float* A, const void* B,
                            const void* C, const float* D, const void* z, const float* delta_bias,
                            int delta_softplus, int dtype, int batch, int dim, int len, int d_state,
-                           const float* states, const void* dout, void* du, void* ddelta,
+                           float* states, const void* dout, void* du, void* ddelta,
                            float* dA, float* dB, float* dC, float* dD, void* dz,
                            float* ddelta_bias, void* stream);
 

@@ -29,7 +29,10 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("b,d,l,n,use_z", [(2, 5, 700, 16, True), (1, 3, 1024, 8, False),
-                                           (3, 2, 64, 4, True), (1, 4, 2048, 16, True)])
+                                           (3, 2, 64, 4, True), (1, 4, 2048, 16, True),
+                                           # dim % 16 == 0 / % 8 == 0: LDS-staged block kernels
+                                           (2, 16, 1300, 16, True), (1, 8, 777, 8, False),
+                                           (2, 32, 1536, 4, True)])
 def test_selective_scan_fwd_bwd_vs_oracle(b, d, l, n, use_z):
     from dna_amd.mamba import selective_scan_fn
     u, delta, A, B, C, D, z, bias = _inputs(b, d, l, n, seed=l + n)
@@ -53,9 +56,10 @@ def test_selective_scan_fwd_bwd_vs_oracle(b, d, l, n, use_z):
         assert _rel(mine.grad.cpu(), theirs.grad) < 1e-3, name
 
 
-def test_selective_scan_bf16():
+@pytest.mark.parametrize("d", [4, 16])
+def test_selective_scan_bf16(d):
     from dna_amd.mamba import selective_scan_fn
-    u, delta, A, B, C, D, z, bias = _inputs(2, 4, 1500, 16, seed=3)
+    u, delta, A, B, C, D, z, bias = _inputs(2, d, 1500, 16, seed=3)
     ref = selective_scan_ref(u.bfloat16().float(), delta.bfloat16().float(), A,
                              B.bfloat16().float(), C.bfloat16().float(), D, z.bfloat16().float(),
                              bias, delta_softplus=True)
