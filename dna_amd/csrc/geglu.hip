@@ -2,6 +2,7 @@
 //   a = dropout( gelu_erf(g[:, :F]) * g[:, F:] ),  g = gated_layers(x) with F = intermediate_size.
 // HBM-bound elementwise: 8 consecutive outputs per thread (16-B bf16 vectors), grid-stride.
 // Algorithmic bytes per output element: fwd 2*s (read g1, g2) + s (write a); bwd 3*s + 2*s.
+// Dropout bits: dropout_keep8 (16-bit slices of one Philox draw per 8 elements).
 #include "common.h"
 
 namespace dna {
@@ -32,9 +33,8 @@ template <> struct Vec8<float> {
   }
 };
 
-__device__ __forceinline__ uint32_t keep8(uint64_t seed, uint64_t off, uint64_t elem, uint32_t th) {
-  // elem is a multiple of 8: two Philox groups of 4
-  return dropout_keep4(seed, off, elem >> 2, th) | (dropout_keep4(seed, off, (elem >> 2) + 1, th) << 4);
+__device__ __forceinline__ uint32_t keep8(uint64_t seed, uint64_t off, uint64_t elem, uint32_t th16) {
+  return dropout_keep8(seed, off, elem >> 3, th16);  // elem is a multiple of 8
 }
 
 template <typename T>
@@ -108,7 +108,7 @@ extern "C" int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, floa
   if (rows == 0) return DNA_OK;
   const dim3 grid = geglu::grid_for(rows, inter);
   hipStream_t s = as_stream(stream);
-  const uint32_t th = dropout_threshold(p_drop);
+  const uint32_t th = dropout_threshold16(p_drop);
   const float ks = 1.f / (1.f - p_drop);
   if (dtype == DNA_BF16)
     hipLaunchKernelGGL(geglu::fwd_kernel<bf16>, grid, dim3(128), 0, s, (const bf16*)g,
@@ -129,7 +129,7 @@ extern "C" int dna_geglu_bwd(const void* da, const void* g, int dtype, int rows,
   if (rows == 0) return DNA_OK;
   const dim3 grid = geglu::grid_for(rows, inter);
   hipStream_t s = as_stream(stream);
-  const uint32_t th = dropout_threshold(p_drop);
+  const uint32_t th = dropout_threshold16(p_drop);
   const float ks = 1.f / (1.f - p_drop);
   if (dtype == DNA_BF16)
     hipLaunchKernelGGL(geglu::bwd_kernel<bf16>, grid, dim3(128), 0, s, (const bf16*)da,

@@ -341,7 +341,8 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
           *reinterpret_cast<bf16x4*>(g + (size_t)m * 2 * a.F + c) = h1;
           *reinterpret_cast<bf16x4*>(g + (size_t)m * 2 * a.F + a.F + c) = h2;
           const size_t e = (size_t)m * a.F + c;
-          const uint32_t keep = a.p > 0.f ? dropout_keep4(a.seed, a.off, e >> 2, a.th) : 0xFu;
+          // c % 4 == 0: this lane's 4 columns are one half of a keep8 group
+          const uint32_t keep = a.p > 0.f ? (dropout_keep8(a.seed, a.off, e >> 3, a.th) >> (e & 4)) & 0xFu : 0xFu;
           float o[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -353,7 +354,7 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
       }
   } else {  // EPI_GEGLU_BWD
     // da tile -> LDS (bf16, [256][256], 16-B chunks XOR-swizzled by row&15), then row-contiguous
-    // 8-element chunks per thread: 16-B loads of g, 16-B stores of dg, 2 Philox groups.
+    // 8-element chunks per thread: 16-B loads of g, 16-B stores of dg, one keep8 Philox draw.
     __syncthreads();
     char* T = smem;
 #pragma unroll
@@ -383,9 +384,7 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
       const bf16x8 g2 = *reinterpret_cast<const bf16x8*>(grow + a.F + n);
       const size_t e = (size_t)m * a.F + n;
       uint32_t keep = 0xFFu;
-      if (a.p > 0.f)
-        keep = dropout_keep4(a.seed, a.off, e >> 2, a.th) |
-               (dropout_keep4(a.seed, a.off, (e >> 2) + 1, a.th) << 4);
+      if (a.p > 0.f) keep = dropout_keep8(a.seed, a.off, e >> 3, a.th);
       bf16x8 o1, o2;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -483,7 +482,7 @@ extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* b
   a.B = (const bf16*)w; a.ldb = K;
   a.C = g; a.ldc = 2 * F; a.bias = bias; a.aux = (bf16*)out;
   a.M = M; a.N = F; a.K = K; a.ksplit = K; a.F = F;
-  a.p = p_drop; a.th = dropout_threshold(p_drop); a.ks = 1.f / (1.f - p_drop);
+  a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed; a.off = offset;
   return launch<true, true, EPI_GEGLU>(a, 1, as_stream(stream), "dna_geglu_linear_fwd");
 }
@@ -500,7 +499,7 @@ extern "C" int dna_geglu_linear_dgrad(const void* dy, const void* w, const void*
   a.B = (const bf16*)w; a.ldb = F;
   a.C = nullptr; a.ldc = F; a.g = (const bf16*)g; a.aux = (bf16*)dg;
   a.M = M; a.N = F; a.K = N; a.ksplit = N; a.F = F;
-  a.p = p_drop; a.th = dropout_threshold(p_drop); a.ks = 1.f / (1.f - p_drop);
+  a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed; a.off = offset;
   return launch<true, false, EPI_GEGLU_BWD>(a, 1, as_stream(stream), "dna_geglu_linear_dgrad");
 }

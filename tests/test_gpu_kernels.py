@@ -118,6 +118,11 @@ def test_dropout_mask_consistent_fwd_bwd():
     kept = a != 0
     rate = kept.float().mean().item()
     assert abs(rate - 0.9) < 0.005, rate
+    # neighbours share one 32-bit Philox word (16-bit halves): their bits must be independent
+    k = kept.float()
+    for s in (1, 2, 4):
+        both = (k[:, :-s] * k[:, s:]).mean().item()
+        assert abs(both - rate * rate) < 0.005, (s, both, rate * rate)
     da = torch.randn(n, F, device=DEV)
     a.backward(da)
     g2 = g.detach().clone().requires_grad_(True)
