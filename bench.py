@@ -80,7 +80,8 @@ def make_batches(n_batches, batch, rank, device):
     return out
 
 
-def cpu_baseline(seconds_budget=20.0, threads=None):
+def cpu_baseline(seconds_budget=20.0, threads=None, cfg=None, seq=None, batch=2, max_seq=64,
+                 label="DNABERT-2-117M S=512"):
     """Oracle restatement (PyTorch CPU fp32, oracle/bert_ref.py, pinned to the reference) timing
     the same step (fwd + bert_cross_entropy + bwd + clip + AdamW, dropout 0.1) on a bounded sample."""
     from oracle import bert_ref
@@ -88,7 +89,8 @@ def cpu_baseline(seconds_budget=20.0, threads=None):
     prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    cfg = dict(MODEL_CFG)
+    cfg = dict(cfg or MODEL_CFG)
+    seq = seq or SEQ
     sd = {}
     for n, shape in bert_ref.state_dict_shapes(cfg):
         t = torch.randn(shape) * 0.02 if len(shape) > 1 else torch.zeros(shape)
@@ -100,8 +102,8 @@ def cpu_baseline(seconds_budget=20.0, threads=None):
 
     def step(b):
         rng = np.random.default_rng(b)
-        ids = torch.as_tensor(rng.integers(5, 4096, size=(b, SEQ)))
-        u = torch.as_tensor(rng.random((b, SEQ)))
+        ids = torch.as_tensor(rng.integers(5, 4096, size=(b, seq)))
+        u = torch.as_tensor(rng.random((b, seq)))
         mask = u < 0.15
         labels = torch.where(mask, ids, torch.full_like(ids, -100))
         masked = torch.where(mask, torch.full_like(ids, 4), ids)
@@ -113,8 +115,8 @@ def cpu_baseline(seconds_budget=20.0, threads=None):
         opt.step()
 
     step(1)  # warmup
-    b, n_seq, t_used = 2, 0, 0.0
-    while t_used < seconds_budget * 0.5 and n_seq < 64:
+    b, n_seq, t_used = batch, 0, 0.0
+    while t_used < seconds_budget * 0.5 and n_seq < max_seq:
         t0 = time.perf_counter()
         step(b)
         t_used += time.perf_counter() - t0
@@ -122,8 +124,13 @@ def cpu_baseline(seconds_budget=20.0, threads=None):
     torch.set_num_threads(prev_threads)
     return {"value": round(n_seq / t_used, 4), "unit": "sequences/s", "cores": threads,
             "kind": "port",
-            "sample": f"{n_seq} sequences (batches of {b}) of DNABERT-2-117M S=512 fp32 train steps "
+            "sample": f"{n_seq} sequences (batches of {b}) of {label} fp32 train steps "
                       f"(fwd+loss+bwd+clip+AdamW) with the oracle restatement on {threads} threads"}
+
+
+# BASELINE configs[0] / SURVEY §8(d) config A: 2 layers, d_model 128, 2 heads, S = 128, batch 8
+CONFIG_A = dict(vocab_size=4096, hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
+                intermediate_size=512)
 
 
 def main():
@@ -134,6 +141,7 @@ def main():
     ap.add_argument("--batch", type=int, default=int(os.environ.get("DNA_BENCH_BATCH", 256)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-b64", action="store_true", help="skip the extra per-GPU b=64 measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,6 +196,29 @@ def main():
     value = seqs / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
+    # besides the best per-GPU batch, always report b=64
+    b64 = None
+    if args.batch != 64 and not args.no_b64:
+        bb = make_batches(2, 64, rank, device)
+        for i in range(3):
+            trainer.step(bb[i % 2])
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        n64 = max(5, args.steps // 3)
+        for i in range(n64):
+            trainer.step(bb[i % 2])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e64 = torch.tensor([time.perf_counter() - t2], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(e64, op=dist.ReduceOp.MAX)
+        e64 = float(e64.item())
+        b64 = {"value": round(64 * n64 * world / e64, 2), "ms_per_step": round(e64 / n64 * 1e3, 3),
+               "steps": n64, "warmup": 3, "per_gpu_batch": 64}
+
     roofline, kernels = None, {}
     if timer:
         summ = timer.summary()
@@ -225,6 +256,12 @@ def main():
         cpu = cpu_baseline()
         one = cpu_baseline(seconds_budget=12.0, threads=1)  # the reference forces OMP_NUM_THREADS=1
         cpu["single_thread"] = {"value": one["value"], "cores": 1, "sample": one["sample"]}
+        ca = {}
+        for th in (None, 1):
+            r = cpu_baseline(seconds_budget=4.0, threads=th, cfg=CONFIG_A, seq=128, batch=8,
+                             max_seq=4096, label="config A (2 layers, d=128, S=128)")
+            ca["single_thread" if th == 1 else "all_threads"] = {k: r[k] for k in ("value", "cores", "sample")}
+        cpu["config_a"] = ca
 
     if rank == 0:
         line = {
@@ -240,7 +277,7 @@ def main():
             "model_mfu": round(value / world * TRAIN_FLOP_PER_SEQ / 1e12 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(final_loss, 4),
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
-            "data_pipeline": data_pipeline,
+            "data_pipeline": data_pipeline, "b64": b64,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
