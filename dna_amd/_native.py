@@ -26,6 +26,9 @@ _SIGS = {
     "dna_last_error": (ctypes.c_char_p, []),
     "dna_attn_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp]),
     "dna_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp]),
+    "dna_attn_bwd_ex": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp]),
+    "dna_attn_dbias_part_rows": (_i, [_i, _i]),
+    "dna_colsum_f32": (_i, [_vp, _i, _i, _vp, _i, _vp]),
     "dna_ln_fwd": (_i, [_vp, _i, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _i, _i, _f, _vp, _vp,
                         _vp, _vp, _vp]),
     "dna_ln_bwd_workspace": (_sz, [_i, _i]),

@@ -258,7 +258,8 @@ class BertForMaskedLM(nn.Module):
             att = layer.attention
             qkv = DF.linear(xin, att.self.Wqkv.weight, self._lp(att.self.Wqkv.weight),
                             att.self.Wqkv.bias)
-            ctx = DF.alibi_attention(qkv, key_valid, slopes, b, S, H)
+            ctx = DF.alibi_attention(qkv, key_valid, slopes, b, S, H,
+                                     bias_grad=att.self.Wqkv.bias is not None)
             res = x32
             if i == L - 1:  # last layer: output + MLP only on the subset rows (:480-488)
                 ctx = ctx.index_select(0, index.subset_idx)

@@ -309,11 +309,45 @@ __global__ void delta_kernel(const T* __restrict__ out, const T* __restrict__ do
 
 // ----------------------------------------------------------------------------- bf16 dQ
 // Queries on lanes (as forward). Per 64-key tile: S^T (8 MFMA), dP^T = V dO^T (8), dQ^T += K^T dS^T (8).
+// Column sums over a block's 128 rows of a [128 x 64] fp32 tile held as two 32x32 MFMA
+// accumulators (lane (wave, ql, hh): row wave*32+ql, columns 32dt + 8g + 4hh + e of acc[dt][4g+e]),
+// times `mul`; rows with !valid count as zero. `red` is >= 32 KiB of free LDS (16-B chunks
+// XOR-swizzled by row). Writes 64 floats to out. Fuses the packed-QKV projection's bias gradient
+// (column sums of dqkv) into the attention backward: one partial row per 128-row block.
+__device__ void block_colsum64(float* red, const f32x16 (&acc)[2], float mul, bool valid,
+                               float* __restrict__ out) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, ql = lane & 31, hh = lane >> 5;
+  const int r = wave * 32 + ql;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = valid ? acc[dt][4 * g + e] * mul : 0.f;
+      const int chunk = 8 * dt + 2 * g + hh;  // 16-B chunk of the 64-column row
+      *reinterpret_cast<f32x4*>(red + r * 64 + ((chunk ^ (r & 15)) << 2)) = v;
+    }
+  __syncthreads();
+  const int c = tid & 63, qr = tid >> 6;
+  float s = 0.f;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    const int rr = qr * 32 + i;
+    s += red[rr * 64 + ((((c >> 2) ^ (rr & 15)) << 2) | (c & 3))];
+  }
+  __syncthreads();
+  red[qr * 64 + c] = s;
+  __syncthreads();
+  if (tid < 64) out[c] = (red[c] + red[64 + c]) + (red[128 + c] + red[192 + c]);
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void dq_bf16_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ out, const bf16* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta,
     const uint8_t* __restrict__ key_valid, const float* __restrict__ slopes, int S, int H,
-    float scale_log2, float scale, bf16* __restrict__ dqkv) {
+    float scale_log2, float scale, bf16* __restrict__ dqkv, float* __restrict__ dbias_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Ks = reinterpret_cast<bf16*>(smem);     // [2][64*64] swizzled
   bf16* Vs = Ks + 2 * BK * D;                    // [2][64*64] swizzled
@@ -459,6 +493,10 @@ __global__ __launch_bounds__(256) void dq_bf16_kernel(
         for (int e = 0; e < 4; ++e) v[e] = (bf16)(dq[dt][4 * g + e] * scale);
         *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * hh) = v;
       }
+  }  if (dbias_part) {
+    const int nq = (S + BQ - 1) / BQ;
+    block_colsum64(reinterpret_cast<float*>(smem), dq, scale, qi < S,
+                   dbias_part + ((size_t)b * nq + qblk) * ld + h * D);
   }
 }
 
@@ -472,7 +510,7 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, const uint8_t* __restrict__ key_valid,
     const float* __restrict__ slopes, int S, int H, float scale_log2, float scale,
-    bf16* __restrict__ dqkv) {
+    bf16* __restrict__ dqkv, float* __restrict__ dbias_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Qs = reinterpret_cast<bf16*>(smem);      // [2][64*64] swizzled
   bf16* Os = Qs + 2 * BQT * D;                    // [2][64*64] dO, swizzled
@@ -621,6 +659,11 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
         *reinterpret_cast<bf16x4*>(row + H * D + 32 * dt + 8 * g + 4 * hh) = vk;
         *reinterpret_cast<bf16x4*>(row + 2 * H * D + 32 * dt + 8 * g + 4 * hh) = vv;
       }
+  }  if (dbias_part) {
+    const int nk = (S + BKW - 1) / BKW;
+    float* prow = dbias_part + ((size_t)b * nk + kblk) * ld + h * D;
+    block_colsum64(reinterpret_cast<float*>(smem), dk, scale, kj < S, prow + H * D);
+    block_colsum64(reinterpret_cast<float*>(smem), dv, 1.f, kj < S, prow + 2 * H * D);
   }
 }
 
@@ -817,10 +860,11 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
   return DNA_OK;
 }
 
-extern "C" int dna_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
-                            const uint8_t* key_valid, const float* slopes, int batch, int seqlen,
-                            int heads, int head_dim, int dtype, float softmax_scale, void* dqkv,
-                            float* delta_ws, void* stream) {
+extern "C" int dna_attn_bwd_ex(const void* qkv, const void* out, const void* dout,
+                               const float* lse, const uint8_t* key_valid, const float* slopes,
+                               int batch, int seqlen, int heads, int head_dim, int dtype,
+                               float softmax_scale, void* dqkv, float* delta_ws, float* dbias_part,
+                               void* stream) {
   int st = check_common(qkv, slopes, batch, seqlen, heads, head_dim, dtype, "dna_attn_bwd");
   if (st) return st;
   DNA_CHECK_ARG(out && dout && lse && dqkv && delta_ws, "dna_attn_bwd: null pointer");
@@ -832,11 +876,13 @@ extern "C" int dna_attn_bwd(const void* qkv, const void* out, const void* dout, 
     hipLaunchKernelGGL(dq_bf16_kernel, dim3(((seqlen + BQ - 1) / BQ) * heads * batch), dim3(256),
                        FWD_LDS, s, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
                        delta_ws, key_valid, slopes, seqlen, heads, softmax_scale * LOG2E,
-                       softmax_scale, (bf16*)dqkv);
+                       softmax_scale, (bf16*)dqkv, dbias_part);
     hipLaunchKernelGGL(dkdv_bf16_kernel, dim3(((seqlen + BKW - 1) / BKW) * heads * batch), dim3(256),
                        DKDV_LDS, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws, key_valid,
-                       slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv);
+                       slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv,
+                       dbias_part);
   } else {
+    DNA_CHECK_ARG(!dbias_part, "dna_attn_bwd_ex: fused bias-gradient partials need the bf16 path");
     hipLaunchKernelGGL(delta_kernel<float>, dim3(nd), dim3(256), 0, s, (const float*)out,
                        (const float*)dout, rows, heads, seqlen, delta_ws);
     dim3 grid((seqlen + F32_TILE - 1) / F32_TILE, heads, batch);
@@ -849,4 +895,16 @@ extern "C" int dna_attn_bwd(const void* qkv, const void* out, const void* dout, 
   }
   DNA_LAUNCH_CHECK("dna_attn_bwd");
   return DNA_OK;
+}
+
+extern "C" int dna_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
+                            const uint8_t* key_valid, const float* slopes, int batch, int seqlen,
+                            int heads, int head_dim, int dtype, float softmax_scale, void* dqkv,
+                            float* delta_ws, void* stream) {
+  return dna_attn_bwd_ex(qkv, out, dout, lse, key_valid, slopes, batch, seqlen, heads, head_dim,
+                         dtype, softmax_scale, dqkv, delta_ws, nullptr, stream);
+}
+
+extern "C" int dna_attn_dbias_part_rows(int batch, int seqlen) {
+  return batch * ((seqlen + BQ - 1) / BQ);
 }

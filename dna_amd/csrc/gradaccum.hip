@@ -30,6 +30,35 @@ __global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict
   }
 }
 
+// out[c] (+)= sum_r part[r][c], deterministic: a block = 64 columns x 16 row groups (row r goes
+// to group r % 16, summed in row order with 8 loads in flight), groups combined in fixed order.
+constexpr int CS_GROUPS = 16;
+
+__global__ __launch_bounds__(64 * CS_GROUPS) void colsum_kernel(const float* __restrict__ part,
+                                                                int rows, int cols, int accumulate,
+                                                                float* __restrict__ out) {
+  __shared__ float red[CS_GROUPS][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  float s = 0.f;
+  int r = g;
+  for (; r + 7 * CS_GROUPS < rows; r += 8 * CS_GROUPS) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = part[(size_t)(r + i * CS_GROUPS) * cols + c];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+  }
+  for (; r < rows; r += CS_GROUPS) s += part[(size_t)r * cols + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < CS_GROUPS; ++i) t += red[i][threadIdx.x];
+    out[c] = accumulate ? out[c] + t : t;
+  }
+}
+
 constexpr int SEG_CHUNK = 32;
 
 template <int NV>
@@ -82,6 +111,16 @@ extern "C" int dna_sum_slices_accum(const float* parts, int s, size_t n, float* 
   hipLaunchKernelGGL(gacc::sum_slices_kernel, dim3(nb), dim3(256), 0, as_stream(stream), parts, s,
                      n, out);
   DNA_LAUNCH_CHECK("dna_sum_slices_accum");
+  return DNA_OK;
+}
+
+extern "C" int dna_colsum_f32(const float* part, int rows, int cols, float* out, int accumulate,
+                              void* stream) {
+  DNA_CHECK_ARG(part && out && rows >= 1 && cols >= 64 && cols % 64 == 0,
+                "dna_colsum_f32: bad args (rows %d, cols %d; cols %% 64 == 0 required)", rows, cols);
+  hipLaunchKernelGGL(gacc::colsum_kernel, dim3(cols / 64), dim3(64 * gacc::CS_GROUPS), 0,
+                     as_stream(stream), part, rows, cols, accumulate, out);
+  DNA_LAUNCH_CHECK("dna_colsum_f32");
   return DNA_OK;
 }
 

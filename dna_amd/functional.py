@@ -194,7 +194,7 @@ class AlibiAttention(torch.autograd.Function):
     """softmax(q k^T * scale - slope_h |i-j| + pad_bias) v on packed qkv [T, 3*H*D]."""
 
     @staticmethod
-    def forward(ctx, qkv, key_valid, slopes, b, S, H, scale):
+    def forward(ctx, qkv, key_valid, slopes, b, S, H, scale, bias_grad=False):
         _gpu(qkv, key_valid, slopes)
         qkv = qkv.contiguous()
         T = qkv.shape[0]
@@ -206,6 +206,7 @@ class AlibiAttention(torch.autograd.Function):
                    _dt(qkv), scale, out.data_ptr(), lse.data_ptr(), N.stream_ptr())
         ctx.save_for_backward(qkv, out, lse, key_valid, slopes)
         ctx.cfg = (b, S, H, D, scale)
+        ctx.bias_grad = bias_grad and qkv.dtype == torch.bfloat16
         return out
 
     @staticmethod
@@ -215,17 +216,30 @@ class AlibiAttention(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(b * H * S, device=qkv.device, dtype=torch.float32)
         dout = dout.contiguous()
+        part = None
+        if ctx.bias_grad:  # column sums of dqkv (the packed projection's bias gradient), fused
+            rows = N.lib().dna_attn_dbias_part_rows(b, S)
+            part = torch.empty(rows, qkv.shape[1], device=qkv.device, dtype=torch.float32)
         with _timed("attn_bwd", 10.0 * b * H * S * S * D):
-            N.call("dna_attn_bwd", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(),
+            N.call("dna_attn_bwd_ex", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(),
                    lse.data_ptr(), _p(key_valid), slopes.data_ptr(), b, S, H, D, _dt(qkv), scale,
-                   dqkv.data_ptr(), delta.data_ptr(), N.stream_ptr())
-        return dqkv, None, None, None, None, None, None
+                   dqkv.data_ptr(), delta.data_ptr(), _p(part), N.stream_ptr())
+        if part is not None:
+            colsum = torch.empty(qkv.shape[1], device=qkv.device, dtype=torch.float32)
+            N.call("dna_colsum_f32", part.data_ptr(), part.shape[0], part.shape[1],
+                   colsum.data_ptr(), 0, N.stream_ptr())
+            # picked up by Linear.backward of the projection that produced qkv (same tensor
+            # object: nothing sits between the two nodes), instead of a dy.sum(0) pass
+            dqkv._dna_colsum = colsum
+        return dqkv, None, None, None, None, None, None, None
 
 
-def alibi_attention(qkv, key_valid, slopes, b, S, H, scale=None):
+def alibi_attention(qkv, key_valid, slopes, b, S, H, scale=None, bias_grad=False):
+    """bias_grad: also produce the column sums of dqkv in backward (bf16 path), for the bias of
+    the linear layer that made qkv (see Linear.backward)."""
     D = qkv.shape[1] // (3 * H)
     return AlibiAttention.apply(qkv, key_valid, slopes, b, S, H,
-                                scale if scale is not None else 1.0 / math.sqrt(D))
+                                scale if scale is not None else 1.0 / math.sqrt(D), bias_grad)
 
 
 # ----------------------------------------------------------------------------------- GeGLU
@@ -306,7 +320,10 @@ class Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w_lp = ctx.saved_tensors
+        colsum = getattr(dy, "_dna_colsum", None)
         dy = dy.contiguous()
+        if colsum is not None:
+            dy._dna_colsum = colsum
         flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
         dx = None
         if ctx.needs_input_grad[0]:
@@ -324,7 +341,11 @@ class Linear(torch.autograd.Function):
                 dw = None
             else:
                 dw = wgrad(dy, x)
-        db = dy.sum(0, dtype=torch.float32) if ctx.has_b else None
+        db = None
+        if ctx.has_b:
+            db = getattr(dy, "_dna_colsum", None)  # fused upstream (AlibiAttention.backward)
+            if db is None:
+                db = dy.sum(0, dtype=torch.float32)
         return dx, dw, None, db
 
 

@@ -63,6 +63,16 @@ int dna_attn_bwd(const void* qkv, const void* out, const void* dout, const float
                  const uint8_t* key_valid, const float* slopes, int batch, int seqlen, int heads,
                  int head_dim, int dtype, float softmax_scale, void* dqkv, float* delta_ws,
                  void* stream);
+/* Same, and (bf16 only, dbias_part non-NULL) the column sums of dqkv -- the gradient of the
+ * packed QKV projection's bias, Wqkv.bias (bert_layers.py:64, autograd's sum over tokens) -- as
+ * fp32 partials: dbias_part [dna_attn_dbias_part_rows(batch, seqlen)][3*heads*head_dim], one row
+ * per 128-token block, finished by dna_colsum_f32. The partials use the fp32 gradient values
+ * before their bf16 rounding. */
+int dna_attn_bwd_ex(const void* qkv, const void* out, const void* dout, const float* lse,
+                    const uint8_t* key_valid, const float* slopes, int batch, int seqlen, int heads,
+                    int head_dim, int dtype, float softmax_scale, void* dqkv, float* delta_ws,
+                    float* dbias_part, void* stream);
+int dna_attn_dbias_part_rows(int batch, int seqlen);
 
 /* ------------------------------------------------------------------ fused (bias, act, dropout, residual) + LayerNorm
  * y = LN( dropout( act(x + bias) ) + residual ) over the last dim.
@@ -123,6 +133,10 @@ int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_ids, const i
                           int rows, int cols, int vocab, int padding_idx, float* dword_emb,
                           void* stream);
 
+/* out[c] = sum_r part[r][c] (accumulate != 0: out[c] += ...), fp32, deterministic order;
+ * cols % 64 == 0. Finishes the fused bias-gradient partials (Linear bias grads, autograd's
+ * dy.sum(0)). */
+int dna_colsum_f32(const float* part, int rows, int cols, float* out, int accumulate, void* stream);
 /* out[i] += sum_{k<s} parts[k*n + i]: split-K partials of a weight gradient folded straight
  * into the flat fp32 gradient buffer (16-byte aligned, n % 4 == 0). */
 int dna_sum_slices_accum(const float* parts, int s, size_t n, float* out, void* stream);

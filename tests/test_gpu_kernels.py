@@ -72,6 +72,57 @@ def test_attention_backward(dtype, tol, b, S, H, pads):
     assert hv[~valid].abs().max().item() == 0.0 if (~valid).any() else True
 
 
+@pytest.mark.parametrize("b,S,H,pads", [(2, 128, 2, [(1, 77)]), (3, 512, 12, [(0, 400)]),
+                                        (1, 192, 3, [])])
+def test_attention_backward_fused_bias_grad(b, S, H, pads):
+    """bf16 backward with the fused column sums of dqkv (bias gradient of the QKV projection):
+    same dqkv as without, and the fp32 column sums match dqkv's (pre-rounding values vs rounded:
+    within bf16 rounding)."""
+    from dna_amd import functional as DF
+    from dna_amd.config import alibi_slopes
+    qkv, kv = _qkv(b, S, H, torch.bfloat16, pads, seed=3)
+    slopes = torch.tensor(alibi_slopes(H), device=DEV)
+    g = (torch.randn(b * S, H * 64, device=DEV) * kv[:, None].float()).bfloat16()
+    q1 = qkv.clone().requires_grad_(True)
+    DF.alibi_attention(q1, kv, slopes, b, S, H).backward(g)
+    grads = {}
+
+    class Grab(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x.view_as(x)
+
+        @staticmethod
+        def backward(ctx, d):
+            grads["colsum"] = getattr(d, "_dna_colsum", None)
+            grads["d"] = d
+            return d
+
+    q2 = qkv.clone().requires_grad_(True)
+    DF.alibi_attention(Grab.apply(q2), kv, slopes, b, S, H, bias_grad=True).backward(g)
+    assert torch.equal(q1.grad, q2.grad)
+    cs = grads["colsum"]
+    assert cs is not None and cs.dtype == torch.float32 and cs.shape == (3 * H * 64,)
+    ref = q2.grad.float().sum(0)
+    tol = 1e-2 * ref.abs().max().item() + 1e-3
+    assert (cs - ref).abs().max().item() < tol
+
+
+def test_colsum_f32_deterministic_and_exact():
+    from dna_amd import _native as N
+    g = torch.Generator(device="cpu").manual_seed(5)
+    part = torch.randn(1000, 2304, generator=g, dtype=torch.float64).float().to(DEV)
+    out = torch.full((2304,), 3.0, device=DEV)
+    N.call("dna_colsum_f32", part.data_ptr(), 1000, 2304, out.data_ptr(), 1, N.stream_ptr())
+    ref = part.double().sum(0) + 3.0
+    assert (out.double() - ref).abs().max().item() < 1e-4
+    out2 = torch.zeros(2304, device=DEV)
+    N.call("dna_colsum_f32", part.data_ptr(), 1000, 2304, out2.data_ptr(), 0, N.stream_ptr())
+    out3 = torch.zeros(2304, device=DEV)
+    N.call("dna_colsum_f32", part.data_ptr(), 1000, 2304, out3.data_ptr(), 0, N.stream_ptr())
+    assert torch.equal(out2, out3) and torch.allclose(out2 + 3.0, out)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cols", [64, 128, 768])
 @pytest.mark.parametrize("act,use_bias,use_res", [(0, True, True), (1, True, False), (0, False, True)])
