@@ -1,4 +1,5 @@
-"""HyenaDNA long convolution on MI355X: `fftconv` with the reference's signature and semantics.
+"""HyenaDNA long convolution on MI355X: `fftconv` with the reference's signature and semantics,
+and the Hyena operator modules around it (HyenaFilter, HyenaOperator).
 
 Mirrors `fftconv_ref(u, k, D, dropout_mask, gelu=True, k_rev=None, bidirectional=False)`
 (reference src/models/sequence/hyena.py:60-92) in the form `HyenaFilter.forward` calls it
@@ -7,7 +8,10 @@ Mirrors `fftconv_ref(u, k, D, dropout_mask, gelu=True, k_rev=None, bidirectional
 kernels of dna_amd/csrc/fftconv.hip (four-step FFT of size 2L, fp32 internally); there is no CPU
 or torch.fft fallback -- without the native library or a GPU tensor this raises.
 """
+import math
+
 import torch
+import torch.nn as nn
 
 from . import _native as N
 from .functional import _dt, _gpu, _p, _timed
@@ -86,3 +90,188 @@ def fftconv(u, k, D, dropout_mask=None, gelu=False, k_rev=None, bidirectional=Fa
     if dropout_mask is not None or gelu or k_rev is not None:
         raise NotImplementedError("fftconv: dropout_mask / gelu / k_rev (unused by HyenaFilter)")
     return FFTConv.apply(u, k, D, bidirectional)
+
+
+# --------------------------------------------------------------------------- Hyena operator
+# The modules around the long convolution, with the reference's constructor arguments, module
+# tree and state_dict keys (src/models/sequence/hyena.py:100-509), so reference checkpoints load
+# unchanged. The projections, the short depthwise conv and the tiny implicit-filter MLP are plain
+# torch ops (the MLP runs on [L, emb_dim]); the long convolution is the HIP `fftconv` above.
+class Sin(nn.Module):
+    """sin(freq * x), freq [1, dim] initialised to w (hyena.py:100-110)."""
+
+    def __init__(self, dim, w=10, train_freq=True):
+        super().__init__()
+        self.freq = nn.Parameter(w * torch.ones(1, dim)) if train_freq else w * torch.ones(1, dim)
+
+    def forward(self, x):
+        return torch.sin(self.freq * x)
+
+
+class _OptimModule(nn.Module):
+    """register(): lr == 0 -> buffer, else parameter tagged with its optimizer overrides
+    (reference src/utils/train.py:142-156)."""
+
+    def register(self, name, tensor, lr=None, wd=0.0):
+        if lr == 0.0:
+            self.register_buffer(name, tensor)
+        else:
+            self.register_parameter(name, nn.Parameter(tensor))
+            optim = {}
+            if lr is not None:
+                optim["lr"] = lr
+            if wd is not None:
+                optim["weight_decay"] = wd
+            setattr(getattr(self, name), "_optim", optim)
+
+
+class PositionalEmbedding(_OptimModule):
+    """Complex-exponential time features of the implicit filter (hyena.py:113-137)."""
+
+    def __init__(self, emb_dim: int, seq_len: int, lr_pos_emb: float = 1e-5, **kwargs):
+        super().__init__()
+        self.seq_len = seq_len
+        t = torch.linspace(0, 1, seq_len)[None, :, None]
+        bands = (emb_dim - 1) // 2
+        t_rescaled = torch.linspace(0, seq_len - 1, seq_len)[None, :, None]
+        w = 2 * math.pi * t_rescaled / seq_len
+        f = torch.linspace(1e-4, bands - 1, bands)[None, None]
+        z = torch.exp(-1j * f * w)
+        self.register("z", torch.cat([t, z.real, z.imag], dim=-1), lr=lr_pos_emb)
+        self.register("t", t, lr=0.0)
+
+    def forward(self, L):
+        return self.z[:, :L], self.t[:, :L]
+
+
+class ExponentialModulation(_OptimModule):
+    """h * (exp(-t |deltas|) + shift) (hyena.py:140-163)."""
+
+    def __init__(self, d_model, fast_decay_pct=0.3, slow_decay_pct=1.5, target=1e-2,
+                 modulation_lr=0.0, shift: float = 0.0, **kwargs):
+        super().__init__()
+        self.shift = shift
+        max_decay = math.log(target) / fast_decay_pct
+        min_decay = math.log(target) / slow_decay_pct
+        self.register("deltas", torch.linspace(min_decay, max_decay, d_model)[None, None],
+                      lr=modulation_lr)
+
+    def forward(self, t, x):
+        return x * (torch.exp(-t * self.deltas.abs()) + self.shift)
+
+
+class HyenaFilter(_OptimModule):
+    """Implicit long filter + the long convolution (hyena.py:166-280). `forward` runs the HIP
+    FFT convolution (the reference's `fftconv_ref` path, fused_fft_conv=False)."""
+
+    def __init__(self, d_model, emb_dim=3, order=16, fused_fft_conv=False, seq_len=1024, lr=1e-3,
+                 lr_pos_emb=1e-5, dropout=0.0, w=1, wd=0, bias=True, num_inner_mlps=2,
+                 linear_mixer=False, modulate: bool = True, normalized=False, bidirectional=False,
+                 **kwargs):
+        super().__init__()
+        if emb_dim % 2 == 0 or emb_dim < 3:
+            raise ValueError("emb_dim must be odd and greater or equal to 3 (time, sine and cosine)")
+        self.d_model, self.emb_dim, self.seq_len, self.modulate = d_model, emb_dim, seq_len, modulate
+        self.use_bias = bias
+        self.fused_fft_conv = fused_fft_conv
+        self.bias = nn.Parameter(torch.randn(d_model))
+        self.dropout = nn.Dropout(dropout)
+        self.bidirectional = bidirectional
+        act = Sin(dim=order, w=w)  # one module (one freq) reused by every activation, as in the reference
+        self.pos_emb = PositionalEmbedding(emb_dim, seq_len, lr_pos_emb)
+        if linear_mixer is False:
+            self.implicit_filter = nn.Sequential(nn.Linear(emb_dim, order), act)
+            for _ in range(num_inner_mlps):
+                self.implicit_filter.append(nn.Linear(order, order))
+                self.implicit_filter.append(act)
+            self.implicit_filter.append(nn.Linear(order, d_model, bias=False))
+        else:
+            self.implicit_filter = nn.Sequential(nn.Linear(emb_dim, d_model, bias=False))
+        self.modulation = ExponentialModulation(d_model, **kwargs)
+        self.normalized = normalized
+        for c in self.implicit_filter.children():
+            for name, _ in c.state_dict().items():
+                setattr(getattr(c, name), "_optim", {"weight_decay": wd, "lr": lr})
+
+    def filter(self, L, *args, **kwargs):
+        z, t = self.pos_emb(L)
+        h = self.implicit_filter(z)
+        if self.modulate:
+            h = self.modulation(t, h)
+        if self.normalized:
+            h = h / torch.norm(h, dim=-1, p=1, keepdim=True)
+        return h
+
+    def forward(self, x, L, k=None, bias=None, *args, **kwargs):
+        if k is None:
+            k = self.filter(L)
+        k = k[0] if type(k) is tuple else k
+        if bias is None:
+            bias = self.bias
+        bias = bias if self.use_bias else 0 * bias
+        return fftconv(x, k, bias, bidirectional=self.bidirectional).to(dtype=x.dtype)
+
+
+class HyenaOperator(nn.Module):
+    """Hyena operator (hyena.py:311-509): in_proj -> short depthwise conv -> order-1 gated long
+    convolutions -> out_proj. Supported as in every reference HyenaDNA config: num_heads = 1,
+    num_blocks = 1, inner_factor = 1, outer_mixing = post_order_ffn = False, activation "id";
+    other settings raise."""
+
+    def __init__(self, d_model, l_max, order=2, filter_order=64, num_heads=1, inner_factor=1,
+                 num_blocks=1, fused_bias_fc=False, outer_mixing=False, dropout=0.0,
+                 filter_dropout=0.0, filter_cls="hyena-filter", post_order_ffn=False,
+                 jit_filter=False, short_filter_order=3, activation="id", return_state=False,
+                 bidirectional=False, layer_idx=None, device=None, dtype=None, **filter_args):
+        super().__init__()
+        if (num_heads, inner_factor, num_blocks) != (1, 1, 1) or outer_mixing or post_order_ffn:
+            raise NotImplementedError("HyenaOperator: num_heads/inner_factor/num_blocks = 1, no "
+                                      "outer_mixing / post_order_ffn (all reference configs)")
+        if activation not in (None, "id", "identity", "linear"):
+            raise NotImplementedError(f"HyenaOperator: activation {activation!r}")
+        if fused_bias_fc:
+            raise NotImplementedError("fused_bias_fc (flash_attn FusedDense)")
+        if filter_cls not in ("hyena-filter", None):
+            raise NotImplementedError(f"filter_cls {filter_cls!r}")
+        if order < 2:
+            raise ValueError(f"Order must be at least 2, (got {order})")
+        self.d_model, self.order, self.l_max = d_model, order, l_max
+        self.num_heads, self.inner_factor, self.num_blocks = num_heads, inner_factor, num_blocks
+        self.head_dim = d_model // num_heads
+        self.block_dim = l_max // num_blocks
+        self.filter_order, self.short_filter_order = filter_order, short_filter_order
+        self.return_state, self.bidirectional = return_state, bidirectional
+        self.activation = nn.Identity()
+        self.dropout = nn.Dropout(dropout)
+        self.out_proj = nn.Linear(d_model * inner_factor, d_model)
+        self.in_proj = nn.Linear(d_model, (order + 1) * d_model)
+        total_width = d_model * inner_factor * (order + 1)
+        self.short_filter = nn.Conv1d(total_width, total_width, kernel_size=short_filter_order,
+                                      groups=total_width, padding=short_filter_order - 1)
+        self.filter_fn = HyenaFilter(self.head_dim * inner_factor * (order - 1), order=filter_order,
+                                     seq_len=l_max, channels=1, dropout=filter_dropout,
+                                     bidirectional=bidirectional, **filter_args)
+
+    def forward(self, u, *args, **kwargs):
+        l = u.size(-2)
+        l_filter = min(l, self.l_max)
+        u = self.in_proj(u).transpose(1, 2)                                   # b d l
+        uc = self.short_filter(u)[..., :l_filter]
+        b, C = uc.shape[0], uc.shape[1]
+        uc = uc.reshape(b, 1, C, 1, l_filter)                                 # b ho v z l
+        *x, v = uc.split(self.d_model, dim=2)
+        k = self.filter_fn.filter(l_filter)
+        k = k[0].reshape(l_filter, self.head_dim, self.order - 1).permute(2, 1, 0)   # o v l
+        bias = self.filter_fn.bias.reshape(self.head_dim, self.order - 1).t()          # o v
+        for o, x_i in enumerate(reversed(x[1:])):
+            v = self.dropout(v * x_i)
+            v = self.filter_fn(v, l_filter, k=k[o], bias=bias[o, None, :, None])
+        y = self.activation((v * x[0]).reshape(b, self.d_model, l_filter).transpose(1, 2))
+        y = self.out_proj(y)
+        if self.return_state:
+            return y, None
+        return y
+
+    @property
+    def d_output(self):
+        return self.d_model

@@ -85,3 +85,61 @@ def test_fftconv_linearity_and_errors():
         fftconv(u1[..., :1000], k[..., :1000], b)  # L not a power of 2
     with pytest.raises(RuntimeError):
         fftconv(u1.cpu(), k.cpu(), b.cpu())       # GPU only, no fallback
+
+
+def _op_state(d_model, l_max, order, seed, **kw):
+    """A HyenaOperator with random (non-default) weights and its float64 state_dict."""
+    from dna_amd.hyena import HyenaOperator
+    torch.manual_seed(seed)
+    op = HyenaOperator(d_model=d_model, l_max=l_max, order=order, **kw)
+    with torch.no_grad():
+        for n, p in op.named_parameters():
+            if n.endswith("freq"):
+                continue
+            p.add_(torch.randn_like(p) * 0.05)
+    return op, {k: v.detach().double().clone() for k, v in op.state_dict().items()}
+
+
+def test_hyena_operator_matches_reference_fixture():
+    """dna_amd.hyena.HyenaOperator (HIP long conv) on the reference operator's state_dict and
+    input (hyena_op_golden.npz, produced by running the reference): fp32 output vs the fp64 y."""
+    from dna_amd.hyena import HyenaOperator
+    d = np.load(os.path.join(os.path.dirname(GOLD), "hyena_op_golden.npz"), allow_pickle=False)
+    sd = {k[3:]: torch.tensor(d[k]).float() for k in d.files if k.startswith("sd/")}
+    op = HyenaOperator(d_model=16, l_max=64, order=2, filter_order=16)
+    op.load_state_dict(sd, strict=True)
+    op = op.to(DEV)
+    y = op(torch.tensor(d["x"]).float().to(DEV))
+    assert _rel(y.detach().cpu().numpy(), d["y"]) < 2e-5
+
+
+@pytest.mark.parametrize("d_model,L,order,bi,emb_dim", [(16, 64, 2, False, 3), (32, 4096, 3, True, 5),
+                                                        (24, 1024, 2, True, 5)])
+def test_hyena_operator_fwd_bwd_vs_oracle(d_model, L, order, bi, emb_dim):
+    """Forward and every gradient (input, projections, short conv, implicit-filter MLP, Sin
+    freq, filter bias) of the GPU operator against autograd of the float64 restatement
+    (oracle/hyena_operator_ref.py, pinned to the reference operator on the CPU side)."""
+    from oracle import hyena_operator_ref as HO
+    op, sd64 = _op_state(d_model, L, order, seed=L + order, filter_order=16, emb_dim=emb_dim,
+                         bidirectional=bi, w=10)
+    op = op.to(DEV)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, L, d_model, generator=g, dtype=torch.float64)
+    dy = torch.randn(2, L, d_model, generator=g, dtype=torch.float64)
+    buffers = {n for n, _ in op.named_buffers()}
+    ref_sd = {k: v.clone().requires_grad_(k not in buffers) for k, v in sd64.items()}
+    xr = x.clone().requires_grad_(True)
+    yr = HO.hyena_operator(ref_sd, xr, d_model, order=order, l_max=L, bidirectional=bi)
+    yr.backward(dy)
+    xg = x.float().to(DEV).requires_grad_(True)
+    y = op(xg)
+    assert _rel(y.detach().cpu().numpy(), yr.detach().numpy()) < 5e-5
+    y.backward(dy.float().to(DEV))
+    assert _rel(xg.grad.cpu().numpy(), xr.grad.numpy()) < 5e-5
+    # the shared Sin freq appears under several keys; compare each parameter once
+    for n, p in op.named_parameters():
+        ref = ref_sd[n].grad
+        if n.endswith("freq"):  # one shared parameter: the reference grads of its aliases add up
+            ref = sum(ref_sd[k].grad for k in ref_sd if k.endswith("freq"))
+        assert p.grad is not None, n
+        assert _rel(p.grad.cpu().numpy(), ref.numpy()) < 2e-4, n

@@ -4,6 +4,7 @@ import os
 
 import numpy as np
 import pytest
+import torch
 
 from oracle import hyena_ref as H
 
@@ -45,3 +46,33 @@ def test_oracle_fft_equals_direct_definition(bi):
 def test_pad_before_matches_reference_formula():
     # hyena.py:70-72: padded = L + 2*(L//2); pad_before = padded//2 - L//2
     assert H.pad_before(64, True) == 32 and H.pad_before(65, True) == 32 and H.pad_before(64, False) == 0
+
+
+def _op_fixture():
+    d = np.load(os.path.join(os.path.dirname(GOLD), "hyena_op_golden.npz"), allow_pickle=False)
+    sd = {k[3:]: torch.tensor(d[k]) for k in d.files if k.startswith("sd/")}
+    return d, sd
+
+
+def test_operator_oracle_matches_reference_fixture():
+    """oracle/hyena_operator_ref.py vs the reference HyenaOperator run (hyena_op_golden.npz)."""
+    from oracle import hyena_operator_ref as H
+    d, sd = _op_fixture()
+    k = H.hyena_filter(sd, 64)
+    assert torch.allclose(k, torch.tensor(d["filter_k"]), rtol=0, atol=1e-12)
+    y = H.hyena_operator(sd, torch.tensor(d["x"]), 16, order=2, l_max=64)
+    assert torch.allclose(y, torch.tensor(d["y"]), rtol=0, atol=1e-12)
+    z, t = H.positional_embedding(3, 64)
+    assert torch.equal(z.double(), sd["filter_fn.pos_emb.z"]) and torch.equal(t.double(), sd["filter_fn.pos_emb.t"])
+
+
+def test_operator_module_state_dict_matches_reference():
+    """dna_amd.hyena.HyenaOperator has the reference's module tree: the fixture's state_dict
+    (saved from the reference operator) loads strictly; a CPU forward raises (no fallback)."""
+    from dna_amd.hyena import HyenaOperator
+    d, sd = _op_fixture()
+    op = HyenaOperator(d_model=16, l_max=64, order=2, filter_order=16).double()
+    assert sorted(op.state_dict()) == sorted(sd)
+    op.load_state_dict(sd, strict=True)
+    with pytest.raises(RuntimeError):
+        op(torch.tensor(d["x"]))
