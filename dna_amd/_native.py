@@ -29,6 +29,11 @@ _SIGS = {
     "dna_attn_bwd_ex": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp]),
     "dna_attn_dbias_part_rows": (_i, [_i, _i]),
     "dna_colsum_f32": (_i, [_vp, _i, _i, _vp, _i, _vp]),
+    "dna_hyena_shortconv_fwd": (_i, [_vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "dna_hyena_shortconv_part_elems": (_sz, [_i, _i, _i, _i, _i]),
+    "dna_hyena_shortconv_bwd": (_i, [_vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
+    "dna_hyena_gate_out_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _sz, _vp, _vp]),
+    "dna_hyena_gate_out_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _sz, _vp, _vp, _vp]),
     "dna_ln_fwd": (_i, [_vp, _i, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _i, _i, _f, _vp, _vp,
                         _vp, _vp, _vp]),
     "dna_ln_bwd_workspace": (_sz, [_i, _i]),

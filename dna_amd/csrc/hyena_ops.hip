@@ -1,0 +1,350 @@
+// HyenaOperator data movement around the long convolution (reference
+// src/models/sequence/hyena.py:421-509), fused for gfx950. The reference runs, per layer:
+//   u = in_proj(x) [B, L, C] -> rearrange "b l d -> b d l" -> depthwise causal Conv1d (kernel K,
+//   padding K-1, first L outputs) -> split into x_0 .. x_{order-1}, v (d channels each) ->
+//   v = v * x_{order-1} -> long conv -> ... -> y = v * x_0 -> rearrange back -> out_proj.
+// Here:
+//   shortconv_fwd : u (token-major) -> x_0 .. x_{order-2} and v*x_{order-1}, channel-major, in one
+//                   pass (transpose through LDS; the conv needs a (K-1)-row halo);
+//   gate_out_fwd  : y = v_conv * x_0, channel-major in, token-major out (for out_proj);
+//   gate_out_bwd  : dy (token-major) -> d(v_conv) = dy x_0 and dx_0 = dy v_conv, channel-major;
+//   shortconv_bwd : d(x_0..x_{order-2}), d(v*x_{order-1}) -> du (token-major), recomputing the
+//                   conv outputs it needs from u; dw, dbias as per-block partials (reduced by
+//                   dna_colsum_f32 in a fixed order: deterministic).
+// Tiles: 64 positions x 32 channels per block of 256 threads (small LDS footprint -> several
+// blocks per CU); tiles load with 16-byte vectors; for the conv, lane = position (coalesced
+// channel-major rows) and wave = an 8-channel slice. All math in fp32; HBM-bound.
+#include "common.h"
+
+namespace dna {
+namespace hyop {
+
+constexpr int TP = 64;   // positions per tile
+constexpr int TC = 32;   // channels per tile
+constexpr int CPW = TC / 4;  // channels per wave in the conv phases
+constexpr int PAD = 1;   // LDS row padding (floats)
+
+template <typename T>
+__device__ __forceinline__ T cvt(float v) { return from_f32<T>(v); }
+
+// Load rows [t0 - lo, t0 + TP + hi) x channels [col0, col0 + TC) of a token-major [L, ldc] matrix
+// into lds[row][TC + PAD] (zero outside [0, L)), 16-byte vectors along the channels.
+template <typename T>
+__device__ __forceinline__ void load_tok_tile(float* lds, const T* src, int L, int ldc, int t0,
+                                              int lo, int hi, int col0) {
+  constexpr int VE = 16 / sizeof(T);      // elements per vector
+  constexpr int VPR = TC / VE;            // vectors per row
+  const int rows = TP + lo + hi;
+  for (int i = threadIdx.x; i < rows * VPR; i += blockDim.x) {
+    const int r = i / VPR, cv = (i - r * VPR) * VE;
+    const int t = t0 - lo + r;
+    float* dst = lds + r * (TC + PAD) + cv;
+    if (t >= 0 && t < L) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(src + (size_t)t * ldc + col0 + cv);
+      const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+      for (int q = 0; q < VE; ++q) dst[q] = to_f32(e[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < VE; ++q) dst[q] = 0.f;
+    }
+  }
+}
+
+struct Fwd {
+  const void* u; const float* w; const float* bias; int B, L, d, order, K;
+  void* xs; void* vx;
+};
+
+template <typename T, int K>
+__global__ __launch_bounds__(256) void shortconv_fwd_kernel(Fwd a) {
+  extern __shared__ float smem[];
+  const int G = a.order + 1, C = G * a.d;
+  const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
+  const int R = TP + K - 1;  // rows incl. halo
+  const T* u = (const T*)a.u + (size_t)b * a.L * C;
+  for (int g = 0; g < G; ++g)
+    load_tok_tile(smem + g * R * (TC + PAD), u, a.L, C, t0, K - 1, 0, g * a.d + c0);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int t = t0 + lane;
+  for (int j = wv * CPW; j < wv * CPW + CPW; ++j) {
+    const int c = c0 + j;
+    float last = 0.f;  // conv of group order-1 (x_{order-1})
+    for (int g = 0; g < G; ++g) {
+      const int ch = g * a.d + c;
+      const float* tl = smem + g * R * (TC + PAD);
+      float acc = a.bias[ch];
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc = fmaf(a.w[ch * K + k], tl[(lane + k) * (TC + PAD) + j], acc);
+      if (t < a.L) {
+        if (g < a.order - 1)
+          ((T*)a.xs)[((size_t)b * (a.order - 1) * a.d + g * a.d + c) * a.L + t] = cvt<T>(acc);
+        else if (g == a.order - 1)
+          last = acc;
+        else
+          ((T*)a.vx)[((size_t)b * a.d + c) * a.L + t] = cvt<T>(acc * last);
+      }
+    }
+  }
+}
+
+// y[b, t, c] = yc[b, c, t] * x0[b, c, t]
+template <typename T>
+__global__ __launch_bounds__(256) void gate_out_fwd_kernel(const T* yc, const T* x0, int L, int d,
+                                                           size_t x0_bstride, T* y) {
+  __shared__ float tile[TC][TP + PAD];
+  const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int j = wv; j < TC; j += 4) {
+    const int t = t0 + lane;
+    float v = 0.f;
+    if (t < L) {
+      const size_t o = ((size_t)b * d + c0 + j) * L + t;
+      v = to_f32(yc[o]) * to_f32(x0[(size_t)b * x0_bstride + (size_t)(c0 + j) * L + t]);
+    }
+    tile[j][lane] = v;
+  }
+  __syncthreads();
+  // token-major rows of TC channels: a wave covers 64 / TC rows per pass
+  constexpr int RPW = 64 / TC;
+  const int cl = lane % TC, rsub = lane / TC;
+  for (int r = wv * RPW + rsub; r < TP; r += 4 * RPW) {
+    const int t = t0 + r;
+    if (t < L) y[((size_t)b * L + t) * d + c0 + cl] = cvt<T>(tile[cl][r]);
+  }
+}
+
+// dyc = dy * x0, dx0 = dy * yc (channel-major outputs; dy token-major)
+template <typename T>
+__global__ __launch_bounds__(256) void gate_out_bwd_kernel(const T* dy, const T* yc, const T* x0,
+                                                           int L, int d, size_t x_bstride, T* dyc,
+                                                           T* dx0) {
+  __shared__ float tile[TP][TC + PAD];
+  const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int RPW = 64 / TC;
+  const int cl = lane % TC, rsub = lane / TC;
+  for (int r = wv * RPW + rsub; r < TP; r += 4 * RPW) {
+    const int t = t0 + r;
+    tile[r][cl] = t < L ? to_f32(dy[((size_t)b * L + t) * d + c0 + cl]) : 0.f;
+  }
+  __syncthreads();
+  for (int j = wv; j < TC; j += 4) {
+    const int t = t0 + lane;
+    if (t >= L) continue;
+    const float g = tile[lane][j];
+    const size_t o = ((size_t)b * d + c0 + j) * L + t;
+    const size_t ox = (size_t)b * x_bstride + (size_t)(c0 + j) * L + t;
+    dyc[o] = cvt<T>(g * to_f32(x0[ox]));
+    dx0[ox] = cvt<T>(g * to_f32(yc[o]));
+  }
+}
+
+struct Bwd {
+  const void* u; const float* w; const float* bias; int B, L, d, order, K;
+  const void* dxs; const void* dvx; void* du; float* part;  // part [B * nL][C][K + 1]
+};
+
+// duc (d of the conv outputs) at positions [t0, t0 + TP + K - 1), then
+//   du[t, ch]  = sum_k w[ch][k] duc[t + K - 1 - k]
+//   dw[ch][k] += sum_{t in tile} duc[t] u[t - (K - 1 - k)],  dbias[ch] += sum_{t in tile} duc[t]
+template <typename T, int K>
+__global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
+  extern __shared__ float smem[];
+  const int G = a.order + 1, C = G * a.d;
+  const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
+  const int RU = TP + 2 * (K - 1);  // u rows: [t0 - (K-1), t0 + TP + K - 1)
+  const int RD = TP + K - 1;        // duc rows: [t0, t0 + TP + K - 1)
+  float* us = smem;                              // [G][RU][TC + PAD]
+  float* ds = smem + G * RU * (TC + PAD);        // [G][RD][TC + PAD]
+  const T* u = (const T*)a.u + (size_t)b * a.L * C;
+  for (int g = 0; g < G; ++g)
+    load_tok_tile(us + g * RU * (TC + PAD), u, a.L, C, t0, K - 1, K - 1, g * a.d + c0);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // duc for this tile's positions plus the K-1 after it (0 at t >= L: cropped conv outputs)
+  for (int j = wv * CPW; j < wv * CPW + CPW; ++j) {
+    const int c = c0 + j;
+    for (int rr = lane; rr < RD; rr += 64) {
+      const int t = t0 + rr;
+      float conv_last = 0.f, conv_v = 0.f;
+      if (t < a.L) {
+        // recompute the conv outputs of groups order-1 and order at t (u rows rr .. rr + K - 1)
+        for (int g = a.order - 1; g <= a.order; ++g) {
+          const int ch = g * a.d + c;
+          const float* tl = us + g * RU * (TC + PAD);
+          float acc = a.bias[ch];
+#pragma unroll
+          for (int k = 0; k < K; ++k) acc = fmaf(a.w[ch * K + k], tl[(rr + k) * (TC + PAD) + j], acc);
+          if (g == a.order - 1) conv_last = acc; else conv_v = acc;
+        }
+      }
+      for (int g = 0; g < G; ++g) {
+        float v = 0.f;
+        if (t < a.L) {
+          if (g < a.order - 1) {
+            v = to_f32(((const T*)a.dxs)[((size_t)b * (a.order - 1) * a.d + g * a.d + c) * a.L + t]);
+          } else {
+            const float dvx = to_f32(((const T*)a.dvx)[((size_t)b * a.d + c) * a.L + t]);
+            v = g == a.order - 1 ? dvx * conv_v : dvx * conv_last;
+          }
+        }
+        ds[(g * RD + rr) * (TC + PAD) + j] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // du (token-major): lane = (row parity, channel); 4 waves x 2 rows per pass
+  T* du = (T*)a.du + (size_t)b * a.L * C;
+  constexpr int RPW = 64 / TC;
+  const int cl = lane % TC, rsub = lane / TC;
+  for (int g = 0; g < G; ++g) {
+    const int ch = g * a.d + c0 + cl;
+    float wk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[k] = a.w[ch * K + k];
+    const float* dl = ds + g * RD * (TC + PAD);
+    for (int r = wv * RPW + rsub; r < TP; r += 4 * RPW) {
+      const int t = t0 + r;
+      if (t >= a.L) break;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc = fmaf(wk[k], dl[(r + K - 1 - k) * (TC + PAD) + cl], acc);
+      du[(size_t)t * C + ch] = cvt<T>(acc);
+    }
+  }
+  // dw / dbias partials: a (group, channel) per thread; sum over the tile's TP positions
+  const int nL = gridDim.x;
+  float* prow = a.part + ((size_t)b * nL + blockIdx.x) * C * (K + 1);
+  for (int gc = threadIdx.x; gc < G * TC; gc += blockDim.x) {
+    const int g = gc / TC, j = gc - g * TC;
+    const int ch = g * a.d + c0 + j;
+    const float* dl = ds + g * RD * (TC + PAD);
+    const float* ul = us + g * RU * (TC + PAD);
+    float sw[K + 1];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) sw[k] = 0.f;
+    for (int r = 0; r < TP; ++r) {
+      const float dv = dl[r * (TC + PAD) + j];  // duc at t0 + r (0 past L)
+#pragma unroll
+      for (int k = 0; k < K; ++k) sw[k] = fmaf(dv, ul[(r + k) * (TC + PAD) + j], sw[k]);  // u[t - (K-1-k)]
+      sw[K] += dv;
+    }
+#pragma unroll
+    for (int k = 0; k <= K; ++k) prow[(size_t)ch * (K + 1) + k] = sw[k];
+  }
+}
+
+template <typename F>
+int dispatch_k(int K, F&& f) {
+  switch (K) {
+    case 2: f(std::integral_constant<int, 2>()); return 0;
+    case 3: f(std::integral_constant<int, 3>()); return 0;
+    case 4: f(std::integral_constant<int, 4>()); return 0;
+    default: return -1;
+  }
+}
+
+}  // namespace hyop
+}  // namespace dna
+
+using namespace dna;
+using namespace dna::hyop;
+
+static int hy_check(int B, int L, int d, int order, int K, int dtype, const char* fn) {
+  DNA_CHECK_ARG(B > 0 && L > 0 && d > 0 && d % 64 == 0, "%s: d %% 64 == 0 required (d=%d)", fn, d);
+  DNA_CHECK_ARG(order >= 2 && order <= 4, "%s: order %d unsupported (2..4)", fn, order);
+  DNA_CHECK_ARG(K >= 2 && K <= 4, "%s: short filter order %d unsupported (2..4)", fn, K);
+  DNA_CHECK_ARG(dtype == DNA_F32 || dtype == DNA_BF16, "%s: bad dtype", fn);
+  return DNA_OK;
+}
+
+extern "C" int dna_hyena_shortconv_fwd(const void* u, int dtype, const float* w, const float* bias,
+                                       int B, int L, int d, int order, int K, void* xs, void* vx,
+                                       void* stream) {
+  int st = hy_check(B, L, d, order, K, dtype, "dna_hyena_shortconv_fwd");
+  if (st) return st;
+  DNA_CHECK_ARG(u && w && bias && vx && (order == 2 || xs), "dna_hyena_shortconv_fwd: null pointer");
+  Fwd a{u, w, bias, B, L, d, order, K, xs, vx};
+  const dim3 grid((L + TP - 1) / TP, d / TC, B);
+  const size_t lds = (size_t)(order + 1) * (TP + K - 1) * (TC + PAD) * sizeof(float);
+  hipStream_t s = as_stream(stream);
+  dispatch_k(K, [&](auto kk) {
+    constexpr int KK = decltype(kk)::value;
+    if (dtype == DNA_F32)
+      hipLaunchKernelGGL((shortconv_fwd_kernel<float, KK>), grid, dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((shortconv_fwd_kernel<bf16, KK>), grid, dim3(256), lds, s, a);
+  });
+  DNA_LAUNCH_CHECK("dna_hyena_shortconv_fwd");
+  return DNA_OK;
+}
+
+extern "C" size_t dna_hyena_shortconv_part_elems(int B, int L, int d, int order, int K) {
+  return (size_t)B * ((L + TP - 1) / TP) * (order + 1) * d * (K + 1);
+}
+
+extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w, const float* bias,
+                                       int B, int L, int d, int order, int K, const void* dxs,
+                                       const void* dvx, void* du, float* part, void* stream) {
+  int st = hy_check(B, L, d, order, K, dtype, "dna_hyena_shortconv_bwd");
+  if (st) return st;
+  DNA_CHECK_ARG(u && w && bias && dvx && du && part && (order == 2 || dxs),
+                "dna_hyena_shortconv_bwd: null pointer");
+  Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part};
+  const dim3 grid((L + TP - 1) / TP, d / TC, B);
+  const size_t lds = (size_t)(order + 1) * ((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) * sizeof(float);
+  DNA_CHECK_ARG(lds <= 160 * 1024, "dna_hyena_shortconv_bwd: order %d needs %zu B of LDS", order, lds);
+  hipStream_t s = as_stream(stream);
+  dispatch_k(K, [&](auto kk) {
+    constexpr int KK = decltype(kk)::value;
+    if (dtype == DNA_F32) {
+      auto k = shortconv_bwd_kernel<float, KK>;
+      if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
+    } else {
+      auto k = shortconv_bwd_kernel<bf16, KK>;
+      if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
+    }
+  });
+  DNA_LAUNCH_CHECK("dna_hyena_shortconv_bwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_hyena_gate_out_fwd(const void* yc, const void* x0, int dtype, int B, int L, int d,
+                                      size_t x0_bstride, void* y, void* stream) {
+  DNA_CHECK_ARG(yc && x0 && y && B > 0 && L > 0 && d % TC == 0, "dna_hyena_gate_out_fwd: bad args");
+  const dim3 grid((L + TP - 1) / TP, d / TC, B);
+  hipStream_t s = as_stream(stream);
+  if (dtype == DNA_F32)
+    hipLaunchKernelGGL(gate_out_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)yc,
+                       (const float*)x0, L, d, x0_bstride, (float*)y);
+  else if (dtype == DNA_BF16)
+    hipLaunchKernelGGL(gate_out_fwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)yc,
+                       (const bf16*)x0, L, d, x0_bstride, (bf16*)y);
+  else
+    DNA_CHECK_ARG(false, "dna_hyena_gate_out_fwd: bad dtype");
+  DNA_LAUNCH_CHECK("dna_hyena_gate_out_fwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_hyena_gate_out_bwd(const void* dy, const void* yc, const void* x0, int dtype,
+                                      int B, int L, int d, size_t x_bstride, void* dyc, void* dx0,
+                                      void* stream) {
+  DNA_CHECK_ARG(dy && yc && x0 && dyc && dx0 && B > 0 && L > 0 && d % TC == 0,
+                "dna_hyena_gate_out_bwd: bad args");
+  const dim3 grid((L + TP - 1) / TP, d / TC, B);
+  hipStream_t s = as_stream(stream);
+  if (dtype == DNA_F32)
+    hipLaunchKernelGGL(gate_out_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)dy,
+                       (const float*)yc, (const float*)x0, L, d, x_bstride, (float*)dyc, (float*)dx0);
+  else if (dtype == DNA_BF16)
+    hipLaunchKernelGGL(gate_out_bwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dy,
+                       (const bf16*)yc, (const bf16*)x0, L, d, x_bstride, (bf16*)dyc, (bf16*)dx0);
+  else
+    DNA_CHECK_ARG(false, "dna_hyena_gate_out_bwd: bad dtype");
+  DNA_LAUNCH_CHECK("dna_hyena_gate_out_bwd");
+  return DNA_OK;
+}

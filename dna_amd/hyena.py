@@ -97,6 +97,83 @@ def fftconv(u, k, D, dropout_mask=None, gelu=False, k_rev=None, bidirectional=Fa
 # tree and state_dict keys (src/models/sequence/hyena.py:100-509), so reference checkpoints load
 # unchanged. The projections, the short depthwise conv and the tiny implicit-filter MLP are plain
 # torch ops (the MLP runs on [L, emb_dim]); the long convolution is the HIP `fftconv` above.
+class ShortConvSplit(torch.autograd.Function):
+    """Depthwise causal short conv of the in_proj output + split + first gate, fused
+    (dna_hyena_shortconv_fwd/bwd): u [B, L, C] token-major -> xs [B, order-1, d, L] (x_0 ..
+    x_{order-2}) and vx = v * x_{order-1} [B, d, L], channel-major for the long conv."""
+
+    @staticmethod
+    def forward(ctx, u, weight, bias, order, d):
+        _gpu(u, weight, bias)
+        u = u.contiguous()
+        B, L, C = u.shape
+        K = weight.shape[-1]
+        w = weight.detach().reshape(C, K).float().contiguous()
+        bb = bias.detach().float().contiguous()
+        xs = torch.empty(B, order - 1, d, L, device=u.device, dtype=u.dtype)
+        vx = torch.empty(B, d, L, device=u.device, dtype=u.dtype)
+        with _timed("hyena_shortconv_fwd", B * L * C * u.element_size() + order * B * d * L * u.element_size(), "byte"):
+            N.call("dna_hyena_shortconv_fwd", u.data_ptr(), _dt(u), w.data_ptr(), bb.data_ptr(), B, L,
+                   d, order, K, xs.data_ptr(), vx.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(u, w, bb)
+        ctx.cfg = (order, d, K, weight.shape, weight.dtype)
+        return xs, vx
+
+    @staticmethod
+    def backward(ctx, dxs, dvx):
+        u, w, bb = ctx.saved_tensors
+        order, d, K, wshape, wdtype = ctx.cfg
+        B, L, C = u.shape
+        if dxs is None:
+            dxs = torch.zeros(B, order - 1, d, L, device=u.device, dtype=u.dtype)
+        if dvx is None:
+            dvx = torch.zeros(B, d, L, device=u.device, dtype=u.dtype)
+        dxs = dxs.contiguous().to(u.dtype)
+        dvx = dvx.contiguous().to(u.dtype)
+        du = torch.empty_like(u)
+        nrow = N.lib().dna_hyena_shortconv_part_elems(B, L, d, order, K) // (C * (K + 1))
+        part = torch.empty(nrow, C * (K + 1), device=u.device, dtype=torch.float32)
+        with _timed("hyena_shortconv_bwd", 3 * B * L * C * u.element_size(), "byte"):
+            N.call("dna_hyena_shortconv_bwd", u.data_ptr(), _dt(u), w.data_ptr(), bb.data_ptr(), B, L,
+                   d, order, K, dxs.data_ptr(), dvx.data_ptr(), du.data_ptr(), part.data_ptr(),
+                   N.stream_ptr())
+            s = torch.empty(C * (K + 1), device=u.device, dtype=torch.float32)
+            N.call("dna_colsum_f32", part.data_ptr(), nrow, C * (K + 1), s.data_ptr(), 0, N.stream_ptr())
+        s = s.view(C, K + 1)
+        return du, s[:, :K].reshape(wshape).to(wdtype), s[:, K].contiguous(), None, None
+
+
+class GateOut(torch.autograd.Function):
+    """y = (v_conv * x_0) rearranged to [B, L, d] for out_proj (dna_hyena_gate_out_fwd/bwd)."""
+
+    @staticmethod
+    def forward(ctx, yc, xs):
+        _gpu(yc, xs)
+        yc = yc.contiguous()
+        B, d, L = yc.shape
+        xs = xs.to(yc.dtype)
+        y = torch.empty(B, L, d, device=yc.device, dtype=yc.dtype)
+        bstride = xs.stride(0)
+        assert xs.is_contiguous()
+        with _timed("hyena_gate_fwd", 3 * B * d * L * yc.element_size(), "byte"):
+            N.call("dna_hyena_gate_out_fwd", yc.data_ptr(), xs.data_ptr(), _dt(yc), B, L, d, bstride,
+                   y.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(yc, xs)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        yc, xs = ctx.saved_tensors
+        B, d, L = yc.shape
+        dy = dy.contiguous().to(yc.dtype)
+        dyc = torch.empty_like(yc)
+        dxs = torch.empty_like(xs) if xs.shape[1] == 1 else torch.zeros_like(xs)
+        with _timed("hyena_gate_bwd", 5 * B * d * L * yc.element_size(), "byte"):
+            N.call("dna_hyena_gate_out_bwd", dy.data_ptr(), yc.data_ptr(), xs.data_ptr(), _dt(yc), B, L,
+                   d, xs.stride(0), dyc.data_ptr(), dxs.data_ptr(), N.stream_ptr())
+        return dyc, dxs
+
+
 class Sin(nn.Module):
     """sin(freq * x), freq [1, dim] initialised to w (hyena.py:100-110)."""
 
@@ -255,6 +332,10 @@ class HyenaOperator(nn.Module):
     def forward(self, u, *args, **kwargs):
         l = u.size(-2)
         l_filter = min(l, self.l_max)
+        K = self.short_filter_order
+        if self.d_model % 64 == 0 and 2 <= K <= 4 and self.order <= 4 and l == l_filter:
+            return self._forward_fused(u, l_filter)
+        # other widths: torch ops around the HIP long convolution
         u = self.in_proj(u).transpose(1, 2)                                   # b d l
         uc = self.short_filter(u)[..., :l_filter]
         b, C = uc.shape[0], uc.shape[1]
@@ -267,6 +348,26 @@ class HyenaOperator(nn.Module):
             v = self.dropout(v * x_i)
             v = self.filter_fn(v, l_filter, k=k[o], bias=bias[o, None, :, None])
         y = self.activation((v * x[0]).reshape(b, self.d_model, l_filter).transpose(1, 2))
+        y = self.out_proj(y)
+        if self.return_state:
+            return y, None
+        return y
+
+    def _forward_fused(self, x, L):
+        """d_model % 64 == 0: in_proj -> fused short conv / split / gate (HIP) -> long convs
+        (HIP) -> fused gate + transpose (HIP) -> out_proj. Same math as forward's torch path."""
+        d, order = self.d_model, self.order
+        u = self.in_proj(x)                                                   # [B, L, C] token-major
+        xs, v = ShortConvSplit.apply(u, self.short_filter.weight, self.short_filter.bias, order, d)
+        k = self.filter_fn.filter(L)
+        k = k[0].reshape(L, self.head_dim, order - 1).permute(2, 1, 0)        # o v l
+        bias = self.filter_fn.bias.reshape(self.head_dim, order - 1).t()       # o v
+        for o in range(order - 1):
+            if o > 0:  # reversed(x[1:]): x_{order-1} was gated in the fused kernel
+                v = v * xs[:, order - 1 - o]
+            v = self.dropout(v)
+            v = self.filter_fn(v, L, k=k[o], bias=bias[o])
+        y = self.activation(GateOut.apply(v, xs))
         y = self.out_proj(y)
         if self.return_state:
             return y, None

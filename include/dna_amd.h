@@ -199,6 +199,28 @@ int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const void* kspec,
                     int B, int D, int L, int bidirectional, void* du, float* dk, float* dbias,
                     void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------ HyenaOperator data movement
+ * Around the long convolution in HyenaOperator.forward (src/models/sequence/hyena.py:421-509,
+ * num_heads = num_blocks = inner_factor = 1): u = in_proj(x) [B, L, C = (order+1)*d] token-major
+ * -> depthwise causal Conv1d (weight [C][K] fp32, bias [C] fp32; padding K-1, first L outputs,
+ * :423-425) -> split x_0 .. x_{order-1}, v -> first gate v * x_{order-1} (:459-465).
+ * d % 64 == 0, order 2..4, K 2..4; u/xs/vx in dtype (f32 or bf16), fp32 math.
+ * xs [B, order-1, d, L] = x_0 .. x_{order-2}; vx [B, d, L] (channel-major, the long conv's layout). */
+int dna_hyena_shortconv_fwd(const void* u, int dtype, const float* w, const float* bias, int B,
+                            int L, int d, int order, int K, void* xs, void* vx, void* stream);
+/* Backward: dxs [B, order-1, d, L], dvx [B, d, L] -> du [B, L, C] (written); dw/dbias as fp32
+ * partials part [B * ceil(L/64)][C][K+1] (last column = bias), summed by dna_colsum_f32. */
+size_t dna_hyena_shortconv_part_elems(int B, int L, int d, int order, int K);
+int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w, const float* bias, int B,
+                            int L, int d, int order, int K, const void* dxs, const void* dvx,
+                            void* du, float* part, void* stream);
+/* y [B, L, d] = (yc * x_0) rearranged "b d l -> b l d" (:503-507); x_0 rows at x0 + b*x0_bstride. */
+int dna_hyena_gate_out_fwd(const void* yc, const void* x0, int dtype, int B, int L, int d,
+                           size_t x0_bstride, void* y, void* stream);
+/* dyc = dy * x_0, dx0 = dy * yc (channel-major; dx0 with the same batch stride as x_0). */
+int dna_hyena_gate_out_bwd(const void* dy, const void* yc, const void* x0, int dtype, int B, int L,
+                           int d, size_t x_bstride, void* dyc, void* dx0, void* stream);
+
 /* ------------------------------------------------------------------ Mamba selective scan (Caduceus)
  * selective_scan_fn as called by mamba_ssm Mamba.forward inside Caduceus' BiMambaWrapper
  * (src/models/caduceus/modeling_caduceus.py:68-121; mamba_ssm is external and not vendored):

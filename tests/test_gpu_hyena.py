@@ -7,6 +7,7 @@ import os
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from oracle import hyena_ref as H
 
@@ -113,8 +114,10 @@ def test_hyena_operator_matches_reference_fixture():
     assert _rel(y.detach().cpu().numpy(), d["y"]) < 2e-5
 
 
-@pytest.mark.parametrize("d_model,L,order,bi,emb_dim", [(16, 64, 2, False, 3), (32, 4096, 3, True, 5),
-                                                        (24, 1024, 2, True, 5)])
+@pytest.mark.parametrize("d_model,L,order,bi,emb_dim", [
+    (16, 64, 2, False, 3), (32, 4096, 3, True, 5), (24, 1024, 2, True, 5),   # torch ops + HIP conv
+    (64, 1024, 2, True, 5), (128, 4096, 2, False, 5), (64, 512, 3, True, 3),  # fused HIP path
+])
 def test_hyena_operator_fwd_bwd_vs_oracle(d_model, L, order, bi, emb_dim):
     """Forward and every gradient (input, projections, short conv, implicit-filter MLP, Sin
     freq, filter bias) of the GPU operator against autograd of the float64 restatement
@@ -143,3 +146,47 @@ def test_hyena_operator_fwd_bwd_vs_oracle(d_model, L, order, bi, emb_dim):
             ref = sum(ref_sd[k].grad for k in ref_sd if k.endswith("freq"))
         assert p.grad is not None, n
         assert _rel(p.grad.cpu().numpy(), ref.numpy()) < 2e-4, n
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,L,d,order,K", [(2, 1000, 64, 2, 3), (1, 4096, 128, 3, 4), (3, 64, 64, 2, 2)])
+def test_hyena_fused_kernels_vs_torch(dtype, tol, B, L, d, order, K):
+    """ShortConvSplit / GateOut (fused HIP kernels) fwd + bwd against the same math in torch
+    fp32 (the reference's conv1d / split / gate, hyena.py:421-507) on identical inputs."""
+    from dna_amd.hyena import GateOut, ShortConvSplit
+    g = torch.Generator(device="cpu").manual_seed(B * L + d)
+    C = (order + 1) * d
+    u = torch.randn(B, L, C, generator=g).to(dtype).to(DEV)
+    w = (torch.randn(C, 1, K, generator=g) * 0.5).to(DEV)
+    bias = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    dxs = torch.randn(B, order - 1, d, L, generator=g).to(dtype).to(DEV)
+    dvx = torch.randn(B, d, L, generator=g).to(dtype).to(DEV)
+    # torch reference in fp32
+    ur = u.float().clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), bias.clone().requires_grad_(True)
+    uc = F.conv1d(ur.transpose(1, 2), wr, br, padding=K - 1, groups=C)[..., :L]
+    parts = uc.split(d, dim=1)
+    xs_r = torch.stack(parts[:order - 1], dim=1)
+    vx_r = parts[order] * parts[order - 1]
+    (xs_r * dxs.float()).sum().add((vx_r * dvx.float()).sum()).backward()
+    # fused
+    uf = u.clone().requires_grad_(True)
+    wf, bf = w.clone().requires_grad_(True), bias.clone().requires_grad_(True)
+    xs, vx = ShortConvSplit.apply(uf, wf, bf, order, d)
+    assert xs.dtype == dtype and vx.dtype == dtype
+    (xs.float() * dxs.float()).sum().add((vx.float() * dvx.float()).sum()).backward()
+    for mine, ref in ((xs, xs_r), (vx, vx_r), (uf.grad, ur.grad), (wf.grad, wr.grad), (bf.grad, br.grad)):
+        assert _rel(mine.detach().float().cpu().numpy(), ref.detach().cpu().numpy()) < tol
+    # gate + transpose
+    yc = torch.randn(B, d, L, generator=g).to(dtype).to(DEV).requires_grad_(True)
+    xs2 = xs.detach().clone().requires_grad_(True)
+    y = GateOut.apply(yc, xs2)
+    ref = (yc.detach().float() * xs2.detach().float()[:, 0]).transpose(1, 2)
+    assert y.shape == (B, L, d) and _rel(y.detach().float().cpu().numpy(), ref.cpu().numpy()) < tol
+    dy = torch.randn(B, L, d, generator=g).to(dtype).to(DEV)
+    y.backward(dy)
+    dyt = dy.float().transpose(1, 2)
+    assert _rel(yc.grad.float().cpu().numpy(), (dyt * xs2.detach().float()[:, 0]).cpu().numpy()) < tol
+    assert _rel(xs2.grad[:, 0].float().cpu().numpy(), (dyt * yc.detach().float()).cpu().numpy()) < tol
+    if order > 2:
+        assert xs2.grad[:, 1:].abs().max().item() == 0.0
