@@ -72,32 +72,83 @@ __device__ __forceinline__ void store8(T* p, int pos, int len, const float (&v)[
     if (pos + i < len) p[pos + i] = from_f32<T>(v[i]);
 }
 
-__device__ __forceinline__ float softplus(float x) { return x <= 20.f ? log1pf(__expf(x)) : x; }
-__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + __expf(-x)); }
+constexpr float LOG2E = 1.4426950408889634f;
+// raw v_exp_f32 (2^x); the state-transition arguments delta * A * log2(e) are <= 0
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+// softplus(x) = max(x, 0) + log1p(exp(-|x|)); log1p(y), y in (0, 1]: a 4-term series below 1e-2
+// (error < y^5/5), v_log above (absolute error ~1e-7). log1pf(expf(x)) compiles to a
+// denormal-safe sequence with a float64 convert and a branch per element -- it dominated the
+// chunk kernels.
+__device__ __forceinline__ float softplus(float x) {
+  const float y = ex2(-fabsf(x) * LOG2E);
+  const float s = y < 1e-2f ? y * (1.f - y * (0.5f - y * (1.f / 3.f - 0.25f * y))) : __logf(1.f + y);
+  return fmaxf(x, 0.f) + s;
+}
+__device__ __forceinline__ float sigmoidf(float x) {
+  return __builtin_amdgcn_rcpf(1.f + ex2(-x * LOG2E));
+}
 __device__ __forceinline__ float siluf(float x) { return x * sigmoidf(x); }
 
+// ---- cross-lane primitives: DPP (gfx9 row_shr/row_shl/row_bcast/wave_shr/wave_shl) and
+// v_readlane, all in the VALU; no ds_bpermute round trips through LDS. Lanes a DPP move does not
+// write keep `old`, which is always the identity of the operation, so no lane predicates.
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ float dpp(float old, float src) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL,
+                                                    RM, 0xF, false));
+}
+// value of lane `l` (wave-uniform l)
+__device__ __forceinline__ float bcast(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+// lane i <- lane i-1 (lane 0 <- ident); lane i <- lane i+1 (lane 63 <- ident)
+__device__ __forceinline__ float shr1(float v, float ident) { return dpp<0x138>(ident, v); }
+__device__ __forceinline__ float shl1(float v, float ident) { return dpp<0x130>(ident, v); }
+
+// (P, S) <- earlier (Po, So) applied first, then (P, S):  x -> P (Po x + So) + S
+__device__ __forceinline__ void combine(float Po, float So, float& P, float& S) {
+  S = fmaf(So, P, S);
+  P = Po * P;
+}
+
 // Inclusive wave scan of affine maps (P, S), earlier lanes applied first.
-__device__ __forceinline__ void scan_fwd(float& P, float& S, int lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float Po = __shfl_up(P, off, 64), So = __shfl_up(S, off, 64);
-    if (lane >= off) {
-      S = fmaf(So, P, S);
-      P = Po * P;
-    }
-  }
+__device__ __forceinline__ void scan_fwd(float& P, float& S, int /*lane*/) {
+  combine(dpp<0x111>(1.f, P), dpp<0x111>(0.f, S), P, S);  // row_shr:1
+  combine(dpp<0x112>(1.f, P), dpp<0x112>(0.f, S), P, S);  // row_shr:2
+  combine(dpp<0x114>(1.f, P), dpp<0x114>(0.f, S), P, S);  // row_shr:4
+  combine(dpp<0x118>(1.f, P), dpp<0x118>(0.f, S), P, S);  // row_shr:8
+  combine(dpp<0x142, 0xA>(1.f, P), dpp<0x142, 0xA>(0.f, S), P, S);  // row_bcast:15 -> rows 1, 3
+  combine(dpp<0x143, 0xC>(1.f, P), dpp<0x143, 0xC>(0.f, S), P, S);  // row_bcast:31 -> rows 2, 3
 }
-// Inclusive suffix scan (later lanes applied first).
+// Inclusive suffix scan (later lanes applied first): row_shl within the 16-lane rows, then the
+// row totals (lanes 16, 32, 48) composed with readlane and applied per row.
 __device__ __forceinline__ void scan_rev(float& P, float& S, int lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float Po = __shfl_down(P, off, 64), So = __shfl_down(S, off, 64);
-    if (lane + off < 64) {
-      S = fmaf(So, P, S);
-      P = Po * P;
-    }
-  }
+  combine(dpp<0x101>(1.f, P), dpp<0x101>(0.f, S), P, S);  // row_shl:1
+  combine(dpp<0x102>(1.f, P), dpp<0x102>(0.f, S), P, S);
+  combine(dpp<0x104>(1.f, P), dpp<0x104>(0.f, S), P, S);
+  combine(dpp<0x108>(1.f, P), dpp<0x108>(0.f, S), P, S);
+  const float P1 = bcast(P, 16), S1 = bcast(S, 16), P2 = bcast(P, 32), S2 = bcast(S, 32);
+  const float P3 = bcast(P, 48), S3 = bcast(S, 48);
+  float P23 = P2, S23 = S2;
+  combine(P3, S3, P23, S23);   // rows 2..3 (row 3 applied first)
+  float P13 = P1, S13 = S1;
+  combine(P23, S23, P13, S13); // rows 1..3
+  const int row = lane >> 4;
+  const float Po = row == 0 ? P13 : row == 1 ? P23 : row == 2 ? P3 : 1.f;
+  const float So = row == 0 ? S13 : row == 1 ? S23 : row == 2 ? S3 : 0.f;
+  combine(Po, So, P, S);
 }
+// inclusive prefix sum over the wave
+__device__ __forceinline__ float prefix_sum(float v) {
+  v += dpp<0x111>(0.f, v);
+  v += dpp<0x112>(0.f, v);
+  v += dpp<0x114>(0.f, v);
+  v += dpp<0x118>(0.f, v);
+  v += dpp<0x142, 0xA>(0.f, v);
+  v += dpp<0x143, 0xC>(0.f, v);
+  return v;
+}
+__device__ __forceinline__ float wsum(float v) { return bcast(prefix_sum(v), 63); }
 
 // delta after bias + softplus for one lane's 8 positions (invalid positions -> 0: identity map)
 __device__ __forceinline__ void prep_delta(float (&dl)[ITEMS], float bias, int sp, int pos, int len) {
@@ -141,26 +192,25 @@ __global__ __launch_bounds__(64 * WPB) void fwd_kernel(Args a) {
       float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS];
       load8(Bm + (size_t)n * a.len, pos, a.len, Bv);
       load8(Cm + (size_t)n * a.len, pos, a.len, Cv);
-      const float An = __shfl(Al, n, 64);
+      const float An = bcast(Al, n), An2 = An * LOG2E;
       float P = 1.f, S = 0.f;
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        aa[i] = __expf(dl[i] * An);
+        aa[i] = ex2(dl[i] * An2);
         bb[i] = dl[i] * Bv[i] * uu[i];
         S = fmaf(aa[i], S, bb[i]);
         P *= aa[i];
       }
       scan_fwd(P, S, lane);
       // exclusive prefix = inclusive of the previous lane; lane 0 gets the identity
-      float Pe = __shfl_up(P, 1, 64), Se = __shfl_up(S, 1, 64);
-      if (lane == 0) { Pe = 1.f; Se = 0.f; }
-      float x = fmaf(Pe, __shfl(xcl, n, 64), Se);
+      const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
+      float x = fmaf(Pe, bcast(xcl, n), Se);
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         x = fmaf(aa[i], x, bb[i]);
         y[i] = fmaf(Cv[i], x, y[i]);
       }
-      const float xe = __shfl(x, 63, 64);
+      const float xe = bcast(x, 63);
       if (lane == n) xcl = xe;
     }
     float o[ITEMS];
@@ -227,19 +277,18 @@ __global__ __launch_bounds__(64 * WPB) void bwd_kernel(Args a) {
       float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
       load8(Bm + (size_t)n * a.len, pos, a.len, Bv);
       load8(Cm + (size_t)n * a.len, pos, a.len, Cv);
-      const float An = __shfl(Al, n, 64);
+      const float An = bcast(Al, n), An2 = An * LOG2E;
       // forward states within the chunk from the stored chunk-start state
       float P = 1.f, S = 0.f;
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        aa[i] = __expf(dl[i] * An);
+        aa[i] = ex2(dl[i] * An2);
         bb[i] = dl[i] * Bv[i] * uu[i];
         S = fmaf(aa[i], S, bb[i]);
         P *= aa[i];
       }
       scan_fwd(P, S, lane);
-      float Pe = __shfl_up(P, 1, 64), Se = __shfl_up(S, 1, 64);
-      if (lane == 0) { Pe = 1.f; Se = 0.f; }
+      const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
       const float x0 = a.states[((size_t)ch * nch + c) * N + n];
       float xprev = fmaf(Pe, x0, Se);  // x_{t-1} for the lane's first position
       float x = xprev;
@@ -257,9 +306,8 @@ __global__ __launch_bounds__(64 * WPB) void bwd_kernel(Args a) {
         Pr *= aa[i];
       }
       scan_rev(Pr, Sr, lane);
-      float Pn = __shfl_down(Pr, 1, 64), Sn = __shfl_down(Sr, 1, 64);
-      if (lane == 63) { Pn = 1.f; Sn = 0.f; }
-      float h = fmaf(Pn, __shfl(hcl, n, 64), Sn);  // h_{t+1} for the lane's last position
+      const float Pn = shl1(Pr, 1.f), Sn = shl1(Sr, 0.f);
+      float h = fmaf(Pn, bcast(hcl, n), Sn);  // h_{t+1} for the lane's last position
       float dAn = 0.f;
 #pragma unroll
       for (int i = ITEMS - 1; i >= 0; --i) {
@@ -277,8 +325,8 @@ __global__ __launch_bounds__(64 * WPB) void bwd_kernel(Args a) {
         }
         h = aa[i] * g;
       }
-      const float dAs = wave_sum(dAn);
-      const float h0 = __shfl(h, 0, 64);
+      const float dAs = wsum(dAn);
+      const float h0 = bcast(h, 0);
       if (lane == n) { dAl += dAs; hcl = h0; }
     }
     // delta bias / softplus chain
@@ -305,8 +353,8 @@ __global__ __launch_bounds__(64 * WPB) void bwd_kernel(Args a) {
   }
   // per-channel reductions over the wave, then over the batch (atomics)
   if (lane < N) atomicAdd(a.dA + d * N + lane, dAl);
-  dDacc = wave_sum(dDacc);
-  dbacc = wave_sum(dbacc);
+  dDacc = wsum(dDacc);
+  dbacc = wsum(dbacc);
   if (lane == 0) {
     if (a.dD) atomicAdd(a.dD + d, dDacc);
     if (a.ddelta_bias) atomicAdd(a.ddelta_bias + d, dbacc);
@@ -375,16 +423,19 @@ __device__ __forceinline__ void lds8(const T* p, float (&v)[ITEMS]) {
 // lane-level sums of δ: exclusive prefix (lanes before) and exclusive suffix (lanes after),
 // each summed directly (no differences of large prefix sums), and the chunk total
 __device__ __forceinline__ void delta_sums(float tl, int lane, float& pre, float& suf, float& tot) {
-  float inc = tl, sinc = tl;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float a = __shfl_up(inc, off, 64), b = __shfl_down(sinc, off, 64);
-    if (lane >= off) inc += a;
-    if (lane + off < 64) sinc += b;
-  }
-  pre = inc - tl;     // exact enough: inc and tl are one lane's own values
-  suf = sinc - tl;
-  tot = __shfl(inc, 63, 64);
+  const float inc = prefix_sum(tl);
+  pre = shr1(inc, 0.f);
+  // suffix: row_shl sums within rows, then the later rows' totals (lanes 16, 32, 48)
+  float sinc = tl;
+  sinc += dpp<0x101>(0.f, sinc);
+  sinc += dpp<0x102>(0.f, sinc);
+  sinc += dpp<0x104>(0.f, sinc);
+  sinc += dpp<0x108>(0.f, sinc);
+  const float r1 = bcast(sinc, 16), r2 = bcast(sinc, 32), r3 = bcast(sinc, 48);
+  const int row = lane >> 4;
+  sinc += row == 0 ? (r1 + r2) + r3 : row == 1 ? r2 + r3 : row == 2 ? r3 : 0.f;
+  suf = shl1(sinc, 0.f);
+  tot = bcast(inc, 63);
 }
 
 template <typename T, int N>
@@ -417,11 +468,11 @@ __global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
     for (int n = 0; n < N; ++n) {
       float Bv[ITEMS];
       lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
-      const float An = __shfl(Al, n, 64);
+      const float An = bcast(Al, n), An2 = An * LOG2E;
       float x = 0.f;
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) x = fmaf(__expf(dl[i] * An), x, uu[i] * Bv[i]);
-      const float S = wave_sum(x * __expf(An * suf));
+      for (int i = 0; i < ITEMS; ++i) x = fmaf(ex2(dl[i] * An2), x, uu[i] * Bv[i]);
+      const float S = wsum(x * ex2(An2 * suf));
       if (lane == n) Sl = S;
     }
     if (lane < N) Sbuf[(size_t)ch * nchN + (size_t)c * N + lane] = Sl;
@@ -464,11 +515,11 @@ __global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
     for (int n = 0; n < N; ++n) {
       float Cv[ITEMS];
       lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
-      const float An = __shfl(Al, n, 64);
+      const float An = bcast(Al, n), An2 = An * LOG2E;
       float r = 0.f;
 #pragma unroll
-      for (int i = ITEMS - 1; i >= 0; --i) r = __expf(dl[i] * An) * fmaf(Cv[i], dy[i], r);
-      const float R = wave_sum(r * __expf(An * pre));
+      for (int i = ITEMS - 1; i >= 0; --i) r = ex2(dl[i] * An2) * fmaf(Cv[i], dy[i], r);
+      const float R = wsum(r * ex2(An2 * pre));
       if (lane == n) Rl = R;
     }
     if (lane < N) Rbuf[(size_t)ch * nchN + (size_t)c * N + lane] = Rl;
@@ -529,26 +580,25 @@ __global__ __launch_bounds__(CT) void chunk_fwd_kernel(Args a, Chunked q) {
     load8((const T*)a.u + off, pos, a.len, uu);
     load8((const T*)a.delta + off, pos, a.len, dl);
     prep_delta(dl, bias, a.softplus, pos, a.len);
+    float du_[ITEMS], tl = 0.f;  // delta * u and the lane's delta sum (state-independent)
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) y[i] = 0.f;
+    for (int i = 0; i < ITEMS; ++i) { y[i] = 0.f; du_[i] = dl[i] * uu[i]; tl += dl[i]; }
 #pragma unroll 2
     for (int n = 0; n < N; ++n) {
       float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS];
       lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
       lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
-      const float An = __shfl(Al, n, 64);
-      float P = 1.f, S = 0.f;
+      const float An = bcast(Al, n), An2 = An * LOG2E;
+      float P = ex2(tl * An2), S = 0.f;  // prod_i exp(dl_i A) = exp(A sum_i dl_i)
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        aa[i] = __expf(dl[i] * An);
-        bb[i] = dl[i] * Bv[i] * uu[i];
+        aa[i] = ex2(dl[i] * An2);
+        bb[i] = du_[i] * Bv[i];
         S = fmaf(aa[i], S, bb[i]);
-        P *= aa[i];
       }
       scan_fwd(P, S, lane);
-      float Pe = __shfl_up(P, 1, 64), Se = __shfl_up(S, 1, 64);
-      if (lane == 0) { Pe = 1.f; Se = 0.f; }
-      float x = fmaf(Pe, __shfl(xcl, n, 64), Se);
+      const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
+      float x = fmaf(Pe, bcast(xcl, n), Se);
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         x = fmaf(aa[i], x, bb[i]);
@@ -616,29 +666,31 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) dy[i] = go[i];
     }
-    float ddl[ITEMS], du[ITEMS], y[ITEMS];
-    float dDacc = 0.f, dAl = 0.f;
+    float ddl[ITEMS], du[ITEMS], y[ITEMS], dlu[ITEMS];
+    float dDacc = 0.f, dAl = 0.f, tl = 0.f;
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) { ddl[i] = 0.f; du[i] = Dd * dy[i]; y[i] = 0.f; dDacc = fmaf(dy[i], uu[i], dDacc); }
+    for (int i = 0; i < ITEMS; ++i) {
+      ddl[i] = 0.f; du[i] = Dd * dy[i]; y[i] = 0.f; dDacc = fmaf(dy[i], uu[i], dDacc);
+      dlu[i] = dl[i] * uu[i]; tl += dl[i];
+    }
 #pragma unroll 1
     for (int st = 0; st < N; ++st) {
       const int n = (st + w) % N;
       float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
       lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
       lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
-      const float An = __shfl(Al, n, 64);
-      float P = 1.f, S = 0.f;
+      const float An = bcast(Al, n), An2 = An * LOG2E;
+      const float Pt = ex2(tl * An2);  // prod_i a_i, for both directions
+      float P = Pt, S = 0.f;
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        aa[i] = __expf(dl[i] * An);
-        bb[i] = dl[i] * Bv[i] * uu[i];
+        aa[i] = ex2(dl[i] * An2);
+        bb[i] = dlu[i] * Bv[i];
         S = fmaf(aa[i], S, bb[i]);
-        P *= aa[i];
       }
       scan_fwd(P, S, lane);
-      float Pe = __shfl_up(P, 1, 64), Se = __shfl_up(S, 1, 64);
-      if (lane == 0) { Pe = 1.f; Se = 0.f; }
-      const float xprev = fmaf(Pe, __shfl(xcl, n, 64), Se);
+      const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
+      const float xprev = fmaf(Pe, bcast(xcl, n), Se);
       float x = xprev;
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
@@ -646,16 +698,12 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
         xs[i] = x;
         y[i] = fmaf(Cv[i], x, y[i]);
       }
-      float Pr = 1.f, Sr = 0.f;
+      float Pr = Pt, Sr = 0.f;
 #pragma unroll
-      for (int i = ITEMS - 1; i >= 0; --i) {
-        Sr = aa[i] * (Cv[i] * dy[i] + Sr);
-        Pr *= aa[i];
-      }
+      for (int i = ITEMS - 1; i >= 0; --i) Sr = aa[i] * fmaf(Cv[i], dy[i], Sr);
       scan_rev(Pr, Sr, lane);
-      float Pn = __shfl_down(Pr, 1, 64), Sn = __shfl_down(Sr, 1, 64);
-      if (lane == 63) { Pn = 1.f; Sn = 0.f; }
-      float h = fmaf(Pn, __shfl(hcl, n, 64), Sn);
+      const float Pn = shl1(Pr, 1.f), Sn = shl1(Sr, 0.f);
+      float h = fmaf(Pn, bcast(hcl, n), Sn);
       float dAn = 0.f;
       float* aB = accw + n * CHUNK + lane;
       float* aC = aB + N * CHUNK;
@@ -673,7 +721,7 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
         aC[i * 64] += dy[i] * xs[i];
         h = aa[i] * g;
       }
-      const float dAs = wave_sum(dAn);
+      const float dAs = wsum(dAn);
       if (lane == n) dAl = dAs;
       __syncthreads();
     }
@@ -698,8 +746,8 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
       store8((T*)a.dz + off, pos, a.len, dzv);
     }
     if (lane < N) atomicAdd(a.dA + d * N + lane, dAl);
-    dDacc = wave_sum(dDacc);
-    dbacc = wave_sum(dbacc);
+    dDacc = wsum(dDacc);
+    dbacc = wsum(dbacc);
     if (lane == 0) {
       if (a.dD) atomicAdd(a.dD + d, dDacc);
       if (a.ddelta_bias) atomicAdd(a.ddelta_bias + d, dbacc);
