@@ -99,13 +99,37 @@ __host__ __device__ __forceinline__ uint32_t dropout_threshold(float p) {
 }
 
 // ---------------------------------------------------------------------------------------- math
+// erf(z), branchless (Abramowitz & Stegun 7.1.26: |error| < 1.5e-7 in exact arithmetic,
+// < 6e-7 evaluated in fp32), with e = exp(-z^2) as a by-product: one v_rcp, one v_exp, 5 FMAs.
+// The OCML erff it replaces branches on |z| per element (divergent, both paths run) and was the
+// largest VALU cost of the GeGLU kernels. GELU from it: |error| < 5e-7 on [-10, 10] (checked
+// against math.erf), below bf16 resolution of every tensor it feeds.
+__device__ __forceinline__ float erf_fast(float z, float& e) {
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  e = __builtin_amdgcn_exp2f(-az * az * 1.4426950408889634f);
+  return copysignf(fmaf(-p, e, 1.f), z);
+}
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+  float e;
+  return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f, e));
+}
+// GELU(x) and its derivative Phi(x) + x phi(x), sharing one erf / exp
+__device__ __forceinline__ void gelu_erf_and_grad(float x, float& g, float& dg) {
+  float e;
+  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f, e));
+  g = x * cdf;
+  dg = fmaf(x * 0.3989422804014327f, e, cdf);  // e = exp(-x^2 / 2)
 }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float g, dg;
+  gelu_erf_and_grad(x, g, dg);
+  return dg;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -80,9 +80,10 @@ __global__ __launch_bounds__(128) void bwd_kernel(const T* __restrict__ da, cons
     for (int j = 0; j < 8; ++j) {
       float dd = d[j];
       if (p > 0.f) dd = ((keep >> j) & 1) ? dd * ks : 0.f;
-      const float x = g1[j];
-      o1[j] = dd * g2[j] * gelu_erf_grad(x);
-      o2[j] = dd * gelu_erf(x);
+      float ge, dge;
+      gelu_erf_and_grad(g1[j], ge, dge);
+      o1[j] = dd * g2[j] * dge;
+      o2[j] = dd * ge;
     }
     Vec8<T>::store(dg + (size_t)r * 2 * F + c, o1);
     Vec8<T>::store(dg + (size_t)r * 2 * F + F + c, o2);

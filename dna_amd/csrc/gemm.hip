@@ -391,8 +391,10 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
         float dd = (float)d[q];
         if (a.p > 0.f) dd = ((keep >> q) & 1) ? dd * a.ks : 0.f;
         const float x = (float)g1[q];
-        o1[q] = (bf16)(dd * (float)g2[q] * gelu_erf_grad(x));
-        o2[q] = (bf16)(dd * gelu_erf(x));
+        float ge, dge;
+        gelu_erf_and_grad(x, ge, dge);
+        o1[q] = (bf16)(dd * (float)g2[q] * dge);
+        o2[q] = (bf16)(dd * ge);
       }
       bf16* dg = a.aux + (size_t)m * 2 * a.F;
       *reinterpret_cast<bf16x8*>(dg + n) = o1;
