@@ -96,3 +96,17 @@ class GradBucketReducer:
     @property
     def grad_scale(self):
         return 1.0 / self.world
+
+
+def reduce_metrics(loss, num_tokens, group=None):
+    """Rank-mean of the step loss and the global token count as ONE small all-reduce (SURVEY
+    §8(e): DDP loss semantics = mean of per-rank masked-token means; scalar metrics packed into
+    one collective at the logging interval). Returns (mean_loss, total_tokens) as Python numbers;
+    without a process group, the local values."""
+    lv = loss.detach().reshape(()).to(torch.float64)
+    if not (dist.is_available() and dist.is_initialized()):
+        return float(lv.item()), int(num_tokens)
+    world = dist.get_world_size(group)
+    t = torch.stack([lv, torch.tensor(float(num_tokens), dtype=torch.float64, device=lv.device)])
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return float(t[0].item()) / world, int(round(float(t[1].item())))

@@ -154,3 +154,31 @@ def test_grad_bucket_reducer_gloo_two_ranks():
         a, b = torch.tensor(res[0][step]), torch.tensor(res[1][step])
         assert torch.allclose(a, b)  # every rank holds the same averaged gradient
         assert torch.allclose(a, ref[step], atol=1e-6), (a - ref[step]).abs().max()
+
+
+def _metrics_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dna_amd.ddp import reduce_metrics
+        loss = torch.tensor(1.0 + rank)      # per-rank masked-token means
+        q.put((rank, reduce_metrics(loss, 100 * (rank + 1))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reduce_metrics_two_ranks_gloo():
+    """One packed all-reduce: rank-mean loss (DDP loss semantics) and the global token count,
+    identical on every rank."""
+    from dna_amd.ddp import reduce_metrics
+    assert reduce_metrics(torch.tensor(2.5), 7) == (2.5, 7)  # no process group: local values
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_metrics_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert out[0] == out[1] == (1.5, 300)

@@ -78,6 +78,7 @@ def save_checkpoint(path, trainer, epoch):
 
 def train(cfg, dry_run=False, out=sys.stdout):
     from dna_amd.bert_layers import BertForMaskedLM  # noqa: F401
+    from dna_amd.ddp import reduce_metrics
     from dna_amd.trainer import DeviceBatch, MLMTrainer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,7 +180,8 @@ def train(cfg, dry_run=False, out=sys.stdout):
             micro = []
             step = trainer.global_step
             if step % log_every == 0 or step == 1:
-                lv = float(loss.item())
+                # every rank joins: rank-mean loss + global token count in one all-reduce
+                lv, tokens_all = reduce_metrics(loss, num_tokens)
                 ppl_sum += lv
                 ppl_cnt += 1
                 now = time.perf_counter()
@@ -187,7 +189,7 @@ def train(cfg, dry_run=False, out=sys.stdout):
                     print(json.dumps({"step": step, "epoch": epoch, "train/loss": round(lv, 5),
                                       "trainer/loss": round(lv, 5),
                                       "train/perplexity": round(math.exp(ppl_sum / ppl_cnt), 4),
-                                      "train/num_tokens": num_tokens * world,
+                                      "train/num_tokens": tokens_all,
                                       "trainer/lr": trainer.opt.param_groups[0]["lr"],
                                       "timer/step": round((now - t_last) / (log_every if step > 1 else 1), 5)}),
                           file=out, flush=True)
