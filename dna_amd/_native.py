@@ -29,6 +29,9 @@ _SIGS = {
     "dna_attn_bwd_ex": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp]),
     "dna_attn_dbias_part_rows": (_i, [_i, _i]),
     "dna_colsum_f32": (_i, [_vp, _i, _i, _vp, _i, _vp]),
+    "dna_causal_conv1d_fwd": (_i, [_vp, _sz, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
+    "dna_causal_conv1d_part_rows": (_sz, [_i, _i]),
+    "dna_causal_conv1d_bwd": (_i, [_vp, _sz, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _sz, _vp, _vp]),
     "dna_hyena_shortconv_fwd": (_i, [_vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     "dna_hyena_shortconv_part_elems": (_sz, [_i, _i, _i, _i, _i]),
     "dna_hyena_shortconv_bwd": (_i, [_vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),

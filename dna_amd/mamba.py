@@ -6,8 +6,18 @@ Caduceus (reference src/models/caduceus/modeling_caduceus.py:68-121) runs two Ma
 This is that op for the Mamba-1 call Mamba.forward makes: A real [dim, d_state], B/C
 input-dependent [batch, d_state, len], D and delta_bias per channel, optional z gating,
 delta_softplus. Forward and backward run dna_amd/csrc/selective_scan.hip; no CPU fallback.
+
+Around it: `Mamba` (mamba_ssm.modules.mamba_simple.Mamba 1.x, restated: same parameters, names
+and forward math on its non-fused path) with the depthwise causal conv1d + SiLU on the HIP
+kernel of dna_amd/csrc/causal_conv.hip, and `BiMambaWrapper` (the reference's own wrapper,
+modeling_caduceus.py:68-121: forward + flipped reverse Mamba, tied in/out projections, "add" or
+"ew_multiply").
 """
+import math
+
 import torch
+import torch.nn as nn
+import torch.nn.functional as F
 
 from . import _native as N
 from .functional import _dt, _gpu, _p, _timed
@@ -75,3 +85,150 @@ def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_
     if B.dim() != 3 or C.dim() != 3:
         raise NotImplementedError("B/C must be input-dependent [batch, d_state, len] (Mamba form)")
     return SelectiveScan.apply(u, delta, A, B, C, D, z, delta_bias, delta_softplus, return_last_state)
+
+
+class CausalConv1d(torch.autograd.Function):
+    """act(conv1d(x, w, b, padding=K-1, groups=C)[..., :L]) on x [B, C, L] (any batch stride,
+    unit channel/position strides), act = SiLU or identity (dna_causal_conv1d_fwd/bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, silu):
+        _gpu(x, weight)
+        B, C, L = x.shape
+        if x.stride(2) != 1 or x.stride(1) != L:
+            x = x.contiguous()
+        K = weight.shape[-1]
+        w = weight.detach().reshape(C, K).float().contiguous()
+        b = None if bias is None else bias.detach().float().contiguous()
+        out = torch.empty(B, C, L, device=x.device, dtype=x.dtype)
+        with _timed("causal_conv_fwd", 2 * B * C * L * x.element_size(), "byte"):
+            N.call("dna_causal_conv1d_fwd", x.data_ptr(), x.stride(0), _dt(x), w.data_ptr(), _p(b),
+                   B, C, L, K, int(bool(silu)), out.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(x, w, b)
+        ctx.cfg = (bool(silu), weight.shape, weight.dtype, bias is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w, b = ctx.saved_tensors
+        silu, wshape, wdtype, has_b = ctx.cfg
+        B, C, L = x.shape
+        K = w.shape[1]
+        dout = dout.contiguous().to(x.dtype)
+        dx = torch.empty(B, C, L, device=x.device, dtype=x.dtype)
+        rows = N.lib().dna_causal_conv1d_part_rows(B, L)
+        part = torch.empty(rows, C * (K + 1), device=x.device, dtype=torch.float32)
+        with _timed("causal_conv_bwd", 3 * B * C * L * x.element_size(), "byte"):
+            N.call("dna_causal_conv1d_bwd", x.data_ptr(), x.stride(0), _dt(x), w.data_ptr(), _p(b),
+                   dout.data_ptr(), B, C, L, K, int(silu), dx.data_ptr(), dx.stride(0),
+                   part.data_ptr(), N.stream_ptr())
+        s = part.sum(0) if (C * (K + 1)) % 64 else None
+        if s is None:
+            s = torch.empty(C * (K + 1), device=x.device, dtype=torch.float32)
+            N.call("dna_colsum_f32", part.data_ptr(), rows, C * (K + 1), s.data_ptr(), 0, N.stream_ptr())
+        s = s.view(C, K + 1)
+        db = s[:, K].contiguous() if has_b else None
+        return dx, s[:, :K].reshape(wshape).to(wdtype), db, None
+
+
+class Mamba(nn.Module):
+    """mamba_ssm.modules.mamba_simple.Mamba (1.x) as Caduceus builds it (BiMambaWrapper,
+    modeling_caduceus.py:88-91): same constructor, parameter names/shapes and initialisation;
+    forward = the reference's non-fused path (in_proj -> causal depthwise conv1d + SiLU -> x_proj
+    -> dt_proj -> selective_scan_fn(delta_softplus, z gating, D) -> out_proj), with the conv and the
+    scan on HIP kernels. mamba_ssm is not vendored in the reference: parity unpinned."""
+
+    def __init__(self, d_model, d_state=16, d_conv=4, expand=2, dt_rank="auto", dt_min=0.001,
+                 dt_max=0.1, dt_init="random", dt_scale=1.0, dt_init_floor=1e-4, conv_bias=True,
+                 bias=False, use_fast_path=True, layer_idx=None, device=None, dtype=None):
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        self.d_model, self.d_state, self.d_conv, self.expand = d_model, d_state, d_conv, expand
+        self.d_inner = int(expand * d_model)
+        self.dt_rank = math.ceil(d_model / 16) if dt_rank == "auto" else dt_rank
+        self.use_fast_path = use_fast_path
+        self.layer_idx = layer_idx
+        self.in_proj = nn.Linear(d_model, self.d_inner * 2, bias=bias, **fk)
+        self.conv1d = nn.Conv1d(self.d_inner, self.d_inner, bias=conv_bias, kernel_size=d_conv,
+                                groups=self.d_inner, padding=d_conv - 1, **fk)
+        self.activation = "silu"
+        self.act = nn.SiLU()
+        self.x_proj = nn.Linear(self.d_inner, self.dt_rank + d_state * 2, bias=False, **fk)
+        self.dt_proj = nn.Linear(self.dt_rank, self.d_inner, bias=True, **fk)
+        dt_init_std = self.dt_rank ** -0.5 * dt_scale
+        if dt_init == "constant":
+            nn.init.constant_(self.dt_proj.weight, dt_init_std)
+        elif dt_init == "random":
+            nn.init.uniform_(self.dt_proj.weight, -dt_init_std, dt_init_std)
+        else:
+            raise NotImplementedError(dt_init)
+        dt = torch.exp(torch.rand(self.d_inner, **fk) * (math.log(dt_max) - math.log(dt_min))
+                       + math.log(dt_min)).clamp(min=dt_init_floor)
+        inv_dt = dt + torch.log(-torch.expm1(-dt))
+        with torch.no_grad():
+            self.dt_proj.bias.copy_(inv_dt)
+        self.dt_proj.bias._no_reinit = True
+        A = torch.arange(1, d_state + 1, dtype=torch.float32, device=device).repeat(self.d_inner, 1)
+        self.A_log = nn.Parameter(torch.log(A))
+        self.A_log._no_weight_decay = True
+        self.D = nn.Parameter(torch.ones(self.d_inner, device=device))
+        self.D._no_weight_decay = True
+        self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **fk)
+
+    def forward(self, hidden_states, inference_params=None):
+        if inference_params is not None:
+            raise NotImplementedError("Mamba: inference_params (recurrent decoding)")
+        batch, seqlen, _ = hidden_states.shape
+        # in_proj computed channel-major, as the reference does (W @ x^T -> [b, 2E, l])
+        xz = (self.in_proj.weight @ hidden_states.reshape(-1, self.d_model).t()).reshape(
+            2 * self.d_inner, batch, seqlen).permute(1, 0, 2)
+        if self.in_proj.bias is not None:
+            xz = xz + self.in_proj.bias.to(xz.dtype)[:, None]
+        A = -torch.exp(self.A_log.float())
+        x, z = xz.chunk(2, dim=1)
+        x = CausalConv1d.apply(x.contiguous(), self.conv1d.weight, self.conv1d.bias, True)
+        x_dbl = self.x_proj(x.transpose(1, 2).reshape(batch * seqlen, self.d_inner))
+        dt, Bm, Cm = torch.split(x_dbl, [self.dt_rank, self.d_state, self.d_state], dim=-1)
+        dt = (self.dt_proj.weight @ dt.t()).reshape(self.d_inner, batch, seqlen).permute(1, 0, 2)
+        Bm = Bm.reshape(batch, seqlen, self.d_state).transpose(1, 2).contiguous()
+        Cm = Cm.reshape(batch, seqlen, self.d_state).transpose(1, 2).contiguous()
+        y = selective_scan_fn(x, dt.contiguous(), A, Bm, Cm, self.D.float(), z=z.contiguous(),
+                              delta_bias=self.dt_proj.bias.float(), delta_softplus=True)
+        return self.out_proj(y.transpose(1, 2))
+
+
+class BiMambaWrapper(nn.Module):
+    """The reference's BiMambaWrapper (modeling_caduceus.py:68-121) over `Mamba` above."""
+
+    def __init__(self, d_model: int, bidirectional: bool = True, bidirectional_strategy="add",
+                 bidirectional_weight_tie: bool = True, **mamba_kwargs):
+        super().__init__()
+        if bidirectional and bidirectional_strategy is None:
+            bidirectional_strategy = "add"
+        if bidirectional and bidirectional_strategy not in ["add", "ew_multiply"]:
+            raise NotImplementedError(f"`{bidirectional_strategy}` strategy for bi-directionality is not implemented!")
+        self.bidirectional = bidirectional
+        self.bidirectional_strategy = bidirectional_strategy
+        self.mamba_fwd = Mamba(d_model=d_model, **mamba_kwargs)
+        if bidirectional:
+            self.mamba_rev = Mamba(d_model=d_model, **mamba_kwargs)
+            if bidirectional_weight_tie:  # in/out projections shared by both directions
+                self.mamba_rev.in_proj.weight = self.mamba_fwd.in_proj.weight
+                self.mamba_rev.in_proj.bias = self.mamba_fwd.in_proj.bias
+                self.mamba_rev.out_proj.weight = self.mamba_fwd.out_proj.weight
+                self.mamba_rev.out_proj.bias = self.mamba_fwd.out_proj.bias
+        else:
+            self.mamba_rev = None
+
+    def forward(self, hidden_states, inference_params=None):
+        out = self.mamba_fwd(hidden_states, inference_params=inference_params)
+        if self.bidirectional:
+            out_rev = self.mamba_rev(hidden_states.flip(dims=(1,)),
+                                     inference_params=inference_params).flip(dims=(1,))
+            if self.bidirectional_strategy == "add":
+                out = out + out_rev
+            elif self.bidirectional_strategy == "ew_multiply":
+                out = out * out_rev
+            else:
+                raise NotImplementedError(self.bidirectional_strategy)
+        return out

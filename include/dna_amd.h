@@ -221,6 +221,21 @@ int dna_hyena_gate_out_fwd(const void* yc, const void* x0, int dtype, int B, int
 int dna_hyena_gate_out_bwd(const void* dy, const void* yc, const void* x0, int dtype, int B, int L,
                            int d, size_t x_bstride, void* dyc, void* dx0, void* stream);
 
+/* ------------------------------------------------------------------ causal depthwise conv1d (+ SiLU)
+ * Mamba.forward's x = silu(conv1d(x)[..., :L]) (depthwise, kernel K = d_conv, padding K-1;
+ * mamba_ssm via modeling_caduceus.py:88-91): x [B, C, L] (batch stride x_bstride elements,
+ * contiguous rows), w [C][K] fp32, bias [C] fp32 or NULL, silu 0/1; out [B, C, L] contiguous.
+ * K in 2..4, dtype f32/bf16, fp32 math. */
+int dna_causal_conv1d_fwd(const void* x, size_t x_bstride, int dtype, const float* w,
+                          const float* bias, int B, int C, int L, int K, int silu, void* out,
+                          void* stream);
+/* Backward: dx (batch stride dx_bstride) written; dw/dbias partials part
+ * [dna_causal_conv1d_part_rows(B, L)][C][K+1] (last column = bias), summed by dna_colsum_f32. */
+size_t dna_causal_conv1d_part_rows(int B, int L);
+int dna_causal_conv1d_bwd(const void* x, size_t x_bstride, int dtype, const float* w,
+                          const float* bias, const void* dout, int B, int C, int L, int K,
+                          int silu, void* dx, size_t dx_bstride, float* part, void* stream);
+
 /* ------------------------------------------------------------------ Mamba selective scan (Caduceus)
  * selective_scan_fn as called by mamba_ssm Mamba.forward inside Caduceus' BiMambaWrapper
  * (src/models/caduceus/modeling_caduceus.py:68-121; mamba_ssm is external and not vendored):

@@ -1,0 +1,59 @@
+"""CPU restatement of the Caduceus BiMamba mixer (torch, float64).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ as the checker; the product path
+(dna_amd.mamba.Mamba / BiMambaWrapper) runs the causal conv and the selective scan on HIP kernels.
+
+PARITY UNPINNED for the Mamba module itself: mamba_ssm (which Caduceus imports,
+src/models/caduceus/modeling_caduceus.py:10) is neither vendored nor installed, so no reference
+output exists here. `mamba_forward` restates the published non-fused path of
+mamba_ssm.modules.mamba_simple.Mamba.forward (mamba-ssm 1.x):
+    xz = in_proj(h) (channel-major) ; x, z = xz.chunk(2)
+    x  = silu(conv1d(x, depthwise, padding d_conv-1)[..., :L])
+    dt, B, C = split(x_proj(x)) ; dt = dt_proj.weight @ dt
+    y  = selective_scan(x, dt, A = -exp(A_log), B, C, D, z, delta_bias = dt_proj.bias, softplus)
+    out = out_proj(y)
+`bimamba_forward` restates the reference's own BiMambaWrapper.forward (:107-121): the forward
+Mamba plus the reverse one on the flipped sequence, flipped back, combined by "add" or
+"ew_multiply" (the reverse direction's in/out projections tied to the forward's, :97-101).
+"""
+import torch
+import torch.nn.functional as F
+
+from .selective_scan_ref import selective_scan_ref
+
+
+def mamba_forward(sd, h, d_state, d_conv, dt_rank, prefix=""):
+    """Mamba.forward (non-fused path) on h [b, l, d_model] with state_dict `sd`."""
+    b, l, _ = h.shape
+    W = sd[prefix + "in_proj.weight"]
+    xz = torch.einsum("ed,bld->bel", W, h)
+    if prefix + "in_proj.bias" in sd and sd[prefix + "in_proj.bias"] is not None:
+        xz = xz + sd[prefix + "in_proj.bias"][:, None]
+    E = W.shape[0] // 2
+    x, z = xz[:, :E], xz[:, E:]
+    x = F.conv1d(x, sd[prefix + "conv1d.weight"], sd.get(prefix + "conv1d.bias"),
+                 padding=d_conv - 1, groups=E)[..., :l]
+    x = F.silu(x)
+    x_dbl = F.linear(x.transpose(1, 2).reshape(b * l, E), sd[prefix + "x_proj.weight"])
+    dt, B, C = torch.split(x_dbl, [dt_rank, d_state, d_state], dim=-1)
+    dt = (sd[prefix + "dt_proj.weight"] @ dt.t()).reshape(E, b, l).permute(1, 0, 2)
+    B = B.reshape(b, l, d_state).transpose(1, 2)
+    C = C.reshape(b, l, d_state).transpose(1, 2)
+    A = -torch.exp(sd[prefix + "A_log"])
+    y = selective_scan_ref(x, dt, A, B, C, D=sd[prefix + "D"], z=z,
+                           delta_bias=sd[prefix + "dt_proj.bias"], delta_softplus=True)
+    out = F.linear(y.transpose(1, 2), sd[prefix + "out_proj.weight"], sd.get(prefix + "out_proj.bias"))
+    return out
+
+
+def bimamba_forward(sd, h, d_state, d_conv, dt_rank, strategy="add", weight_tie=True):
+    """BiMambaWrapper.forward (modeling_caduceus.py:107-121)."""
+    out = mamba_forward(sd, h, d_state, d_conv, dt_rank, prefix="mamba_fwd.")
+    rev_sd = dict(sd)
+    if weight_tie:
+        for k in ("in_proj.weight", "in_proj.bias", "out_proj.weight", "out_proj.bias"):
+            if "mamba_fwd." + k in sd:
+                rev_sd["mamba_rev." + k] = sd["mamba_fwd." + k]
+    out_rev = mamba_forward(rev_sd, h.flip(dims=(1,)), d_state, d_conv, dt_rank,
+                            prefix="mamba_rev.").flip(dims=(1,))
+    return out + out_rev if strategy == "add" else out * out_rev
