@@ -179,8 +179,9 @@ class FusedLayerNorm(torch.autograd.Function):
         dy = None if dy is None else dy.contiguous()
         dyb = None if dyb is None else dyb.contiguous()
         es = x.element_size()
+        # reads dy / dy_bf16, x, residual; writes dx and (with a residual) d(residual) fp32
         nbytes = n * (d * ((4 if dy is not None else 0) + (2 if dyb is not None else 0) + 2 * es
-                           + (4 if residual is not None else 0)) + 8)
+                           + (8 if residual is not None else 0)) + 8)
         with _timed("ln_bwd", nbytes, "byte"):
             N.call("dna_ln_bwd", _p(dy), _p(dyb), x.data_ptr(), _dt(x), _p(bias), act, p, seed,
                    off, _p(residual), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, d,
