@@ -266,6 +266,7 @@ extern "C" int dna_hyena_shortconv_fwd(const void* u, int dtype, const float* w,
   int st = hy_check(B, L, d, order, K, dtype, "dna_hyena_shortconv_fwd");
   if (st) return st;
   DNA_CHECK_ARG(u && w && bias && vx && (order == 2 || xs), "dna_hyena_shortconv_fwd: null pointer");
+  DNA_CHECK_ARG(((uintptr_t)u & 15) == 0, "dna_hyena_shortconv_fwd: u must be 16-byte aligned");
   Fwd a{u, w, bias, B, L, d, order, K, xs, vx};
   const dim3 grid((L + TP - 1) / TP, d / TC, B);
   const size_t lds = (size_t)(order + 1) * (TP + K - 1) * (TC + PAD) * sizeof(float);
@@ -292,6 +293,7 @@ extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w,
   if (st) return st;
   DNA_CHECK_ARG(u && w && bias && dvx && du && part && (order == 2 || dxs),
                 "dna_hyena_shortconv_bwd: null pointer");
+  DNA_CHECK_ARG(((uintptr_t)u & 15) == 0, "dna_hyena_shortconv_bwd: u must be 16-byte aligned");
   Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part};
   const dim3 grid((L + TP - 1) / TP, d / TC, B);
   const size_t lds = (size_t)(order + 1) * ((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) * sizeof(float);
