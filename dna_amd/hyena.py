@@ -12,6 +12,7 @@ import math
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import _native as N
 from .functional import _dt, _gpu, _p, _timed
@@ -84,12 +85,56 @@ class FFTConv(torch.autograd.Function):
                 None if db is None else db.reshape(bshape), None)
 
 
+def bidirectional_pad_before(L):
+    """fftconv_ref pads L//2 zeros on each side of u (total L + 2*(L//2)) and transforms at
+    n = 2L (hyena.py:68-72): u starts at padded_length//2 - L//2 of the size-2L window."""
+    padded = L + 2 * (L // 2)
+    return padded // 2 - L // 2
+
+
+def _kernel_len(n):
+    """Smallest length the FFT kernels take that is >= n (powers of two from 64)."""
+    return max(64, 1 << (int(n) - 1).bit_length())
+
+
+MAX_KERNEL_LEN = 131072
+
+
 def fftconv(u, k, D, dropout_mask=None, gelu=False, k_rev=None, bidirectional=False):
     """`fftconv_ref` on the GPU (hyena.py:60-92). Supported: dropout_mask=None, gelu=False,
-    k_rev=None (the HyenaFilter call); output dtype = u's dtype, as in the reference."""
+    k_rev=None (the HyenaFilter call); output dtype = u's dtype, as in the reference.
+
+    Any sequence length L, with the reference's exact semantics:
+      * L a power of two in [64, 131072]: the native causal / bidirectional kernels;
+      * causal, other L: u and k zero-padded to the next kernel length (a linear convolution is
+        unchanged by trailing zeros), output sliced to L;
+      * bidirectional, other L: the reference's circular convolution of size 2L,
+        y[t] = sum_j k[j] u~[(t - j) mod 2L], equals the linear convolution of k with
+        roll(u~, L) read at offset L -- run as a causal convolution of kernel length >= 2L, with
+        the D*u term added as the reference adds it (u * D.unsqueeze(-1)).
+    Gradients flow through the pads / roll / slices (exact)."""
     if dropout_mask is not None or gelu or k_rev is not None:
         raise NotImplementedError("fftconv: dropout_mask / gelu / k_rev (unused by HyenaFilter)")
-    return FFTConv.apply(u, k, D, bidirectional)
+    L = u.shape[-1]
+    if L == _kernel_len(L) and L <= MAX_KERNEL_LEN:
+        return FFTConv.apply(u, k, D, bidirectional)
+    if not bidirectional:
+        Lp = _kernel_len(L)
+        if Lp > MAX_KERNEL_LEN:
+            raise NotImplementedError(f"fftconv: L={L} > {MAX_KERNEL_LEN}")
+        y = FFTConv.apply(F.pad(u, (0, Lp - L)), F.pad(k, (0, Lp - L)), D, False)
+        return y[..., :L]
+    N = 2 * L
+    pb = bidirectional_pad_before(L)
+    ut = F.pad(u, (pb, N - L - pb))
+    v = torch.cat([ut[..., L:], ut[..., :L]], dim=-1)          # roll(u~, L)
+    Lp = _kernel_len(N)
+    if Lp > MAX_KERNEL_LEN:
+        raise NotImplementedError(f"fftconv: bidirectional L={L} needs kernel length {Lp} > {MAX_KERNEL_LEN}")
+    y = FFTConv.apply(F.pad(v, (0, Lp - N)), F.pad(k, (0, Lp - L)), None, False)[..., L:N]
+    if D is not None:
+        y = y + u * D.unsqueeze(-1)
+    return y.to(u.dtype)
 
 
 # --------------------------------------------------------------------------- Hyena operator

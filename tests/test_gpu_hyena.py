@@ -82,8 +82,9 @@ def test_fftconv_linearity_and_errors():
     assert (lhs - rhs).abs().max().item() < 1e-4 * rhs.abs().max().item()
     with pytest.raises(NotImplementedError):
         fftconv(u1, k, b, gelu=True)
-    with pytest.raises(Exception):
-        fftconv(u1[..., :1000], k[..., :1000], b)  # L not a power of 2
+    with pytest.raises(NotImplementedError):  # bidirectional, L not a kernel size, 2L > 131072
+        fftconv(torch.zeros(1, 4, 70000, device=DEV), torch.zeros(4, 70000, device=DEV), b,
+                bidirectional=True)
     with pytest.raises(RuntimeError):
         fftconv(u1.cpu(), k.cpu(), b.cpu())       # GPU only, no fallback
 
@@ -190,3 +191,61 @@ def test_hyena_fused_kernels_vs_torch(dtype, tol, B, L, d, order, K):
     assert _rel(xs2.grad[:, 0].float().cpu().numpy(), (dyt * yc.detach().float()).cpu().numpy()) < tol
     if order > 2:
         assert xs2.grad[:, 1:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("bi", [False, True])
+@pytest.mark.parametrize("B,D,L,five_d", [(2, 3, 130, True), (1, 4, 65, False), (3, 2, 1000, True),
+                                          (2, 5, 33, False), (1, 2, 1026, True), (2, 3, 4000, False)])
+def test_fftconv_any_length_vs_oracle(B, D, L, five_d, bi):
+    """Lengths that are not a kernel size (BPE configs use 130, char configs 1026): causal via
+    zero padding, bidirectional via the rolled causal construction; fwd and du/dk/dbias vs the
+    float64 oracle (fftconv_ref semantics at the same L)."""
+    from dna_amd.hyena import fftconv
+    rng = np.random.default_rng(L * 7 + D + int(bi))
+    shape = (B, 1, D, 1, L) if five_d else (B, D, L)
+    u = rng.standard_normal(shape).astype(np.float32)
+    k = (rng.standard_normal((D, L)) * np.exp(-np.linspace(0, 3, L))[None]).astype(np.float32)
+    bias = rng.standard_normal((1, D, 1)).astype(np.float32)
+    dy = rng.standard_normal(shape).astype(np.float32)
+    ur = u.reshape(B, D, L)
+    y_ref = H.fftconv_fwd(ur, k, bias, bidirectional=bi)
+    du_ref, dk_ref, db_ref = H.fftconv_bwd(dy.reshape(B, D, L), ur, k, bias, bidirectional=bi)
+    ut = torch.tensor(u, device=DEV, requires_grad=True)
+    kt = torch.tensor(k, device=DEV, requires_grad=True)
+    # the reference adds u * D.unsqueeze(-1): D is [1, D, 1] for the operator's 5-D layout and
+    # per channel [D] for a 3-D input
+    bt = torch.tensor(bias if five_d else bias.reshape(D), device=DEV, requires_grad=True)
+    y = fftconv(ut, kt, bt, bidirectional=bi)
+    assert y.shape == ut.shape and y.dtype == torch.float32
+    assert _rel(y.detach().cpu().numpy().reshape(B, D, L), y_ref) < 2e-5
+    y.backward(torch.tensor(dy, device=DEV))
+    assert _rel(ut.grad.cpu().numpy().reshape(B, D, L), du_ref) < 2e-5
+    assert _rel(kt.grad.cpu().numpy(), dk_ref) < 2e-5
+    assert _rel(bt.grad.cpu().numpy().reshape(-1), np.asarray(db_ref).reshape(-1)) < 2e-5
+
+
+def test_hyena_operator_bpe_length_vs_oracle():
+    """HyenaDNA BPE config length (pad_max_length 130): fused operator path (d_model 64),
+    bidirectional, fwd + input/parameter grads vs the float64 operator oracle."""
+    from oracle import hyena_operator_ref as HO
+    L, d_model = 130, 64
+    op, sd64 = _op_state(d_model, L, 2, seed=21, filter_order=16, emb_dim=5, bidirectional=True, w=10)
+    op = op.to(DEV)
+    buffers = {n for n, _ in op.named_buffers()}
+    ref_sd = {k: v.clone().requires_grad_(k not in buffers) for k, v in sd64.items()}
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(3, L, d_model, generator=g, dtype=torch.float64)
+    dy = torch.randn(3, L, d_model, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    yr = HO.hyena_operator(ref_sd, xr, d_model, order=2, l_max=L, bidirectional=True)
+    yr.backward(dy)
+    xg = x.float().to(DEV).requires_grad_(True)
+    y = op(xg)
+    assert _rel(y.detach().cpu().numpy(), yr.detach().numpy()) < 5e-5
+    y.backward(dy.float().to(DEV))
+    assert _rel(xg.grad.cpu().numpy(), xr.grad.numpy()) < 5e-5
+    for n, p in op.named_parameters():
+        ref = ref_sd[n].grad
+        if n.endswith("freq"):
+            ref = sum(ref_sd[kk].grad for kk in ref_sd if kk.endswith("freq"))
+        assert _rel(p.grad.cpu().numpy(), ref.numpy()) < 2e-4, n
