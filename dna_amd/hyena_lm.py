@@ -1,0 +1,166 @@
+"""HyenaDNA language model around the HIP Hyena operator (BASELINE config D).
+
+Mirrors the reference's `LMBackbone` / `BertLMHeadModel` (registry model "blm",
+src/models/sequence/long_conv_lm.py:320-682) as configs/experiment/hyena-dna/*.yaml build it:
+token embeddings (GPT2Embeddings, no positions), `n_layer` pre-norm blocks of
+[dropout -> add -> LayerNorm -> HyenaOperator] and [dropout -> add -> LayerNorm -> Mlp(fc1, GELU
+tanh, fc2)], a final dropout -> add -> LayerNorm, and an LM head tied to the embedding table.
+The Block / Mlp / GPT2Embeddings modules come from flash_attn in the reference (not installed
+here), so their forward is restated from flash_attn's published code (prenorm Block with
+residual_in_fp32) with the same parameter names -- parity of the backbone is unpinned; the
+Hyena operator inside is pinned (oracle/hyena_operator_ref.py). The long convolution and the
+operator's data movement run on HIP kernels; embeddings, LayerNorm, MLP and head are torch ops.
+"""
+from collections import namedtuple
+from functools import partial
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .hyena import HyenaOperator
+
+
+CausalLMOutput = namedtuple("CausalLMOutput", ["logits"])
+
+
+class GPT2Embeddings(nn.Module):
+    """flash_attn.modules.embedding.GPT2Embeddings: word (+ optional learned position)."""
+
+    def __init__(self, embed_dim, vocab_size, max_position_embeddings, padding_idx=None,
+                 device=None, dtype=None):
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        self.word_embeddings = nn.Embedding(vocab_size, embed_dim, padding_idx=padding_idx, **fk)
+        self.max_position_embeddings = max_position_embeddings
+        if max_position_embeddings > 0:
+            self.position_embeddings = nn.Embedding(max_position_embeddings, embed_dim, **fk)
+
+    def forward(self, input_ids, position_ids=None):
+        h = self.word_embeddings(input_ids)
+        if self.max_position_embeddings > 0:
+            if position_ids is None:
+                position_ids = torch.arange(input_ids.shape[1], device=input_ids.device)
+            h = h + self.position_embeddings(position_ids)
+        return h
+
+
+class Mlp(nn.Module):
+    """flash_attn.modules.mlp.Mlp: fc2(act(fc1(x)))."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None,
+                 activation=partial(F.gelu, approximate="tanh"), device=None, dtype=None):
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        hidden_features = hidden_features or in_features * 4
+        self.fc1 = nn.Linear(in_features, hidden_features, **fk)
+        self.activation = activation
+        self.fc2 = nn.Linear(hidden_features, out_features or in_features, **fk)
+
+    def forward(self, x):
+        return self.fc2(self.activation(self.fc1(x)))
+
+
+class Block(nn.Module):
+    """flash_attn.modules.block.Block with prenorm=True (the reference's create_block,
+    long_conv_lm.py:205-267): returns (hidden_states, residual)."""
+
+    def __init__(self, dim, mixer, mlp, norm_eps=1e-5, resid_dropout1=0.0, resid_dropout2=0.0,
+                 residual_in_fp32=False):
+        super().__init__()
+        self.mixer = mixer
+        self.dropout1 = nn.Dropout(resid_dropout1)
+        self.norm1 = nn.LayerNorm(dim, eps=norm_eps)
+        self.mlp = mlp
+        self.dropout2 = nn.Dropout(resid_dropout2)
+        self.norm2 = nn.LayerNorm(dim, eps=norm_eps)
+        self.residual_in_fp32 = residual_in_fp32
+
+    def forward(self, hidden_states, residual=None):
+        dropped = self.dropout1(hidden_states)
+        residual = dropped + residual if residual is not None else dropped
+        hidden_states = self.norm1(residual.to(dtype=self.norm1.weight.dtype))
+        if self.residual_in_fp32:
+            residual = residual.to(torch.float32)
+        hidden_states = self.mixer(hidden_states)
+        dropped = self.dropout2(hidden_states)
+        residual = dropped + residual
+        hidden_states = self.norm2(residual.to(dtype=self.norm2.weight.dtype))
+        if self.residual_in_fp32:
+            residual = residual.to(torch.float32)
+        return self.mlp(hidden_states), residual
+
+
+def _init_weights(module, n_layer, initializer_range=0.02, rescale_prenorm_residual=True):
+    """long_conv_lm.py:270-318 (reseeds with 2222 per module, as the reference does)."""
+    torch.manual_seed(2222)
+    if isinstance(module, nn.Linear):
+        nn.init.normal_(module.weight, std=initializer_range)
+        if module.bias is not None:
+            nn.init.zeros_(module.bias)
+    elif isinstance(module, nn.Embedding):
+        nn.init.normal_(module.weight, std=initializer_range)
+    if rescale_prenorm_residual:
+        for name, p in module.named_parameters():
+            if name in ["out_proj.weight", "fc2.weight"]:
+                nn.init.kaiming_normal_(p)
+
+
+class LMBackbone(nn.Module):
+    """long_conv_lm.py:320-576 (layer = a Hyena operator config; no attention layers)."""
+
+    def __init__(self, d_model, n_layer, d_inner, vocab_size, layer=None, attn_layer_idx=None,
+                 attn_cfg=None, max_position_embeddings=0, resid_dropout=0.0, embed_dropout=0.1,
+                 layer_norm_epsilon=1e-5, initializer_cfg=None, fused_mlp=False,
+                 fused_dropout_add_ln=False, residual_in_fp32=False, checkpoint_mlp=False,
+                 checkpoint_mixer=False, device=None, dtype=None, **kwargs):
+        super().__init__()
+        if attn_layer_idx:
+            raise NotImplementedError("LMBackbone: attention layers (flash_attn MHA) are out of scope")
+        if fused_mlp or fused_dropout_add_ln:
+            raise NotImplementedError("fused_mlp / fused_dropout_add_ln (flash_attn CUDA extensions)")
+        layer = dict(layer or {})
+        name = layer.pop("_name_", "hyena")
+        if name != "hyena":
+            raise NotImplementedError(f"LMBackbone layer {name!r} (hyena only)")
+        self.residual_in_fp32 = residual_in_fp32
+        self.embeddings = GPT2Embeddings(d_model, vocab_size, max_position_embeddings)
+        self.layers = nn.ModuleList([
+            Block(d_model, HyenaOperator(d_model, layer_idx=i, **layer),
+                  Mlp(d_model, hidden_features=d_inner), norm_eps=layer_norm_epsilon,
+                  resid_dropout1=embed_dropout if i == 0 else resid_dropout,
+                  resid_dropout2=resid_dropout, residual_in_fp32=residual_in_fp32)
+            for i in range(n_layer)])
+        self.drop_f = nn.Dropout(resid_dropout)
+        self.ln_f = nn.LayerNorm(d_model, eps=layer_norm_epsilon)
+        self.apply(partial(_init_weights, n_layer=n_layer, **(initializer_cfg or {})))
+
+    def forward(self, input_ids, position_ids=None):
+        hidden_states = self.embeddings(input_ids, position_ids=position_ids)
+        residual = None
+        for layer in self.layers:
+            hidden_states, residual = layer(hidden_states, residual)
+        dropped = self.drop_f(hidden_states)
+        residual = dropped + residual if residual is not None else dropped
+        return self.ln_f(residual.to(dtype=self.ln_f.weight.dtype))
+
+
+class BertLMHeadModel(nn.Module):
+    """Registry model "blm" (long_conv_lm.py:578-682): backbone + LM head tied to the
+    embeddings; forward((input_ids, mask)) -> (CausalLMOutput(logits=(logits, mask)), None)."""
+
+    def __init__(self, d_model, n_layer, d_inner, vocab_size, pad_vocab_size_multiple=1, **kwargs):
+        super().__init__()
+        if vocab_size % pad_vocab_size_multiple:
+            vocab_size += pad_vocab_size_multiple - vocab_size % pad_vocab_size_multiple
+        self.backbone = LMBackbone(d_model, n_layer, d_inner, vocab_size, **kwargs)
+        self.lm_head = nn.Linear(d_model, vocab_size, bias=False)
+        self.apply(partial(_init_weights, n_layer=n_layer,
+                           **(kwargs.get("initializer_cfg") or {})))
+        self.lm_head.weight = self.backbone.embeddings.word_embeddings.weight
+
+    def forward(self, input_ids, position_ids=None, inference_params=None, state=None):
+        mask = input_ids[1]
+        ids = input_ids[0]
+        logits = self.lm_head(self.backbone(ids, position_ids=position_ids))
+        return CausalLMOutput(logits=(logits, mask)), None

@@ -1,0 +1,70 @@
+#!/usr/bin/env python
+"""HyenaDNA LM training step at BASELINE config D scale: HyenaDNA-small (d_model 256, 8 layers,
+d_inner 1024, order 2, filter_order 64, emb_dim 5, bidirectional -- SURVEY §8f row 1) at
+seq_len 65536, char vocabulary (12 -> 16), bf16 autocast, on 1 GPU. One step = fwd + CE over the
+15 %-masked positions + bwd + fused AdamW. Synthetic uniform ACGT tokens, random init.
+Reports sequences/s and tokens/s and the share of the HIP long-conv / operator kernels."""
+import argparse
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dna_amd.functional import OpTimer  # noqa: E402
+from dna_amd.hyena_lm import BertLMHeadModel  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=2)
+    ap.add_argument("--L", type=int, default=65536)
+    ap.add_argument("--layers", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=5)
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    layer = {"_name_": "hyena", "emb_dim": 5, "filter_order": 64, "short_filter_order": 3,
+             "l_max": a.L, "modulate": True, "w": 10, "lr_pos_emb": 0.0, "bidirectional": True}
+    m = BertLMHeadModel(d_model=256, n_layer=a.layers, d_inner=1024, vocab_size=12,
+                        pad_vocab_size_multiple=8, embed_dropout=0.1, residual_in_fp32=True,
+                        layer=layer).cuda()
+    opt = torch.optim.AdamW(m.parameters(), lr=6e-4, weight_decay=0.1, fused=True)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    ids = torch.randint(7, 11, (a.B, a.L), device="cuda", generator=g)   # A C G T char ids
+    masked = torch.rand(a.B, a.L, device="cuda", generator=g) < 0.15
+    inp = torch.where(masked, torch.full_like(ids, 3), ids)              # [MASK] = 3
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            (out, _) = m((inp, masked))
+            logits = out.logits[0]
+        loss = F.cross_entropy(logits[masked].float(), ids[masked])
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    timer = OpTimer()
+    timer.__enter__()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    timer.__exit__()
+    summ = timer.summary()
+    own = sum(n * t for k, (n, t, u, kind) in summ.items()) / a.steps
+    print(f"HyenaDNA-small (d256 x{a.layers}) L={a.L} B={a.B} bf16 train step: {dt * 1e3:.1f} ms, "
+          f"{a.B / dt:.2f} seq/s, {a.B * a.L / dt:.0f} tokens/s, loss {loss.item():.3f}; HIP Hyena "
+          f"kernels {own:.1f} ms ({own / (dt * 1e3):.0%}): "
+          + ", ".join(f"{k} {t:.3f} ms x{n / a.steps:.0f}" for k, (n, t, u, kind) in summ.items()),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()

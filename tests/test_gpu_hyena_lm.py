@@ -1,0 +1,48 @@
+"""GPU: HyenaDNA LM (blm) logits and gradients vs the float64 backbone oracle
+(oracle/hyena_lm_ref.py: the Hyena operator pinned to the reference, the flash_attn Block/Mlp
+restated -- unpinned). Eval mode; tolerances fwd 1e-4, grads 2e-3 relative."""
+import pytest
+import torch
+
+from oracle import hyena_lm_ref as LM
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+@pytest.mark.parametrize("d_model,L,bi", [(64, 256, True), (64, 130, True), (32, 512, False)])
+def test_hyena_lm_vs_oracle(d_model, L, bi):
+    from dna_amd.hyena_lm import BertLMHeadModel
+    layer = {"_name_": "hyena", "emb_dim": 5, "filter_order": 16, "short_filter_order": 3,
+             "l_max": L, "modulate": True, "w": 10, "lr_pos_emb": 0.0, "bidirectional": bi}
+    m = BertLMHeadModel(d_model=d_model, n_layer=2, d_inner=4 * d_model, vocab_size=16,
+                        embed_dropout=0.0, residual_in_fp32=True, layer=layer)
+    torch.manual_seed(3)
+    with torch.no_grad():  # break the reference init's identical-weights symmetry
+        for n, p in m.named_parameters():
+            if not n.endswith("freq"):
+                p.add_(torch.randn_like(p) * 0.02)
+    buffers = {n for n, _ in m.named_buffers()}
+    sd = {k: v.detach().double().clone().requires_grad_(k not in buffers) for k, v in m.state_dict().items()}
+    sd["lm_head.weight"] = sd["backbone.embeddings.word_embeddings.weight"]  # tied
+    m = m.to(DEV).eval()
+    ids = torch.randint(0, 16, (2, L), generator=torch.Generator().manual_seed(4))
+    mask = torch.ones(2, L, dtype=torch.bool)
+    ref = LM.lm_logits(sd, ids, d_model, 2, l_max=L, bidirectional=bi)
+    (out, _) = m((ids.to(DEV), mask.to(DEV)))
+    logits = out.logits[0]
+    assert _rel(logits, ref) < 1e-4
+    g = torch.randn(ref.shape, generator=torch.Generator().manual_seed(5), dtype=torch.float64)
+    ref.backward(g)
+    logits.backward(g.float().to(DEV))
+    for n, p in m.named_parameters():
+        r = sd[n].grad
+        if n.endswith("freq"):
+            pre = n[: n.index("implicit_filter.")]
+            r = sum(sd[k].grad for k in sd if k.startswith(pre) and k.endswith("freq"))
+        assert _rel(p.grad, r) < 2e-3, n
