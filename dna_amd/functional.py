@@ -5,6 +5,7 @@ the vendor library (hipBLASLt through torch.mm), with fp32 weight-gradient outpu
 No CPU fallback: every op raises if the native library is missing or a tensor is not on a GPU.
 """
 import math
+import os
 
 import torch
 
@@ -350,9 +351,13 @@ class Linear(torch.autograd.Function):
         return dx, dw, None, db
 
 
-def wgrad_splits(rows, m, n, target_tiles=512, max_splits=16):
+def wgrad_splits(rows, m, n, target_tiles=512, max_splits=None):
     """Split-K factor for dW = dY^T X: the contraction runs over all `rows` tokens while the
-    output has only (m/256)*(n/256) tiles (9..72 for DNABERT-2), far fewer than 256 CUs."""
+    output has only (m/256)*(n/256) tiles (9..72 for DNABERT-2), far fewer than 256 CUs.
+    Smallest power of two giving >= target_tiles tiles, capped at 64 (measured at b=256: Wqkv
+    545 us at s=32 vs 635-738 at s=16; Wg best at 8, Wwo at 16, Wo flat from 16 to 64)."""
+    if max_splits is None:
+        max_splits = int(os.environ.get("DNA_WGRAD_MAX_SPLITS", 64))
     tiles = max(1, (m // 256) * (n // 256))
     s = 1
     while s < max_splits and tiles * s < target_tiles:
