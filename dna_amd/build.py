@@ -27,6 +27,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-I", INCLUDE, "-I", CSRC,
              "-mllvm", "-amdgpu-mfma-vgpr-form",
              "-Wno-unused-result"]
+# per-file extra device flags. attention.hip: scores are never NaN, and without -fno-honor-nans
+# every fmaxf of an MFMA result gets a canonicalising v_max in front of it; the SLP vectoriser
+# turns the per-score multiplies into v_pk_mul_f32 on odd register pairs (v_mov/v_alignbit
+# shuffles around every pair, and packed f32 beside MFMAs is slower anyway)
+FILE_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize"]}
 CXX_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-I", INCLUDE, "-I", CSRC, "-Wall",
              "-Wno-unused-function"]
 
@@ -41,7 +46,7 @@ def _compile(src):
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
         return obj, None
     if src.endswith(".hip"):
-        cmd = [HIPCC] + HIP_FLAGS + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + HIP_FLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     else:
         cmd = ["g++"] + CXX_FLAGS + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -17,6 +17,10 @@
 //
 // fp32 path: exact-arithmetic reference-grade kernels (one thread per query / key) used for the
 // 1e-3 fp32 parity mode; not a throughput path.
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "common.h"
 
 namespace dna {
@@ -39,10 +43,12 @@ typedef __attribute__((ext_vector_type(4))) short s16x4;
 //  * transposed reads (ds_read_b64_tr_b16, a 32-lane half reads rows r0..r0+3, 4 chunks): rows r0
 //    and r0+2 must land in different chunk halves, i.e. their keys differ in bit 2 -- so the key
 //    is the bit-reversal of (r>>1)&7.
-__device__ __forceinline__ int swz(int r, int c) {
+__device__ __forceinline__ int swz_key(int r) {
   const int k = (r >> 1) & 7;
-  const int key = ((k & 1) << 2) | (k & 2) | ((k >> 2) & 1);
-  return r * D + ((((c >> 3) ^ key) & 7) << 3) + (c & 7);
+  return ((k & 1) << 2) | (k & 2) | ((k >> 2) & 1);
+}
+__device__ __forceinline__ int swz(int r, int c) {
+  return r * D + ((((c >> 3) ^ swz_key(r)) & 7) << 3) + (c & 7);
 }
 
 __device__ __forceinline__ bf16x4 tr_read(const bf16* lds_elem_ptr) {
@@ -288,6 +294,254 @@ __global__ __launch_bounds__(256) void fwd_bf16_kernel(const bf16* __restrict__ 
         *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * g + 4 * hh) = v;
       }
     if (hh == 0) lse[((size_t)b * H + h) * S + qi] = (m + __log2f(ltot)) * LN2;
+  }
+}
+
+// ----------------------------------------------------------------------------- bf16 forward, v2
+// Same math as fwd_bf16_kernel, reorganised for issue rate (the v1 loop was VALU-issue bound on
+// per-score bias arithmetic and per-tile address recomputation):
+//  * a wave owns 64 queries = two 32-query blocks, so every K row read and V transposed read
+//    from LDS feeds two MFMAs; a workgroup (4 waves) owns 256 queries of one (batch, head);
+//  * ALiBi enters the MFMA as the initial accumulator: for a 32-key half that lies wholly left
+//    (right) of a 32-query block the bias is slope*(key offset) + a per-lane constant U, and the
+//    key-offset part is a loop-invariant vector (+/- slope/scale * a_r) passed as the C operand.
+//    A score then costs max3/2 + one FMA + v_exp + one add + cvt/2; only the diagonal half and
+//    halves containing pad keys take the explicit per-score bias path;
+//  * deferred rescaling: the running max m only moves when a half-tile's max exceeds it by more
+//    than DEFER log2 units (P values stay <= 2^DEFER, exact in bf16/fp32 range);
+//  * the cross-lane-half max/sum is one v_permlane32_swap; LDS addresses are per-lane constants
+//    plus immediates.
+constexpr int BQ2 = 256;          // queries per workgroup (4 waves x 64)
+constexpr float DEFER = 8.0f;     // log2 units
+
+__device__ __forceinline__ float pair_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                            __builtin_bit_cast(unsigned, x), false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                            __builtin_bit_cast(unsigned, x), false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+// fmaxf of three. This file is compiled with -fno-honor-nans (dna_amd/build.py): scores are never
+// NaN, and without it the compiler puts an IEEE-mode canonicalising v_max before every fmaxf of
+// an MFMA result. (Inline asm is no way round that: the hazard recognizer does not see an asm
+// statement reading an MFMA result, so it would read stale accumulators.)
+__device__ __forceinline__ float max3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
+// key offset (within a 32-key half, lane half hh excluded) of accumulator register r
+__device__ __forceinline__ constexpr int aoff(int r) { return (r & 3) + 8 * (r >> 2); }
+
+__global__ __launch_bounds__(256, 2) void fwd2_bf16_kernel(const bf16* __restrict__ qkv,
+                                                           const uint8_t* __restrict__ key_valid,
+                                                           const float* __restrict__ slopes,
+                                                           int S, int H, float c,
+                                                           bf16* __restrict__ out,
+                                                           float* __restrict__ lse) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Ks = reinterpret_cast<bf16*>(smem);               // [2][64*64] swizzled
+  bf16* Vs = Ks + 2 * BK * D;                             // [2][64*64] swizzled
+  float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);  // [2][64] pad bias (log2 units)
+
+  int qblk, h, b;
+  decode_block((S + BQ2 - 1) / BQ2, H, qblk, h, b);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches stay uniform
+  const int ql = lane & 31, hh = lane >> 5;
+  const int ld = 3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * ld;
+  const int q0 = qblk * BQ2 + wave * 64;
+  const float slope2 = slopes[h] * LOG2E;
+  const float sl_t = slope2 / c;  // ALiBi slope in raw-score units
+  const float invc = 1.f / c;
+
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qrow = min(q0 + 32 * j + ql, S - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[j][s] = *reinterpret_cast<const bf16x8*>(base + (size_t)qrow * ld + h * D + 16 * s + 8 * hh);
+  }
+  f32x16 initL, initR;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    initL[r] = sl_t * (float)aoff(r);
+    initR[r] = -initL[r];
+  }
+
+  // per-lane LDS element offsets (tile buffer, kh and s add immediates)
+  int so[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int cidx = tid + i * 256;
+    so[i] = swz(cidx >> 3, (cidx & 7) * 8);
+  }
+  int kro[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) kro[s] = swz(ql, 16 * s + 8 * hh);
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int vr0 = 4 * (g16 >> 1) + (i16 >> 2);
+  int vro[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+    vro[dt][0] = swz(vr0, dcol);
+    vro[dt][1] = swz(vr0 + 8, dcol);
+  }
+
+  auto load_tile = [&](int kt, TileRegs& t, float& bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cidx = tid + i * 256;
+      const bf16* src = base + (size_t)(kt * BK + (cidx >> 3)) * ld + h * D + (cidx & 7) * 8;
+      t.k[i] = *reinterpret_cast<const bf16x8*>(src + H * D);
+      t.v[i] = *reinterpret_cast<const bf16x8*>(src + 2 * H * D);
+    }
+    bias = 0.f;
+    if (tid < BK && key_valid) bias = key_valid[(size_t)b * S + kt * BK + tid] ? 0.f : PAD_BIAS * LOG2E;
+  };
+  auto store_tile = [&](int buf, const TileRegs& t, float bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<bf16x8*>(Ks + buf * BK * D + so[i]) = t.k[i];
+      *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + so[i]) = t.v[i];
+    }
+    if (tid < BK) kb[buf * BK + tid] = bias;
+  };
+
+  f32x16 o[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o[j][0][i] = 0.f; o[j][1][i] = 0.f; }
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+
+  const int nt = S / BK;
+  const int kt0 = (qblk * (BQ2 / BK) + 1) % nt;  // near-diagonal tiles first
+  {
+    TileRegs t; float bias;
+    load_tile(kt0, t, bias);
+    store_tile(0, t, bias);
+  }
+  __syncthreads();
+
+  for (int it = 0; it < nt; ++it) {
+    int kt = kt0 + it;
+    if (kt >= nt) kt -= nt;
+    const int buf = it & 1;
+    TileRegs nx; float nbias = 0.f;
+    if (it + 1 < nt) load_tile(kt + 1 < nt ? kt + 1 : kt + 1 - nt, nx, nbias);
+
+    const bf16* K = Ks + buf * BK * D;
+    const bf16* V = Vs + buf * BK * D;
+    const float* kbias = kb + buf * BK;
+    const bool haspad = key_valid && wave_any(kbias[lane] != 0.f);
+
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int kb2 = kt * BK + 32 * kh;  // first key of this half
+      bf16x8 kf[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        kf[s] = *reinterpret_cast<const bf16x8*>(K + kh * 32 * D + kro[s]);
+      bf16x8 pbf[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int qf0 = q0 + 32 * j;  // wave-uniform
+        const int qi = qf0 + ql;
+        const bool generic = haspad || kb2 == qf0;
+        const bool left = kb2 < qf0;
+        // every path leaves true score (log2 units) = sacc * c + U, U a per-lane constant, so
+        // the max / exp tail below is one code path (no per-path vector phis)
+        f32x16 sacc;
+        float U = 0.f;
+        if (!generic) {
+          if (left) sacc = mfma(kf[0], qf[j][0], initL);
+          else sacc = mfma(kf[0], qf[j][0], initR);
+#pragma unroll
+          for (int s = 1; s < 4; ++s) sacc = mfma(kf[s], qf[j][s], sacc);
+          const float dqk = (float)(kb2 + 4 * hh - qi);
+          U = left ? slope2 * dqk : -slope2 * dqk;
+        } else {
+          f32x16 zero;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) zero[r] = 0.f;
+          sacc = mfma(kf[0], qf[j][0], zero);
+#pragma unroll
+          for (int s = 1; s < 4; ++s) sacc = mfma(kf[s], qf[j][s], sacc);
+          const float dqk = (float)(kb2 + 4 * hh - qi);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + 32 * kh + 8 * g + 4 * hh);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g + e;
+              sacc[r] = fmaf(fmaf(-slope2, fabsf(dqk + (float)aoff(r)), pb[e]), invc, sacc[r]);
+            }
+          }
+        }
+        float mx = max3(sacc[0], sacc[1], sacc[2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) mx = max3(mx, sacc[r], sacc[r + 1]);
+        float tm = pair_max(fmaf(fmaxf(mx, sacc[15]), c, U));
+        if (wave_any(tm > m[j] + DEFER)) {
+          const float mn = fmaxf(m[j], tm);
+          const float alpha = ex2(m[j] - mn);
+          m[j] = mn;
+          l[j] *= alpha;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) { o[j][0][i] *= alpha; o[j][1][i] *= alpha; }
+        }
+        float ps = 0.f;
+        const float off = U - m[j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = ex2(fmaf(sacc[r], c, off));
+          sacc[r] = p;
+          ps += p;
+        }
+        l[j] += ps;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pbf[j][s][e] = (bf16)sacc[8 * s + e];
+      }
+      // O^T += V^T P^T over the 32 keys of this half (2 k-steps of 16), V reads shared by j
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16* vb = V + (kh * 32 + 16 * s) * D;
+          const bf16x8 a = cat(tr_read(vb + vro[dt][0]), tr_read(vb + vro[dt][1]));
+          o[0][dt] = mfma(a, pbf[0][s], o[0][dt]);
+          o[1][dt] = mfma(a, pbf[1][s], o[1][dt]);
+        }
+    }
+    if (it + 1 < nt) store_tile(buf ^ 1, nx, nbias);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qi = q0 + 32 * j + ql;
+    const float ltot = pair_sum(l[j]);
+    const float inv = 1.f / ltot;
+    if (qi < S) {
+      bf16* orow = out + ((size_t)b * S + qi) * (H * D) + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (bf16)(o[j][dt][4 * g + e] * inv);
+          *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * g + 4 * hh) = v;
+        }
+      if (hh == 0) lse[((size_t)b * H + h) * S + qi] = (m[j] + __log2f(ltot)) * LN2;
+    }
   }
 }
 
@@ -667,6 +921,358 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
   }
 }
 
+// ----------------------------------------------------------------------------- bf16 backward, v2
+// Same decomposition as dq_bf16_kernel / dkdv_bf16_kernel (no atomics, deterministic) with the
+// per-score VALU work cut the way fwd2_bf16_kernel does it:
+//  * row constants enter the MFMAs as initial accumulators. dK/dV kernel (queries on rows):
+//    S starts from (-LSE2 -+ slope2*q)/c, so with the per-lane (key) constant U = +-slope2*k +
+//    pad(k), P = exp2(S*c + U) is one FMA + v_exp; dP starts from -delta, so dS = P * dP.
+//    dQ kernel (queries on lanes): S^T starts from the +-slope/scale*offset vector of a
+//    separable block, dP^T from -delta;
+//  * blocks are classified per 32x32 (before / after / diagonal) with scalar branches; only
+//    diagonal blocks (and, in the dQ kernel, key tiles with pad keys) compute |q - k| per score.
+__global__ __launch_bounds__(256, 2) void dkdv2_bf16_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, const uint8_t* __restrict__ key_valid,
+    const float* __restrict__ slopes, int S, int H, float c, float scale,
+    bf16* __restrict__ dqkv, float* __restrict__ dbias_part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Qs = reinterpret_cast<bf16*>(smem);                // [2][64*64] swizzled
+  bf16* Os = Qs + 2 * BQT * D;                              // [2][64*64] dO, swizzled
+  float* rc = reinterpret_cast<float*>(Os + 2 * BQT * D);   // [2][4][64] row constants:
+  // [0] (-LSE2 - slope2*q)/c  (query after the key), [1] (-LSE2 + slope2*q)/c  (before),
+  // [2] -LSE2/c  (diagonal blocks), [3] -delta
+
+  int kblk, h, b;
+  decode_block((S + BKW - 1) / BKW, H, kblk, h, b);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kl = lane & 31, hh = lane >> 5;
+  const int ld = 3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * ld;
+  const bf16* obase = dout + (size_t)b * S * (H * D);
+  const int kw0 = kblk * BKW + wave * 32;  // this wave's first key (uniform)
+  const int kj = kw0 + kl;
+  const int krow = min(kj, S - 1);
+  const float slope2 = slopes[h] * LOG2E;
+  const float invc = 1.f / c;
+  const float sl_t = slope2 * invc;
+  const float kbias = (key_valid && !key_valid[(size_t)b * S + krow]) ? PAD_BIAS * LOG2E : 0.f;
+  const float* lse_bh = lse + ((size_t)b * H + h) * S;
+  const float* dl_bh = delta + ((size_t)b * H + h) * S;
+
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)krow * ld + H * D + h * D + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)krow * ld + 2 * H * D + h * D + 16 * s + 8 * hh);
+  }
+
+  struct QRegs { bf16x8 q[2], o[2]; float l, d; };
+  auto load_tile = [&](int qt, QRegs& t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int cc = tid + i * 256, r = cc >> 3, ch = cc & 7;
+      const size_t row = (size_t)(qt * BQT + r);
+      t.q[i] = *reinterpret_cast<const bf16x8*>(base + row * ld + h * D + ch * 8);
+      t.o[i] = *reinterpret_cast<const bf16x8*>(obase + row * (H * D) + h * D + ch * 8);
+    }
+    if (tid < BQT) { t.l = lse_bh[qt * BQT + tid] * LOG2E; t.d = dl_bh[qt * BQT + tid]; }
+  };
+  auto store_tile = [&](int buf, int qt, const QRegs& t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int cc = tid + i * 256, r = cc >> 3, ch = cc & 7;
+      *reinterpret_cast<bf16x8*>(Qs + buf * BQT * D + swz(r, ch * 8)) = t.q[i];
+      *reinterpret_cast<bf16x8*>(Os + buf * BQT * D + swz(r, ch * 8)) = t.o[i];
+    }
+    if (tid < BQT) {
+      const float sq = slope2 * (float)(qt * BQT + tid);
+      float* R = rc + buf * 4 * BQT + tid;
+      R[0] = (-t.l - sq) * invc;
+      R[BQT] = (-t.l + sq) * invc;
+      R[2 * BQT] = -t.l * invc;
+      R[3 * BQT] = -t.d;
+    }
+  };
+
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dk[0][i] = dk[1][i] = dv[0][i] = dv[1][i] = 0.f; }
+
+  const int nt = S / BQT;
+  {
+    QRegs t;
+    load_tile(0, t);
+    store_tile(0, 0, t);
+  }
+  __syncthreads();
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const float kjf = (float)kj;
+
+  for (int qt = 0; qt < nt; ++qt) {
+    const int buf = qt & 1;
+    QRegs nx;
+    if (qt + 1 < nt) load_tile(qt + 1, nx);
+    const bf16* Q = Qs + buf * BQT * D;
+    const bf16* O = Os + buf * BQT * D;
+    const float* RC = rc + buf * 4 * BQT;
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int qb = qt * BQT + qh * 32;  // first query of this half (uniform)
+      const bool after = qb > kw0;        // every query after every key (32-aligned blocks)
+      const bool before = qb < kw0;
+      const int sel = after ? 0 : (before ? 1 : 2);
+      // register r = 4g + e  <->  query qb + 8g + 4hh + e
+      f32x16 sa, pa;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(RC + sel * BQT + qh * 32 + 8 * g4 + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 3 * BQT + qh * 32 + 8 * g4 + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { sa[4 * g4 + e] = l4[e]; pa[4 * g4 + e] = d4[e]; }
+      }
+      const int r0 = qh * 32 + kl;  // A-operand row = query
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 aq = *reinterpret_cast<const bf16x8*>(Q + swz(r0, 16 * s + 8 * hh));
+        const bf16x8 ao = *reinterpret_cast<const bf16x8*>(O + swz(r0, 16 * s + 8 * hh));
+        sa = mfma(aq, kf[s], sa);  // (S - LSE2 -+ slope2 q) / c   [q][key]
+        pa = mfma(ao, vf[s], pa);  // dP - delta
+      }
+      // both paths leave exponent = sa * c + U (U per lane), so the tail is one code path
+      float U = kbias;
+      if (after || before) {
+        U = fmaf(after ? slope2 : -slope2, kjf, kbias);
+      } else {
+        const float lq = (float)(qb + 4 * hh - kj);  // q - k at register offset 0
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sa[r] = fmaf(-sl_t, fabsf(lq + (float)aoff(r)), sa[r]);
+      }
+      bf16x8 pb[2], sb[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = ex2(fmaf(sa[r], c, U));
+        pb[r >> 3][r & 7] = (bf16)p;
+        sb[r >> 3][r & 7] = (bf16)(p * pa[r]);
+      }
+      // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int qrow = qh * 32 + 16 * s + 4 * (g16 >> 1) + (i16 >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+          const bf16x8 ao = cat(tr_read(O + swz(qrow, dcol)), tr_read(O + swz(qrow + 8, dcol)));
+          const bf16x8 aq = cat(tr_read(Q + swz(qrow, dcol)), tr_read(Q + swz(qrow + 8, dcol)));
+          dv[dt] = mfma(ao, pb[s], dv[dt]);
+          dk[dt] = mfma(aq, sb[s], dk[dt]);
+        }
+      }
+    }
+    if (qt + 1 < nt) store_tile(buf ^ 1, qt + 1, nx);
+    __syncthreads();
+  }
+  if (kj < S) {
+    bf16* row = dqkv + ((size_t)b * S + kj) * ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 vk, vv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vk[e] = (bf16)(dk[dt][4 * g + e] * scale);
+          vv[e] = (bf16)dv[dt][4 * g + e];
+        }
+        *reinterpret_cast<bf16x4*>(row + H * D + 32 * dt + 8 * g + 4 * hh) = vk;
+        *reinterpret_cast<bf16x4*>(row + 2 * H * D + 32 * dt + 8 * g + 4 * hh) = vv;
+      }
+  }
+  if (dbias_part) {
+    const int nk = (S + BKW - 1) / BKW;
+    float* prow = dbias_part + ((size_t)b * nk + kblk) * ld + h * D;
+    block_colsum64(reinterpret_cast<float*>(smem), dk, scale, kj < S, prow + H * D);
+    block_colsum64(reinterpret_cast<float*>(smem), dv, 1.f, kj < S, prow + 2 * H * D);
+  }
+}
+
+// dQ with queries on lanes: per 32-key half, S^T from the ALiBi vector of a separable block,
+// P = exp2(S c + U - LSE2), dS = P (dP - delta) with dP^T started from -delta,
+// dQ^T += K^T dS^T. Also writes delta for the dK/dV kernel and the fused bias-gradient column
+// partials (as dq_bf16_kernel).
+__global__ __launch_bounds__(256, 2) void dq2_bf16_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ out, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta,
+    const uint8_t* __restrict__ key_valid, const float* __restrict__ slopes, int S, int H,
+    float c, float scale, bf16* __restrict__ dqkv, float* __restrict__ dbias_part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Ks = reinterpret_cast<bf16*>(smem);     // [2][64*64] swizzled
+  bf16* Vs = Ks + 2 * BK * D;                    // [2][64*64] swizzled
+  float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);
+
+  int qblk, h, b;
+  decode_block((S + BQ - 1) / BQ, H, qblk, h, b);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ql = lane & 31, hh = lane >> 5;
+  const int ld = 3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * ld;
+  const int q0 = qblk * BQ + wave * 32;  // uniform
+  const int qi = q0 + ql;
+  const int qrow = min(qi, S - 1);
+  const float slope2 = slopes[h] * LOG2E;
+  const float invc = 1.f / c;
+  const float sl_t = slope2 * invc;
+  const float lse2 = lse[((size_t)b * H + h) * S + qrow] * LOG2E;
+
+  bf16x8 qf[4], df[4];
+  const size_t orow_off = ((size_t)b * S + qrow) * (H * D) + h * D;
+  float dl = 0.f;  // delta = rowsum(dO * O): this lane holds half the row, lane^32 the other
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)qrow * ld + h * D + 16 * s + 8 * hh);
+    df[s] = *reinterpret_cast<const bf16x8*>(dout + orow_off + 16 * s + 8 * hh);
+    const bf16x8 o8 = *reinterpret_cast<const bf16x8*>(out + orow_off + 16 * s + 8 * hh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl = fmaf((float)df[s][j], (float)o8[j], dl);
+  }
+  dl = pair_sum(dl);
+  if (hh == 0 && qi < S) delta[((size_t)b * H + h) * S + qi] = dl;
+  f32x16 negd;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negd[r] = -dl;
+
+  auto load_tile = [&](int kt, TileRegs& t, float& bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int cc = tid + i * 256, r = cc >> 3, ch = cc & 7;
+      const bf16* src = base + (size_t)(kt * BK + r) * ld + h * D + ch * 8;
+      t.k[i] = *reinterpret_cast<const bf16x8*>(src + H * D);
+      t.v[i] = *reinterpret_cast<const bf16x8*>(src + 2 * H * D);
+    }
+    bias = 0.f;
+    if (tid < BK && key_valid) bias = key_valid[(size_t)b * S + kt * BK + tid] ? 0.f : PAD_BIAS * LOG2E;
+  };
+  auto store_tile = [&](int buf, const TileRegs& t, float bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int cc = tid + i * 256, r = cc >> 3, ch = cc & 7;
+      *reinterpret_cast<bf16x8*>(Ks + buf * BK * D + swz(r, ch * 8)) = t.k[i];
+      *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + swz(r, ch * 8)) = t.v[i];
+    }
+    if (tid < BK) kb[buf * BK + tid] = bias;
+  };
+
+  f32x16 dq[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dq[0][i] = 0.f; dq[1][i] = 0.f; }
+
+  const int nt = S / BK;
+  {
+    TileRegs t; float bias;
+    load_tile(0, t, bias);
+    store_tile(0, t, bias);
+  }
+  __syncthreads();
+  const int g16 = lane >> 4, i16 = lane & 15;
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int buf = kt & 1;
+    TileRegs nx; float nbias = 0.f;
+    if (kt + 1 < nt) load_tile(kt + 1, nx, nbias);
+    const bf16* K = Ks + buf * BK * D;
+    const bf16* V = Vs + buf * BK * D;
+    const float* kbias = kb + buf * BK;
+    const bool haspad = key_valid && wave_any(kbias[lane] != 0.f);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int kb2 = kt * BK + 32 * kh;  // uniform
+      const bool generic = haspad || kb2 == q0;
+      const bool left = kb2 < q0;
+      const float dqk = (float)(kb2 + 4 * hh - qi);  // k - q at register offset 0
+      const int r0 = kh * 32 + ql;
+      f32x16 sa, pa;
+      {
+        bf16x8 ak[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ak[s] = *reinterpret_cast<const bf16x8*>(K + swz(r0, 16 * s + 8 * hh));
+        if (generic) {
+          f32x16 z;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) z[i] = 0.f;
+          sa = mfma(ak[0], qf[0], z);
+        } else if (left) {
+          f32x16 ini;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ini[r] = sl_t * (float)aoff(r);
+          sa = mfma(ak[0], qf[0], ini);
+        } else {
+          f32x16 ini;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ini[r] = -sl_t * (float)aoff(r);
+          sa = mfma(ak[0], qf[0], ini);
+        }
+#pragma unroll
+        for (int s = 1; s < 4; ++s) sa = mfma(ak[s], qf[s], sa);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(V + swz(r0, 16 * s + 8 * hh));
+        pa = mfma(av, df[s], s == 0 ? negd : pa);
+      }
+      // both paths leave exponent = sa * c + off (off per lane): one tail code path
+      float off = -lse2;
+      if (!generic) {
+        off += left ? slope2 * dqk : -slope2 * dqk;
+      } else {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + 32 * kh + 8 * g4 + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g4 + e;
+            sa[r] = fmaf(fmaf(-slope2, fabsf(dqk + (float)aoff(r)), pb[e]), invc, sa[r]);
+          }
+        }
+      }
+      bf16x8 db[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) db[r >> 3][r & 7] = (bf16)(ex2(fmaf(sa[r], c, off)) * pa[r]);
+      // dQ^T[d][q] += K^T[d][key] dS^T[key][q]   (k-steps over 16 keys)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int krow = kh * 32 + 16 * s + 4 * (g16 >> 1) + (i16 >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+          const bf16x8 a = cat(tr_read(K + swz(krow, dcol)), tr_read(K + swz(krow + 8, dcol)));
+          dq[dt] = mfma(a, db[s], dq[dt]);
+        }
+      }
+    }
+    if (kt + 1 < nt) store_tile(buf ^ 1, nx, nbias);
+    __syncthreads();
+  }
+  if (qi < S) {
+    bf16* row = dqkv + ((size_t)b * S + qi) * ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (bf16)(dq[dt][4 * g + e] * scale);
+        *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * hh) = v;
+      }
+  }
+  if (dbias_part) {
+    const int nq = (S + BQ - 1) / BQ;
+    block_colsum64(reinterpret_cast<float*>(smem), dq, scale, qi < S,
+                   dbias_part + ((size_t)b * nq + qblk) * ld + h * D);
+  }
+}
+
 // ----------------------------------------------------------------------------- fp32 path
 // One thread per query (forward, dQ) or per key (dK/dV); K/V (or Q/dO) tiles staged in LDS.
 constexpr int F32_TILE = 64;
@@ -816,6 +1422,7 @@ __global__ __launch_bounds__(64) void dkdv_f32_kernel(const float* __restrict__ 
 
 constexpr size_t FWD_LDS = 2 * (2 * BK * D * sizeof(bf16)) + 2 * BK * sizeof(float);
 constexpr size_t DKDV_LDS = 2 * (2 * BQT * D * sizeof(bf16)) + 4 * BQT * sizeof(float);
+constexpr size_t DKDV2_LDS = 2 * (2 * BQT * D * sizeof(bf16)) + 8 * BQT * sizeof(float);
 
 }  // namespace attn
 }  // namespace dna
@@ -848,9 +1455,17 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
   DNA_CHECK_ARG(out && lse, "dna_attn_fwd: null output");
   hipStream_t s = as_stream(stream);
   if (dtype == DNA_BF16) {
-    dim3 grid(((seqlen + BQ - 1) / BQ) * heads * batch);
-    hipLaunchKernelGGL(fwd_bf16_kernel, grid, dim3(256), FWD_LDS, s, (const bf16*)qkv, key_valid,
-                       slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+    // A/B switch for benchmarks: DNA_ATTN_FWD=1 runs the v1 forward
+    static const int forced = getenv("DNA_ATTN_FWD") ? atoi(getenv("DNA_ATTN_FWD")) : 0;
+    if (forced == 1) {
+      dim3 grid(((seqlen + BQ - 1) / BQ) * heads * batch);
+      hipLaunchKernelGGL(fwd_bf16_kernel, grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
+                         key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+    } else {
+      dim3 grid(((seqlen + BQ2 - 1) / BQ2) * heads * batch);
+      hipLaunchKernelGGL(fwd2_bf16_kernel, grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
+                         key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+    }
   } else {
     dim3 grid((seqlen + F32_TILE - 1) / F32_TILE, heads, batch);
     hipLaunchKernelGGL(fwd_f32_kernel, grid, dim3(64), 0, s, (const float*)qkv, key_valid, slopes,
@@ -871,8 +1486,18 @@ extern "C" int dna_attn_bwd_ex(const void* qkv, const void* out, const void* dou
   hipStream_t s = as_stream(stream);
   const int rows = batch * seqlen;
   const int nd = (rows * heads + 255) / 256;
-  if (dtype == DNA_BF16) {
+  static const bool bwd_v1 = getenv("DNA_ATTN_BWD") && atoi(getenv("DNA_ATTN_BWD")) == 1;
+  if (dtype == DNA_BF16 && !bwd_v1) {
     // dQ kernel also produces delta = rowsum(dO*O), consumed by the dK/dV kernel after it
+    hipLaunchKernelGGL(dq2_bf16_kernel, dim3(((seqlen + BQ - 1) / BQ) * heads * batch), dim3(256),
+                       FWD_LDS, s, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
+                       delta_ws, key_valid, slopes, seqlen, heads, softmax_scale * LOG2E,
+                       softmax_scale, (bf16*)dqkv, dbias_part);
+    hipLaunchKernelGGL(dkdv2_bf16_kernel, dim3(((seqlen + BKW - 1) / BKW) * heads * batch),
+                       dim3(256), DKDV2_LDS, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws,
+                       key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale,
+                       (bf16*)dqkv, dbias_part);
+  } else if (dtype == DNA_BF16) {  // v1 kernels (DNA_ATTN_BWD=1, benchmarks)
     hipLaunchKernelGGL(dq_bf16_kernel, dim3(((seqlen + BQ - 1) / BQ) * heads * batch), dim3(256),
                        FWD_LDS, s, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
                        delta_ws, key_valid, slopes, seqlen, heads, softmax_scale * LOG2E,
