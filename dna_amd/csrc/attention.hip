@@ -19,6 +19,7 @@
 // 1e-3 fp32 parity mode; not a throughput path.
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -568,6 +569,42 @@ __global__ void delta_kernel(const T* __restrict__ out, const T* __restrict__ do
 // times `mul`; rows with !valid count as zero. `red` is >= 32 KiB of free LDS (16-B chunks
 // XOR-swizzled by row). Writes 64 floats to out. Fuses the packed-QKV projection's bias gradient
 // (column sums of dqkv) into the attention backward: one partial row per 128-row block.
+// Generalisation to NW waves (NW/4 groups of 4 waves = 128 rows): group g writes its 64 sums to
+// out + g * row_stride, so the partial-row layout stays one row per 128 rows whatever the block.
+// `red` needs NW * 32 * 64 floats.
+template <int NW>
+__device__ void block_colsum64_nw(float* red, const f32x16 (&acc)[2], float mul, bool valid,
+                                  float* __restrict__ out, size_t row_stride) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, ql = lane & 31, hh = lane >> 5;
+  const int r = wave * 32 + ql;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = valid ? acc[dt][4 * g + e] * mul : 0.f;
+      const int chunk = 8 * dt + 2 * g + hh;  // 16-B chunk of the 64-column row
+      *reinterpret_cast<f32x4*>(red + r * 64 + ((chunk ^ (r & 15)) << 2)) = v;
+    }
+  __syncthreads();
+  const int c = tid & 63, qr = tid >> 6;
+  float s = 0.f;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    const int rr = qr * 32 + i;
+    s += red[rr * 64 + ((((c >> 2) ^ (rr & 15)) << 2) | (c & 3))];
+  }
+  __syncthreads();
+  red[qr * 64 + c] = s;
+  __syncthreads();
+  if ((tid & 255) < 64) {
+    const float* rg = red + (tid >> 8) * 256;
+    out[(tid >> 8) * row_stride + c] = (rg[c] + rg[64 + c]) + (rg[128 + c] + rg[192 + c]);
+  }
+  __syncthreads();
+}
+
 __device__ void block_colsum64(float* red, const f32x16 (&acc)[2], float mul, bool valid,
                                float* __restrict__ out) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, ql = lane & 31, hh = lane >> 5;
@@ -931,7 +968,8 @@ __global__ __launch_bounds__(256) void dkdv_bf16_kernel(
 //    separable block, dP^T from -delta;
 //  * blocks are classified per 32x32 (before / after / diagonal) with scalar branches; only
 //    diagonal blocks (and, in the dQ kernel, key tiles with pad keys) compute |q - k| per score.
-__global__ __launch_bounds__(256, 2) void dkdv2_bf16_kernel(
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void dkdv2_bf16_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, const uint8_t* __restrict__ key_valid,
     const float* __restrict__ slopes, int S, int H, float c, float scale,
@@ -943,15 +981,17 @@ __global__ __launch_bounds__(256, 2) void dkdv2_bf16_kernel(
   // [0] (-LSE2 - slope2*q)/c  (query after the key), [1] (-LSE2 + slope2*q)/c  (before),
   // [2] -LSE2/c  (diagonal blocks), [3] -delta
 
+  constexpr int NTHR = NW * 64, KPB = NW * 32;  // threads, keys per workgroup
+  constexpr int NSTG = 512 / NTHR;               // 16-B staging chunks per thread per tensor
   int kblk, h, b;
-  decode_block((S + BKW - 1) / BKW, H, kblk, h, b);
+  decode_block((S + KPB - 1) / KPB, H, kblk, h, b);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kl = lane & 31, hh = lane >> 5;
   const int ld = 3 * H * D;
   const bf16* base = qkv + (size_t)b * S * ld;
   const bf16* obase = dout + (size_t)b * S * (H * D);
-  const int kw0 = kblk * BKW + wave * 32;  // this wave's first key (uniform)
+  const int kw0 = kblk * KPB + wave * 32;  // this wave's first key (uniform)
   const int kj = kw0 + kl;
   const int krow = min(kj, S - 1);
   const float slope2 = slopes[h] * LOG2E;
@@ -968,11 +1008,11 @@ __global__ __launch_bounds__(256, 2) void dkdv2_bf16_kernel(
     vf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)krow * ld + 2 * H * D + h * D + 16 * s + 8 * hh);
   }
 
-  struct QRegs { bf16x8 q[2], o[2]; float l, d; };
+  struct QRegs { bf16x8 q[NSTG], o[NSTG]; float l, d; };
   auto load_tile = [&](int qt, QRegs& t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int cc = tid + i * 256, r = cc >> 3, ch = cc & 7;
+    for (int i = 0; i < NSTG; ++i) {
+      int cc = tid + i * NTHR, r = cc >> 3, ch = cc & 7;
       const size_t row = (size_t)(qt * BQT + r);
       t.q[i] = *reinterpret_cast<const bf16x8*>(base + row * ld + h * D + ch * 8);
       t.o[i] = *reinterpret_cast<const bf16x8*>(obase + row * (H * D) + h * D + ch * 8);
@@ -981,8 +1021,8 @@ __global__ __launch_bounds__(256, 2) void dkdv2_bf16_kernel(
   };
   auto store_tile = [&](int buf, int qt, const QRegs& t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int cc = tid + i * 256, r = cc >> 3, ch = cc & 7;
+    for (int i = 0; i < NSTG; ++i) {
+      int cc = tid + i * NTHR, r = cc >> 3, ch = cc & 7;
       *reinterpret_cast<bf16x8*>(Qs + buf * BQT * D + swz(r, ch * 8)) = t.q[i];
       *reinterpret_cast<bf16x8*>(Os + buf * BQT * D + swz(r, ch * 8)) = t.o[i];
     }
@@ -1017,46 +1057,52 @@ __global__ __launch_bounds__(256, 2) void dkdv2_bf16_kernel(
     const bf16* Q = Qs + buf * BQT * D;
     const bf16* O = Os + buf * BQT * D;
     const float* RC = rc + buf * 4 * BQT;
+    // stage 1: S and dP for both 32-query halves (16 MFMAs) before any per-half VALU tail, so
+    // the second half's MFMAs run under the first half's exp work
+    f32x16 sa[2], pa[2];
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
       const int qb = qt * BQT + qh * 32;  // first query of this half (uniform)
-      const bool after = qb > kw0;        // every query after every key (32-aligned blocks)
-      const bool before = qb < kw0;
-      const int sel = after ? 0 : (before ? 1 : 2);
+      const int sel = qb > kw0 ? 0 : (qb < kw0 ? 1 : 2);
       // register r = 4g + e  <->  query qb + 8g + 4hh + e
-      f32x16 sa, pa;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const f32x4 l4 = *reinterpret_cast<const f32x4*>(RC + sel * BQT + qh * 32 + 8 * g4 + 4 * hh);
         const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 3 * BQT + qh * 32 + 8 * g4 + 4 * hh);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { sa[4 * g4 + e] = l4[e]; pa[4 * g4 + e] = d4[e]; }
+        for (int e = 0; e < 4; ++e) { sa[qh][4 * g4 + e] = l4[e]; pa[qh][4 * g4 + e] = d4[e]; }
       }
       const int r0 = qh * 32 + kl;  // A-operand row = query
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const bf16x8 aq = *reinterpret_cast<const bf16x8*>(Q + swz(r0, 16 * s + 8 * hh));
         const bf16x8 ao = *reinterpret_cast<const bf16x8*>(O + swz(r0, 16 * s + 8 * hh));
-        sa = mfma(aq, kf[s], sa);  // (S - LSE2 -+ slope2 q) / c   [q][key]
-        pa = mfma(ao, vf[s], pa);  // dP - delta
+        sa[qh] = mfma(aq, kf[s], sa[qh]);  // (S - LSE2 -+ slope2 q) / c   [q][key]
+        pa[qh] = mfma(ao, vf[s], pa[qh]);  // dP - delta
       }
-      // both paths leave exponent = sa * c + U (U per lane), so the tail is one code path
+    }
+    // stage 2 per half: P, dS (one tail for every block class), then dV^T += dO^T P,
+    // dK^T += Q^T dS
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int qb = qt * BQT + qh * 32;
+      const bool after = qb > kw0;  // every query after every key (32-aligned blocks)
+      const bool before = qb < kw0;
       float U = kbias;
       if (after || before) {
         U = fmaf(after ? slope2 : -slope2, kjf, kbias);
       } else {
         const float lq = (float)(qb + 4 * hh - kj);  // q - k at register offset 0
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sa[r] = fmaf(-sl_t, fabsf(lq + (float)aoff(r)), sa[r]);
+        for (int r = 0; r < 16; ++r) sa[qh][r] = fmaf(-sl_t, fabsf(lq + (float)aoff(r)), sa[qh][r]);
       }
       bf16x8 pb[2], sb[2];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = ex2(fmaf(sa[r], c, U));
+        const float p = ex2(fmaf(sa[qh][r], c, U));
         pb[r >> 3][r & 7] = (bf16)p;
-        sb[r >> 3][r & 7] = (bf16)(p * pa[r]);
+        sb[r >> 3][r & 7] = (bf16)(p * pa[qh][r]);
       }
-      // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int qrow = qh * 32 + 16 * s + 4 * (g16 >> 1) + (i16 >> 2);
@@ -1089,11 +1135,11 @@ __global__ __launch_bounds__(256, 2) void dkdv2_bf16_kernel(
         *reinterpret_cast<bf16x4*>(row + 2 * H * D + 32 * dt + 8 * g + 4 * hh) = vv;
       }
   }
-  if (dbias_part) {
+  if (dbias_part) {  // partial rows are per 128 keys (dna_attn_dbias_part_rows)
     const int nk = (S + BKW - 1) / BKW;
-    float* prow = dbias_part + ((size_t)b * nk + kblk) * ld + h * D;
-    block_colsum64(reinterpret_cast<float*>(smem), dk, scale, kj < S, prow + H * D);
-    block_colsum64(reinterpret_cast<float*>(smem), dv, 1.f, kj < S, prow + 2 * H * D);
+    float* prow = dbias_part + ((size_t)b * nk + kblk * (NW / 4)) * ld + h * D;
+    block_colsum64_nw<NW>(reinterpret_cast<float*>(smem), dk, scale, kj < S, prow + H * D, ld);
+    block_colsum64_nw<NW>(reinterpret_cast<float*>(smem), dv, 1.f, kj < S, prow + 2 * H * D, ld);
   }
 }
 
@@ -1101,7 +1147,8 @@ __global__ __launch_bounds__(256, 2) void dkdv2_bf16_kernel(
 // P = exp2(S c + U - LSE2), dS = P (dP - delta) with dP^T started from -delta,
 // dQ^T += K^T dS^T. Also writes delta for the dK/dV kernel and the fused bias-gradient column
 // partials (as dq_bf16_kernel).
-__global__ __launch_bounds__(256, 2) void dq2_bf16_kernel(
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void dq2_bf16_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ out, const bf16* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta,
     const uint8_t* __restrict__ key_valid, const float* __restrict__ slopes, int S, int H,
@@ -1111,14 +1158,16 @@ __global__ __launch_bounds__(256, 2) void dq2_bf16_kernel(
   bf16* Vs = Ks + 2 * BK * D;                    // [2][64*64] swizzled
   float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);
 
+  constexpr int NTHR = NW * 64, QPB = NW * 32;  // threads, queries per workgroup
+  constexpr int NSTG = 512 / NTHR;
   int qblk, h, b;
-  decode_block((S + BQ - 1) / BQ, H, qblk, h, b);
+  decode_block((S + QPB - 1) / QPB, H, qblk, h, b);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ql = lane & 31, hh = lane >> 5;
   const int ld = 3 * H * D;
   const bf16* base = qkv + (size_t)b * S * ld;
-  const int q0 = qblk * BQ + wave * 32;  // uniform
+  const int q0 = qblk * QPB + wave * 32;  // uniform
   const int qi = q0 + ql;
   const int qrow = min(qi, S - 1);
   const float slope2 = slopes[h] * LOG2E;
@@ -1143,10 +1192,11 @@ __global__ __launch_bounds__(256, 2) void dq2_bf16_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) negd[r] = -dl;
 
-  auto load_tile = [&](int kt, TileRegs& t, float& bias) {
+  struct KVRegs { bf16x8 k[NSTG], v[NSTG]; };
+  auto load_tile = [&](int kt, KVRegs& t, float& bias) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int cc = tid + i * 256, r = cc >> 3, ch = cc & 7;
+    for (int i = 0; i < NSTG; ++i) {
+      int cc = tid + i * NTHR, r = cc >> 3, ch = cc & 7;
       const bf16* src = base + (size_t)(kt * BK + r) * ld + h * D + ch * 8;
       t.k[i] = *reinterpret_cast<const bf16x8*>(src + H * D);
       t.v[i] = *reinterpret_cast<const bf16x8*>(src + 2 * H * D);
@@ -1154,10 +1204,10 @@ __global__ __launch_bounds__(256, 2) void dq2_bf16_kernel(
     bias = 0.f;
     if (tid < BK && key_valid) bias = key_valid[(size_t)b * S + kt * BK + tid] ? 0.f : PAD_BIAS * LOG2E;
   };
-  auto store_tile = [&](int buf, const TileRegs& t, float bias) {
+  auto store_tile = [&](int buf, const KVRegs& t, float bias) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int cc = tid + i * 256, r = cc >> 3, ch = cc & 7;
+    for (int i = 0; i < NSTG; ++i) {
+      int cc = tid + i * NTHR, r = cc >> 3, ch = cc & 7;
       *reinterpret_cast<bf16x8*>(Ks + buf * BK * D + swz(r, ch * 8)) = t.k[i];
       *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + swz(r, ch * 8)) = t.v[i];
     }
@@ -1170,7 +1220,7 @@ __global__ __launch_bounds__(256, 2) void dq2_bf16_kernel(
 
   const int nt = S / BK;
   {
-    TileRegs t; float bias;
+    KVRegs t; float bias;
     load_tile(0, t, bias);
     store_tile(0, t, bias);
   }
@@ -1179,7 +1229,7 @@ __global__ __launch_bounds__(256, 2) void dq2_bf16_kernel(
 
   for (int kt = 0; kt < nt; ++kt) {
     const int buf = kt & 1;
-    TileRegs nx; float nbias = 0.f;
+    KVRegs nx; float nbias = 0.f;
     if (kt + 1 < nt) load_tile(kt + 1, nx, nbias);
     const bf16* K = Ks + buf * BK * D;
     const bf16* V = Vs + buf * BK * D;
@@ -1266,10 +1316,10 @@ __global__ __launch_bounds__(256, 2) void dq2_bf16_kernel(
         *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * hh) = v;
       }
   }
-  if (dbias_part) {
+  if (dbias_part) {  // partial rows are per 128 queries (dna_attn_dbias_part_rows)
     const int nq = (S + BQ - 1) / BQ;
-    block_colsum64(reinterpret_cast<float*>(smem), dq, scale, qi < S,
-                   dbias_part + ((size_t)b * nq + qblk) * ld + h * D);
+    block_colsum64_nw<NW>(reinterpret_cast<float*>(smem), dq, scale, qi < S,
+                          dbias_part + ((size_t)b * nq + qblk * (NW / 4)) * ld + h * D, ld);
   }
 }
 
@@ -1488,15 +1538,33 @@ extern "C" int dna_attn_bwd_ex(const void* qkv, const void* out, const void* dou
   const int nd = (rows * heads + 255) / 256;
   static const bool bwd_v1 = getenv("DNA_ATTN_BWD") && atoi(getenv("DNA_ATTN_BWD")) == 1;
   if (dtype == DNA_BF16 && !bwd_v1) {
-    // dQ kernel also produces delta = rowsum(dO*O), consumed by the dK/dV kernel after it
-    hipLaunchKernelGGL(dq2_bf16_kernel, dim3(((seqlen + BQ - 1) / BQ) * heads * batch), dim3(256),
-                       FWD_LDS, s, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
-                       delta_ws, key_valid, slopes, seqlen, heads, softmax_scale * LOG2E,
-                       softmax_scale, (bf16*)dqkv, dbias_part);
-    hipLaunchKernelGGL(dkdv2_bf16_kernel, dim3(((seqlen + BKW - 1) / BKW) * heads * batch),
-                       dim3(256), DKDV2_LDS, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws,
-                       key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale,
-                       (bf16*)dqkv, dbias_part);
+    // dQ kernel also produces delta = rowsum(dO*O), consumed by the dK/dV kernel after it.
+    // 8-wave workgroups (256 queries / keys each) when the sequence fills them: half the
+    // K/V and Q/dO re-streaming of 4-wave ones. Colsum scratch: NW*32 rows x 64 floats.
+    static const int nw_env = getenv("DNA_ATTN_BWD_NW") ? atoi(getenv("DNA_ATTN_BWD_NW")) : 8;
+    const bool w8 = nw_env == 8 && seqlen % 256 == 0;
+    const size_t red = (w8 ? 8 : 4) * 32 * 64 * sizeof(float);
+    const size_t dq_lds = std::max(FWD_LDS, dbias_part ? red : (size_t)0);
+    const size_t kv_lds = std::max(DKDV2_LDS, dbias_part ? red : (size_t)0);
+    if (w8) {
+      hipLaunchKernelGGL((dq2_bf16_kernel<8>), dim3((seqlen / 256) * heads * batch), dim3(512),
+                         dq_lds, s, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
+                         delta_ws, key_valid, slopes, seqlen, heads, softmax_scale * LOG2E,
+                         softmax_scale, (bf16*)dqkv, dbias_part);
+      hipLaunchKernelGGL((dkdv2_bf16_kernel<8>), dim3((seqlen / 256) * heads * batch), dim3(512),
+                         kv_lds, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws, key_valid,
+                         slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv,
+                         dbias_part);
+    } else {
+      hipLaunchKernelGGL((dq2_bf16_kernel<4>), dim3(((seqlen + BQ - 1) / BQ) * heads * batch),
+                         dim3(256), dq_lds, s, (const bf16*)qkv, (const bf16*)out,
+                         (const bf16*)dout, lse, delta_ws, key_valid, slopes, seqlen, heads,
+                         softmax_scale * LOG2E, softmax_scale, (bf16*)dqkv, dbias_part);
+      hipLaunchKernelGGL((dkdv2_bf16_kernel<4>), dim3(((seqlen + BKW - 1) / BKW) * heads * batch),
+                         dim3(256), kv_lds, s, (const bf16*)qkv, (const bf16*)dout, lse, delta_ws,
+                         key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, softmax_scale,
+                         (bf16*)dqkv, dbias_part);
+    }
   } else if (dtype == DNA_BF16) {  // v1 kernels (DNA_ATTN_BWD=1, benchmarks)
     hipLaunchKernelGGL(dq_bf16_kernel, dim3(((seqlen + BQ - 1) / BQ) * heads * batch), dim3(256),
                        FWD_LDS, s, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--H", type=int, default=12)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--which", default="fwd,bwd")
+    ap.add_argument("--dbias", type=int, default=1, help="backward with the fused bias partials")
     a = ap.parse_args()
     b, S, H, D = a.b, a.S, a.H, 64
     T = b * S
@@ -39,10 +40,13 @@ def main():
         N.call("dna_attn_fwd", qkv.data_ptr(), kv.data_ptr(), slopes.data_ptr(), b, S, H, D, 1, sc,
                out.data_ptr(), lse.data_ptr(), st)
 
+    # the training step runs the backward with the fused Wqkv bias-gradient partials
+    part = torch.empty(N.lib().dna_attn_dbias_part_rows(b, S), 3 * H * D, device="cuda")
+
     def bwd():
-        N.call("dna_attn_bwd", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+        N.call("dna_attn_bwd_ex", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
                kv.data_ptr(), slopes.data_ptr(), b, S, H, D, 1, sc, dqkv.data_ptr(),
-               delta.data_ptr(), st)
+               delta.data_ptr(), part.data_ptr() if a.dbias else None, st)
 
     fwd()
     for name, fn, fl in (("fwd", fwd, 4.0), ("bwd", bwd, 10.0)):
