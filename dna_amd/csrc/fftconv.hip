@@ -27,6 +27,9 @@
 // All arithmetic fp32; inputs/outputs fp32 or bf16 (u, y, dy, du), filters and grads fp32.
 #include <math.h>
 
+#include <mutex>
+#include <vector>
+
 #include "common.h"
 
 namespace dna {
@@ -41,12 +44,15 @@ __device__ __forceinline__ cf cmul(cf a, cf b) {
 }
 __device__ __forceinline__ cf cconj(cf a) { return make_float2(a.x, -a.y); }
 
-// exp(-2 pi i m / N) for integer m in [0, N): the sincospi argument 2m/N is exact in fp32.
-__device__ __forceinline__ cf twiddle(uint32_t m, int logN) {
-  float s, c;
-  sincospif(-2.0f * (float)m / (float)(1u << logN), &s, &c);
-  return make_float2(c, s);
-}
+// W_{2^18}^j = exp(-2 pi i j / 2^18), j < 2^18: computed on the host in double precision and
+// rounded once (ensure_twiddles, first use per device). Every table a block builds (W_M, the
+// two-level W_N, the bias-tap phases) is a strided read of it (L2/MALL-resident, 2 MB) instead
+// of an OCML sincospif per entry (~40 VALU each, ~1000 per block).
+constexpr int LOG_TW = 18;
+__device__ cf g_w18[1 << LOG_TW];
+
+// exp(-2 pi i m / N) for integer m in [0, N), N = 2^logN <= 2^18.
+__device__ __forceinline__ cf twiddle(uint32_t m, int logN) { return g_w18[m << (LOG_TW - logN)]; }
 
 // ------------------------------------------------------------------ register butterflies
 // multiply by W_4^1 = -i (forward) / +i (inverse)
@@ -566,6 +572,29 @@ inline int pad_before(int L, int bidirectional) {
 using namespace dna;
 using namespace dna::fftc;
 
+// Upload g_w18 once per device (immutable afterwards). Synchronous: nothing can be using the
+// table before its first upload on that device.
+static int ensure_twiddles() {
+  static std::mutex mu;
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("fftconv: hipGetDevice failed");
+    return DNA_ERR_HIP;
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  if (done[dev]) return DNA_OK;
+  std::vector<cf> h((size_t)1 << LOG_TW);
+  const double step = -2.0 * M_PI / (double)((size_t)1 << LOG_TW);
+  for (size_t j = 0; j < h.size(); ++j) h[j] = make_float2((float)cos(step * (double)j), (float)sin(step * (double)j));
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_w18), h.data(), h.size() * sizeof(cf)) != hipSuccess) {
+    set_error("fftconv: twiddle table upload failed");
+    return DNA_ERR_HIP;
+  }
+  done[dev] = true;
+  return DNA_OK;
+}
+
 extern "C" size_t dna_fftconv_workspace(int B, int D, int L) {
   Geo g;
   if (B <= 0 || D <= 0 || !geometry(L, g)) return 0;
@@ -589,6 +618,7 @@ extern "C" int dna_fftconv_filter(const float* k, const float* bias, int D, int 
   const size_t N = (size_t)1 << g.logN;
   const int Q = (D + 1) / 2;
   DNA_CHECK_ARG(ws_bytes >= (size_t)Q * N * sizeof(cf), "dna_fftconv_filter: workspace too small");
+  if (int st = ensure_twiddles()) return st;
   hipStream_t s = as_stream(stream);
   Pairing pr{D, 1, Q};  // channels paired (2q, 2q+1)
   cf* w = (cf*)ws;
@@ -610,6 +640,7 @@ extern "C" int dna_fftconv_fwd(const void* u, int dtype, const void* kspec, int 
   const size_t N = (size_t)1 << g.logN;
   const int BP = (B + 1) / 2, P = BP * D;
   DNA_CHECK_ARG(ws_bytes >= (size_t)P * N * sizeof(cf), "dna_fftconv_fwd: workspace too small");
+  if (int st = ensure_twiddles()) return st;
   hipStream_t s = as_stream(stream);
   Pairing pr{B, D, BP};
   cf* w = (cf*)ws;
@@ -678,6 +709,7 @@ extern "C" int dna_fftconv_bwd(const void* dy, const void* u, int dtype, const v
   const size_t P = (size_t)((B + 1) / 2) * D;
   DNA_CHECK_ARG(ws_bytes >= (2 * P + (size_t)D) * N * sizeof(cf) + (size_t)D * DB_CHUNKS * sizeof(float),
                 "dna_fftconv_bwd: workspace too small");
+  if (int st = ensure_twiddles()) return st;
   const int pb = pad_before(L, bidirectional);
   hipStream_t s = as_stream(stream);
   if (dtype == DNA_BF16)
