@@ -61,6 +61,10 @@ class GradBucketReducer:
     def _launch(self, bi):
         s, e, _ = self.buckets[bi]
         self._fired[bi] = True
+        # weight gradients may still be in flight on the side stream (functional.Linear)
+        from .functional import join_side_stream
+        if self.flat.grad.is_cuda:
+            join_side_stream()
         self._works.append(dist.all_reduce(self.flat.grad[s:e], op=dist.ReduceOp.SUM,
                                            group=self.group, async_op=True))
 
