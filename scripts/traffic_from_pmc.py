@@ -18,8 +18,10 @@ import sys
 # family -> (regex selecting its kernels, regex selecting the one kernel counted per op launch)
 FAMILIES = {
     "gemm": (r"Cijk_|sum_slices_kernel", r"Cijk_"),
-    "attn_fwd": (r"attn::fwd_bf16_kernel|attn4fwd_bf16", r"attn::fwd_bf16_kernel|attn4fwd_bf16"),
-    "attn_bwd": (r"attn::(dq|dkdv)_bf16_kernel|attn(2dq|4dkdv)_bf16", r"attn::dq_bf16_kernel|attn2dq_bf16"),
+    "attn_fwd": (r"attn::fwd2?_bf16_kernel|attn4fwd_bf16|attn16fwd2_bf16",
+                 r"attn::fwd2?_bf16_kernel|attn4fwd_bf16|attn16fwd2_bf16"),
+    "attn_bwd": (r"attn::(dq|dkdv)2?_bf16_kernel|attn(2dq|4dkdv)_bf16|dq2_bf16|dkdv2_bf16",
+                 r"attn::dq2?_bf16_kernel|attn2dq_bf16|dq2_bf16"),
     "geglu_fwd": (r"geglu10fwd_kernel|geglu::fwd_kernel", r"geglu10fwd_kernel|geglu::fwd_kernel"),
     "geglu_bwd": (r"geglu10bwd_kernel|geglu::bwd_kernel", r"geglu10bwd_kernel|geglu::bwd_kernel"),
     "ln_fwd": (r"2ln10fwd_kernel|ln::fwd_kernel", r"2ln10fwd_kernel|ln::fwd_kernel"),
