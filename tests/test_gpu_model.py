@@ -167,3 +167,26 @@ def test_direct_grad_accumulation_matches_autograd():
         grads.append(flat.grad.clone())
     scale = grads[0].abs().max().item()
     assert (grads[0] - grads[1]).abs().max().item() < 1e-3 * scale
+
+
+def test_wgrad_side_stream_same_gradients(monkeypatch):
+    """DNA_WGRAD_STREAM=1 (weight gradients on a side stream, joined at the end of backward) gives
+    bit-identical flat gradients to the single-stream path (same kernels, same split-K order)."""
+    from dna_amd.bert_layers import BertForMaskedLM, MLMIndex
+    from dna_amd.flat import FlatParams
+    z, cfg = _golden("cfgA")
+    ids, mask, labels = _batch(z)
+    idx = MLMIndex.build(ids, labels)
+    grads = []
+    for side in ("0", "1"):
+        monkeypatch.setenv("DNA_WGRAD_STREAM", side)
+        torch.manual_seed(0)
+        m = BertForMaskedLM(cfg, precision="bf16").to(DEV).eval()
+        flat = FlatParams(m, DEV)
+        flat.enable_direct_grad(True)
+        for _ in range(2):  # two backwards: the join must also hold across steps
+            flat.zero_grad()
+            loss, _ = m.mlm_loss(ids, mask, idx)
+            loss.backward()
+        grads.append(flat.grad.clone())  # read right after backward(): no explicit sync
+    assert torch.equal(grads[0], grads[1])
