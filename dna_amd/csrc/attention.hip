@@ -335,7 +335,8 @@ __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballo
 // key offset (within a 32-key half, lane half hh excluded) of accumulator register r
 __device__ __forceinline__ constexpr int aoff(int r) { return (r & 3) + 8 * (r >> 2); }
 
-__global__ __launch_bounds__(256, 2) void fwd2_bf16_kernel(const bf16* __restrict__ qkv,
+template <int NQB>
+__global__ __launch_bounds__(256, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_bf16_kernel(const bf16* __restrict__ qkv,
                                                            const uint8_t* __restrict__ key_valid,
                                                            const float* __restrict__ slopes,
                                                            int S, int H, float c,
@@ -347,20 +348,21 @@ __global__ __launch_bounds__(256, 2) void fwd2_bf16_kernel(const bf16* __restric
   float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);  // [2][64] pad bias (log2 units)
 
   int qblk, h, b;
-  decode_block((S + BQ2 - 1) / BQ2, H, qblk, h, b);
+  constexpr int QPB = 4 * 32 * NQB;  // queries per workgroup
+  decode_block((S + QPB - 1) / QPB, H, qblk, h, b);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches stay uniform
   const int ql = lane & 31, hh = lane >> 5;
   const int ld = 3 * H * D;
   const bf16* base = qkv + (size_t)b * S * ld;
-  const int q0 = qblk * BQ2 + wave * 64;
+  const int q0 = qblk * QPB + wave * 32 * NQB;
   const float slope2 = slopes[h] * LOG2E;
   const float sl_t = slope2 / c;  // ALiBi slope in raw-score units
   const float invc = 1.f / c;
 
-  bf16x8 qf[2][4];
+  bf16x8 qf[NQB][4];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NQB; ++j) {
     const int qrow = min(q0 + 32 * j + ql, S - 1);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -413,15 +415,17 @@ __global__ __launch_bounds__(256, 2) void fwd2_bf16_kernel(const bf16* __restric
     if (tid < BK) kb[buf * BK + tid] = bias;
   };
 
-  f32x16 o[2][2];
+  f32x16 o[NQB][2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < NQB; ++j)
 #pragma unroll
     for (int i = 0; i < 16; ++i) { o[j][0][i] = 0.f; o[j][1][i] = 0.f; }
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  float m[NQB], l[NQB];
+#pragma unroll
+  for (int j = 0; j < NQB; ++j) { m[j] = -INFINITY; l[j] = 0.f; }
 
   const int nt = S / BK;
-  const int kt0 = (qblk * (BQ2 / BK) + 1) % nt;  // near-diagonal tiles first
+  const int kt0 = (qblk * (QPB / BK) + (NQB == 1 ? 0 : 1)) % nt;  // near-diagonal tiles first
   {
     TileRegs t; float bias;
     load_tile(kt0, t, bias);
@@ -448,9 +452,9 @@ __global__ __launch_bounds__(256, 2) void fwd2_bf16_kernel(const bf16* __restric
 #pragma unroll
       for (int s = 0; s < 4; ++s)
         kf[s] = *reinterpret_cast<const bf16x8*>(K + kh * 32 * D + kro[s]);
-      bf16x8 pbf[2][2];
+      bf16x8 pbf[NQB][2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NQB; ++j) {
         const int qf0 = q0 + 32 * j;  // wave-uniform
         const int qi = qf0 + ql;
         const bool generic = haspad || kb2 == qf0;
@@ -517,8 +521,8 @@ __global__ __launch_bounds__(256, 2) void fwd2_bf16_kernel(const bf16* __restric
         for (int dt = 0; dt < 2; ++dt) {
           const bf16* vb = V + (kh * 32 + 16 * s) * D;
           const bf16x8 a = cat(tr_read(vb + vro[dt][0]), tr_read(vb + vro[dt][1]));
-          o[0][dt] = mfma(a, pbf[0][s], o[0][dt]);
-          o[1][dt] = mfma(a, pbf[1][s], o[1][dt]);
+#pragma unroll
+          for (int j = 0; j < NQB; ++j) o[j][dt] = mfma(a, pbf[j][s], o[j][dt]);
         }
     }
     if (it + 1 < nt) store_tile(buf ^ 1, nx, nbias);
@@ -526,7 +530,7 @@ __global__ __launch_bounds__(256, 2) void fwd2_bf16_kernel(const bf16* __restric
   }
 
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NQB; ++j) {
     const int qi = q0 + 32 * j + ql;
     const float ltot = pair_sum(l[j]);
     const float inv = 1.f / ltot;
@@ -1512,9 +1516,19 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
       hipLaunchKernelGGL(fwd_bf16_kernel, grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
                          key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
     } else {
-      dim3 grid(((seqlen + BQ2 - 1) / BQ2) * heads * batch);
-      hipLaunchKernelGGL(fwd2_bf16_kernel, grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
-                         key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+      if (forced == 4) {  // four 32-query blocks per wave, 1 wave per SIMD (A/B)
+        dim3 grid(((seqlen + 511) / 512) * heads * batch);
+        hipLaunchKernelGGL((fwd2_bf16_kernel<4>), grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
+                           key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+      } else if (forced == 3) {  // one 32-query block per wave, 3 waves per SIMD (A/B)
+        dim3 grid(((seqlen + 127) / 128) * heads * batch);
+        hipLaunchKernelGGL((fwd2_bf16_kernel<1>), grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
+                           key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+      } else {
+        dim3 grid(((seqlen + BQ2 - 1) / BQ2) * heads * batch);
+        hipLaunchKernelGGL((fwd2_bf16_kernel<2>), grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
+                           key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+      }
     }
   } else {
     dim3 grid((seqlen + F32_TILE - 1) / F32_TILE, heads, batch);
