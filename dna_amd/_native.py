@@ -48,7 +48,8 @@ _SIGS = {
                               _u64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dna_embed_ln_bwd_rows": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _f, _u64,
                                    _u64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
-    "dna_embed_grad_segsum": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "dna_embed_grad_segsum_workspace": (_sz, [_i, _i]),
+    "dna_embed_grad_segsum": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "dna_sum_slices_accum": (_i, [_vp, _i, _sz, _vp, _vp]),
     "dna_geglu_fwd": (_i, [_vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_geglu_bwd": (_i, [_vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),

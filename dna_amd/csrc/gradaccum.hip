@@ -4,8 +4,8 @@
 //    [s, M, N] batched GEMM folded into the parameter's gradient in one pass (no separate reduce
 //    + AccumulateGrad add; replaces autograd's accumulation for Linear weights).
 //  * dna_embed_grad_segsum: d(word_embeddings) from per-token row gradients, by token id:
-//    rows visited in id-sorted order, summed in registers per run of equal ids, one atomic row
-//    flush per run per 32-row chunk -- frequent BPE tokens (thousands of rows per id in a
+//    rows visited in id-sorted order, summed in registers per run of equal ids per 32-row chunk,
+//    runs crossing chunks joined in chunk order (deterministic, no atomics) -- frequent BPE tokens (thousands of rows per id in a
 //    65,536-token batch) no longer serialise on one row (nn.Embedding backward with
 //    padding_idx=0, bert_layers.py:45-47).
 #include "common.h"
@@ -61,31 +61,51 @@ __global__ __launch_bounds__(64 * CS_GROUPS) void colsum_kernel(const float* __r
 
 constexpr int SEG_CHUNK = 32;
 
+// Deterministic: a run of equal ids lying inside one chunk belongs to that chunk's wave (plain
+// read-modify-write of its table row). A run crossing a chunk boundary leaves one partial per
+// chunk it touches in `work` (slot 0: the chunk's first run continued from the previous chunk,
+// slot 1: its last run continuing into the next); segsum_join_kernel then sums those partials
+// in chunk order. No atomics, so the table gradient is bit-identical run to run.
+__device__ __forceinline__ bool seg_cont(const int64_t* ids, int a, int b, int rows) {
+  return a >= 0 && b < rows && ids[a] == ids[b];
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ drows,
                                                      const int64_t* __restrict__ sorted_ids,
                                                      const int64_t* __restrict__ perm, int rows,
                                                      int cols, int vocab, int pad_idx,
-                                                     float* __restrict__ dE) {
+                                                     float* __restrict__ dE,
+                                                     float* __restrict__ work) {
   const int lane = threadIdx.x & 63;
   const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int p0 = chunk * SEG_CHUNK;
   if (p0 >= rows) return;
   const int p1 = min(rows, p0 + SEG_CHUNK);
+  const bool cross_start = seg_cont(sorted_ids, p0 - 1, p0, rows);
+  const bool cross_end = seg_cont(sorted_ids, p1 - 1, p1, rows);
   float acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.f;
   long cur = (long)sorted_ids[p0];
-  auto flush = [&](long id) {
+  bool first = true;
+  auto flush = [&](long id, bool last) {
     if (id == pad_idx || id < 0 || id >= vocab) return;
-    float* dst = dE + (size_t)id * cols;
+    int slot = -1;
+    if (first && cross_start) slot = 0;
+    else if (last && cross_end) slot = 1;
+    float* dst = slot < 0 ? dE + (size_t)id * cols : work + ((size_t)chunk * 2 + slot) * cols;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) atomicAdd(dst + k * 64 + lane, acc[k]);
+    for (int k = 0; k < NV; ++k) {
+      if (slot < 0) dst[k * 64 + lane] += acc[k];
+      else dst[k * 64 + lane] = acc[k];
+    }
   };
   for (int p = p0; p < p1; ++p) {
     const long id = (long)sorted_ids[p];
     if (id != cur) {
-      flush(cur);
+      flush(cur, false);
+      first = false;
 #pragma unroll
       for (int k = 0; k < NV; ++k) acc[k] = 0.f;
       cur = id;
@@ -94,7 +114,38 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ d
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] += src[k * 64 + lane];
   }
-  flush(cur);
+  flush(cur, true);
+}
+
+// One wave per chunk whose last run starts inside it and crosses its end: sum the run's partials
+// (this chunk's slot 1, then slot 0 of every following chunk the run reaches) in chunk order.
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_join_kernel(const int64_t* __restrict__ sorted_ids,
+                                                          int rows, int cols, int vocab,
+                                                          int pad_idx, float* __restrict__ dE,
+                                                          const float* __restrict__ work) {
+  const int lane = threadIdx.x & 63;
+  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int p0 = chunk * SEG_CHUNK;
+  if (p0 >= rows) return;
+  const int p1 = min(rows, p0 + SEG_CHUNK);
+  if (!seg_cont(sorted_ids, p1 - 1, p1, rows)) return;                 // last run ends here
+  if (sorted_ids[p0] == sorted_ids[p1 - 1] && seg_cont(sorted_ids, p0 - 1, p0, rows))
+    return;                                                              // run started earlier
+  const long id = (long)sorted_ids[p1 - 1];
+  if (id == pad_idx || id < 0 || id >= vocab) return;
+  float acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = work[((size_t)chunk * 2 + 1) * cols + k * 64 + lane];
+  for (int c = chunk + 1;; ++c) {
+    const int q0 = c * SEG_CHUNK, q1 = min(rows, q0 + SEG_CHUNK);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] += work[((size_t)c * 2) * cols + k * 64 + lane];
+    if (sorted_ids[q1 - 1] != id || !seg_cont(sorted_ids, q1 - 1, q1, rows)) break;
+  }
+  float* dst = dE + (size_t)id * cols;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) dst[k * 64 + lane] += acc[k];
 }
 
 }  // namespace gacc
@@ -124,12 +175,20 @@ extern "C" int dna_colsum_f32(const float* part, int rows, int cols, float* out,
   return DNA_OK;
 }
 
+extern "C" size_t dna_embed_grad_segsum_workspace(int rows, int cols) {
+  const size_t chunks = (size_t)(rows + gacc::SEG_CHUNK - 1) / gacc::SEG_CHUNK;
+  return chunks * 2 * (size_t)cols * sizeof(float);
+}
+
 extern "C" int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_ids,
                                      const int64_t* perm, int rows, int cols, int vocab,
-                                     int padding_idx, float* dword_emb, void* stream) {
+                                     int padding_idx, float* dword_emb, float* work,
+                                     size_t work_bytes, void* stream) {
   DNA_CHECK_ARG(drows && sorted_ids && perm && dword_emb, "dna_embed_grad_segsum: null pointer");
   DNA_CHECK_ARG(cols % 64 == 0 && cols <= 1024, "dna_embed_grad_segsum: cols %% 64 != 0");
   if (rows == 0) return DNA_OK;
+  DNA_CHECK_ARG(work && work_bytes >= dna_embed_grad_segsum_workspace(rows, cols),
+                "dna_embed_grad_segsum: workspace too small");
   const int chunks = (rows + gacc::SEG_CHUNK - 1) / gacc::SEG_CHUNK;
   dim3 grid((chunks + 3) / 4);
   hipStream_t s = as_stream(stream);
@@ -137,7 +196,9 @@ extern "C" int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_i
 #define DNA_SEG_CASE(K)                                                                         \
   case K:                                                                                       \
     hipLaunchKernelGGL(gacc::segsum_kernel<K>, grid, dim3(256), 0, s, drows, sorted_ids, perm,   \
-                       rows, cols, vocab, padding_idx, dword_emb);                               \
+                       rows, cols, vocab, padding_idx, dword_emb, work);                         \
+    hipLaunchKernelGGL(gacc::segsum_join_kernel<K>, grid, dim3(256), 0, s, sorted_ids, rows,     \
+                       cols, vocab, padding_idx, dword_emb, work);                               \
     break;
     DNA_SEG_CASE(1) DNA_SEG_CASE(2) DNA_SEG_CASE(3) DNA_SEG_CASE(4) DNA_SEG_CASE(6)
     DNA_SEG_CASE(8) DNA_SEG_CASE(12) DNA_SEG_CASE(16)

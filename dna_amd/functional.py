@@ -129,10 +129,12 @@ class EmbeddingLN(torch.autograd.Function):
                tt[0].data_ptr(), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), T, d, V,
                p, seed, off, drows.data_ptr(), dtt[0].data_ptr(), dg.data_ptr(), db.data_ptr(),
                ws.data_ptr(), nws, N.stream_ptr())
-        sorted_ids, perm = torch.sort(ids)
+        sorted_ids, perm = torch.sort(ids, stable=True)  # fixed summation order run to run
         dE = torch.zeros_like(E)
+        nsw = N.lib().dna_embed_grad_segsum_workspace(T, d)
+        sw = torch.empty(max(nsw // 4, 4), device=E.device, dtype=torch.float32)
         N.call("dna_embed_grad_segsum", drows.data_ptr(), sorted_ids.data_ptr(), perm.data_ptr(),
-               T, d, V, 0, dE.data_ptr(), N.stream_ptr())
+               T, d, V, 0, dE.data_ptr(), sw.data_ptr(), nsw, N.stream_ptr())
         return None, dE, dtt, dg, db, None, None, None, None, None, None
 
 

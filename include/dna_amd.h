@@ -128,10 +128,13 @@ int dna_embed_ln_bwd_rows(const float* dy, const void* dy_bf16, const int64_t* i
 
 /* dword_emb[id] += sum of drows[perm[p]] over the id-sorted positions p (sorted_ids ascending,
  * perm = the argsort of ids); rows with id == padding_idx are skipped. Replaces the scatter-add
- * of nn.Embedding backward (padding_idx=0, bert_layers.py:45-47). */
+ * of nn.Embedding backward (padding_idx=0, bert_layers.py:45-47). Deterministic for a given
+ * (sorted_ids, perm): runs crossing 32-row chunks are joined through `work` in chunk order
+ * (work_bytes >= dna_embed_grad_segsum_workspace(rows, cols)). */
+size_t dna_embed_grad_segsum_workspace(int rows, int cols);
 int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_ids, const int64_t* perm,
                           int rows, int cols, int vocab, int padding_idx, float* dword_emb,
-                          void* stream);
+                          float* work, size_t work_bytes, void* stream);
 
 /* out[c] = sum_r part[r][c] (accumulate != 0: out[c] += ...), fp32, deterministic order;
  * cols % 64 == 0. Finishes the fused bias-gradient partials (Linear bias grads, autograd's
