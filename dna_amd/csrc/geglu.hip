@@ -1,6 +1,7 @@
 // GeGLU (+ dropout) of BertGatedLinearUnitMLP (bert_layers.py:292-296), fwd and bwd.
 //   a = dropout( gelu_erf(g[:, :F]) * g[:, F:] ),  g = gated_layers(x) with F = intermediate_size.
-// HBM-bound elementwise: 8 consecutive outputs per thread (16-B bf16 vectors), grid-stride.
+// HBM-bound elementwise: 8 consecutive outputs per thread (16-B bf16 vectors), grid-stride,
+// U rows per thread per iteration.
 // Algorithmic bytes per output element: fwd 2*s (read g1, g2) + s (write a); bwd 3*s + 2*s.
 // Dropout bits: dropout_keep8 (16-bit slices of one Philox draw per 8 elements).
 #include "common.h"
@@ -37,62 +38,92 @@ __device__ __forceinline__ uint32_t keep8(uint64_t seed, uint64_t off, uint64_t 
   return dropout_keep8(seed, off, elem >> 3, th16);  // elem is a multiple of 8
 }
 
-template <typename T>
+// U rows per iteration: every load of the U rows is issued before any arithmetic, so a wave
+// keeps U*2 (fwd) / U*3 (bwd) 16-B vectors per lane in flight instead of 2 / 3 (the U=1 kernels
+// reached only 66 % of HBM bandwidth at the bench shape).
+template <typename T, int U>
 __global__ __launch_bounds__(128) void fwd_kernel(const T* __restrict__ g, int rows, int F,
                                                   float p, uint32_t th, float ks, uint64_t seed,
                                                   uint64_t off, T* __restrict__ a) {
-  // 2-D launch: blockIdx.y walks rows, x covers one row's F/8 vectors (no 64-bit div/mod)
+  // 2-D launch: blockIdx.y walks row groups, x covers one row's F/8 vectors (no 64-bit div/mod)
   const int f8 = F / 8;
-  for (int r = blockIdx.y; r < rows; r += gridDim.y)
+  for (int r0 = blockIdx.y * U; r0 < rows; r0 += gridDim.y * U)
   for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < f8; v += gridDim.x * blockDim.x) {
     const size_t c = (size_t)v * 8;
-    const size_t e = (size_t)r * F + c;
-    Vec8<T> g1, g2;
-    g1.load(g + (size_t)r * 2 * F + c);
-    g2.load(g + (size_t)r * 2 * F + F + c);
-    float o[8];
-    uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
+    Vec8<T> g1[U], g2[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = gelu_erf(g1[j]) * g2[j];
-      o[j] = p > 0.f ? (((keep >> j) & 1) ? v * ks : 0.f) : v;
+    for (int u = 0; u < U; ++u) {
+      const int r = min(r0 + u, rows - 1);  // tail rows re-read the last row, never stored
+      g1[u].load(g + (size_t)r * 2 * F + c);
+      g2[u].load(g + (size_t)r * 2 * F + F + c);
     }
-    Vec8<T>::store(a + e, o);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = r0 + u;
+      if (U > 1 && r >= rows) break;
+      const size_t e = (size_t)r * F + c;
+      float o[8];
+      uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = gelu_erf(g1[u][j]) * g2[u][j];
+        o[j] = p > 0.f ? (((keep >> j) & 1) ? v * ks : 0.f) : v;
+      }
+      Vec8<T>::store(a + e, o);
+    }
   }
 }
 
-template <typename T>
+template <typename T, int U>
 __global__ __launch_bounds__(128) void bwd_kernel(const T* __restrict__ da, const T* __restrict__ g,
                                                   int rows, int F, float p, uint32_t th, float ks,
                                                   uint64_t seed, uint64_t off, T* __restrict__ dg) {
   const int f8 = F / 8;
-  for (int r = blockIdx.y; r < rows; r += gridDim.y)
+  for (int r0 = blockIdx.y * U; r0 < rows; r0 += gridDim.y * U)
   for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < f8; v += gridDim.x * blockDim.x) {
     const size_t c = (size_t)v * 8;
-    const size_t e = (size_t)r * F + c;
-    Vec8<T> g1, g2, d;
-    g1.load(g + (size_t)r * 2 * F + c);
-    g2.load(g + (size_t)r * 2 * F + F + c);
-    d.load(da + e);
-    uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
-    float o1[8], o2[8];
+    Vec8<T> g1[U], g2[U], d[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float dd = d[j];
-      if (p > 0.f) dd = ((keep >> j) & 1) ? dd * ks : 0.f;
-      float ge, dge;
-      gelu_erf_and_grad(g1[j], ge, dge);
-      o1[j] = dd * g2[j] * dge;
-      o2[j] = dd * ge;
+    for (int u = 0; u < U; ++u) {
+      const int r = min(r0 + u, rows - 1);
+      g1[u].load(g + (size_t)r * 2 * F + c);
+      g2[u].load(g + (size_t)r * 2 * F + F + c);
+      d[u].load(da + (size_t)r * F + c);
     }
-    Vec8<T>::store(dg + (size_t)r * 2 * F + c, o1);
-    Vec8<T>::store(dg + (size_t)r * 2 * F + F + c, o2);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = r0 + u;
+      if (U > 1 && r >= rows) break;
+      const size_t e = (size_t)r * F + c;
+      uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
+      float o1[8], o2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float dd = d[u][j];
+        if (p > 0.f) dd = ((keep >> j) & 1) ? dd * ks : 0.f;
+        float ge, dge;
+        gelu_erf_and_grad(g1[u][j], ge, dge);
+        o1[j] = dd * g2[u][j] * dge;
+        o2[j] = dd * ge;
+      }
+      Vec8<T>::store(dg + (size_t)r * 2 * F + c, o1);
+      Vec8<T>::store(dg + (size_t)r * 2 * F + F + c, o2);
+    }
   }
 }
 
-inline dim3 grid_for(int rows, int F) {
+// Rows per iteration (bf16 bench path; DNA_GEGLU_UNROLL=1/2/4 for A/B runs).
+inline int unroll_rows(int rows) {
+  static const int env = getenv("DNA_GEGLU_UNROLL") ? atoi(getenv("DNA_GEGLU_UNROLL")) : 0;
+  int u = env == 1 || env == 2 || env == 4 ? env : 2;
+  while (u > 1 && rows < 2048 * u) u /= 2;  // small launches keep one row per block
+  return u;
+}
+
+inline dim3 grid_for(int rows, int F, int u = 1) {
   const int bx = (F / 8 + 127) / 128;  // 3072/8 = 384 vectors -> 3 blocks of 128 per row
-  const int by = rows < 8192 ? (rows ? rows : 1) : 8192;
+  const int groups = (rows + u - 1) / u;
+  const int by = groups < 8192 ? (groups ? groups : 1) : 8192;
   return dim3(bx, by);
 }
 
@@ -107,15 +138,22 @@ extern "C" int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, floa
   DNA_CHECK_ARG(inter % 8 == 0 && rows >= 0, "dna_geglu_fwd: intermediate %% 8 != 0");
   DNA_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "dna_geglu_fwd: bad p");
   if (rows == 0) return DNA_OK;
-  const dim3 grid = geglu::grid_for(rows, inter);
   hipStream_t s = as_stream(stream);
   const uint32_t th = dropout_threshold16(p_drop);
   const float ks = 1.f / (1.f - p_drop);
-  if (dtype == DNA_BF16)
-    hipLaunchKernelGGL(geglu::fwd_kernel<bf16>, grid, dim3(128), 0, s, (const bf16*)g,
+  const int u = dtype == DNA_BF16 ? geglu::unroll_rows(rows) : 1;
+  const dim3 grid = geglu::grid_for(rows, inter, u);
+  if (dtype == DNA_BF16 && u == 4)
+    hipLaunchKernelGGL((geglu::fwd_kernel<bf16, 4>), grid, dim3(128), 0, s, (const bf16*)g,
+                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a);
+  else if (dtype == DNA_BF16 && u == 2)
+    hipLaunchKernelGGL((geglu::fwd_kernel<bf16, 2>), grid, dim3(128), 0, s, (const bf16*)g,
+                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a);
+  else if (dtype == DNA_BF16)
+    hipLaunchKernelGGL((geglu::fwd_kernel<bf16, 1>), grid, dim3(128), 0, s, (const bf16*)g,
                        rows, inter, p_drop, th, ks, seed, offset, (bf16*)a);
   else if (dtype == DNA_F32)
-    hipLaunchKernelGGL(geglu::fwd_kernel<float>, grid, dim3(128), 0, s, (const float*)g,
+    hipLaunchKernelGGL((geglu::fwd_kernel<float, 1>), grid, dim3(128), 0, s, (const float*)g,
                        rows, inter, p_drop, th, ks, seed, offset, (float*)a);
   else
     DNA_CHECK_ARG(false, "dna_geglu_fwd: bad dtype");
@@ -128,15 +166,22 @@ extern "C" int dna_geglu_bwd(const void* da, const void* g, int dtype, int rows,
   DNA_CHECK_ARG(da && g && dg, "dna_geglu_bwd: null pointer");
   DNA_CHECK_ARG(inter % 8 == 0 && rows >= 0, "dna_geglu_bwd: intermediate %% 8 != 0");
   if (rows == 0) return DNA_OK;
-  const dim3 grid = geglu::grid_for(rows, inter);
   hipStream_t s = as_stream(stream);
   const uint32_t th = dropout_threshold16(p_drop);
   const float ks = 1.f / (1.f - p_drop);
-  if (dtype == DNA_BF16)
-    hipLaunchKernelGGL(geglu::bwd_kernel<bf16>, grid, dim3(128), 0, s, (const bf16*)da,
+  const int u = dtype == DNA_BF16 ? geglu::unroll_rows(rows) : 1;
+  const dim3 grid = geglu::grid_for(rows, inter, u);
+  if (dtype == DNA_BF16 && u == 4)
+    hipLaunchKernelGGL((geglu::bwd_kernel<bf16, 4>), grid, dim3(128), 0, s, (const bf16*)da,
+                       (const bf16*)g, rows, inter, p_drop, th, ks, seed, offset, (bf16*)dg);
+  else if (dtype == DNA_BF16 && u == 2)
+    hipLaunchKernelGGL((geglu::bwd_kernel<bf16, 2>), grid, dim3(128), 0, s, (const bf16*)da,
+                       (const bf16*)g, rows, inter, p_drop, th, ks, seed, offset, (bf16*)dg);
+  else if (dtype == DNA_BF16)
+    hipLaunchKernelGGL((geglu::bwd_kernel<bf16, 1>), grid, dim3(128), 0, s, (const bf16*)da,
                        (const bf16*)g, rows, inter, p_drop, th, ks, seed, offset, (bf16*)dg);
   else if (dtype == DNA_F32)
-    hipLaunchKernelGGL(geglu::bwd_kernel<float>, grid, dim3(128), 0, s, (const float*)da,
+    hipLaunchKernelGGL((geglu::bwd_kernel<float, 1>), grid, dim3(128), 0, s, (const float*)da,
                        (const float*)g, rows, inter, p_drop, th, ks, seed, offset, (float*)dg);
   else
     DNA_CHECK_ARG(false, "dna_geglu_bwd: bad dtype");

@@ -202,6 +202,30 @@ def test_geglu(dtype, tol):
     assert (g.grad.float() - g2.grad).abs().max().item() < tol * 8
 
 
+@pytest.mark.parametrize("n", [4096, 8193, 16387, 70001])
+def test_geglu_row_unrolled_bf16(n):
+    """bf16 kernels (U = 2 or 4 rows per thread, ragged row tails) == the fp32 U=1 kernels on the
+    same bf16 inputs: identical dropout masks, values within bf16 rounding."""
+    from dna_amd import _native as N
+    torch.manual_seed(0)
+    F = 64
+    g = torch.randn(n, 2 * F, device=DEV).to(torch.bfloat16)
+    da = torch.randn(n, F, device=DEV).to(torch.bfloat16)
+    outs = {}
+    for dt, code in ((torch.bfloat16, 1), (torch.float32, 0)):
+        a = torch.empty(n, F, device=DEV, dtype=dt)
+        dg = torch.empty(n, 2 * F, device=DEV, dtype=dt)
+        N.call("dna_geglu_fwd", g.to(dt).data_ptr(), code, n, F, 0.1, 7, 3, a.data_ptr(),
+               N.stream_ptr())
+        N.call("dna_geglu_bwd", da.to(dt).data_ptr(), g.to(dt).data_ptr(), code, n, F, 0.1, 7, 3,
+               dg.data_ptr(), N.stream_ptr())
+        outs[code] = (a.float(), dg.float())
+    (a1, dg1), (a0, dg0) = outs[1], outs[0]
+    assert torch.equal(a1 == 0, a0 == 0)
+    assert (a1 - a0).abs().max().item() <= 8e-3 * a0.abs().max().item()
+    assert (dg1 - dg0).abs().max().item() <= 8e-3 * dg0.abs().max().item()
+
+
 @pytest.mark.parametrize("cols", [64, 128, 768])
 def test_embedding_ln(cols):
     from dna_amd import functional as DF
