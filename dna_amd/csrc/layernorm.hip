@@ -399,8 +399,12 @@ int dispatch_cols(int cols, F&& f) {
 }
 
 inline int bwd_blocks(int rows) {
+  // DNA_LN_BWD_BLOCKS: A/B switch for the grid cap (more blocks = more rows in flight, more
+  // [3][cols] partials for reduce_partials)
+  static const int cap = getenv("DNA_LN_BWD_BLOCKS") ? atoi(getenv("DNA_LN_BWD_BLOCKS")) : BWD_BLOCKS;
+  const int lim = cap >= 64 ? cap : BWD_BLOCKS;
   int nb = (rows + WAVES - 1) / WAVES;
-  return nb < BWD_BLOCKS ? nb : BWD_BLOCKS;
+  return nb < lim ? nb : lim;
 }
 
 }  // namespace ln
