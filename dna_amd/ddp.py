@@ -40,6 +40,7 @@ class GradBucketReducer:
         self._works = []
         self._fired = [False] * len(self.buckets)
         self._sync = True
+        self.fired_in_backward = 0
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in flat.params]
         for p in flat.params:  # contributions written directly by fused kernels report here
             p._dna_notify = self._hook
@@ -88,6 +89,8 @@ class GradBucketReducer:
         """Call after backward: launch what did not fire, wait for all collectives."""
         if not self.enabled or not self._sync:
             return
+        # how many buckets the backward itself launched (overlap evidence; tests read it)
+        self.fired_in_backward = sum(self._fired)
         if self.expected is None:
             self.expected = dict(self._seen)
         for bi in range(len(self.buckets)):
@@ -102,15 +105,23 @@ class GradBucketReducer:
         return 1.0 / self.world
 
 
-def reduce_metrics(loss, num_tokens, group=None):
+def reduce_metrics(loss, num_tokens, group=None, extra=None):
     """Rank-mean of the step loss and the global token count as ONE small all-reduce (SURVEY
     §8(e): DDP loss semantics = mean of per-rank masked-token means; scalar metrics packed into
     one collective at the logging interval). Returns (mean_loss, total_tokens) as Python numbers;
-    without a process group, the local values."""
+    without a process group, the local values. With `extra` (a list of scalar tensors or numbers:
+    torchmetric states whose dist_reduce_fx is "sum"), returns (mean_loss, [their global sums])
+    in place of the token count, still one collective."""
     lv = loss.detach().reshape(()).to(torch.float64)
-    if not (dist.is_available() and dist.is_initialized()):
-        return float(lv.item()), int(num_tokens)
-    world = dist.get_world_size(group)
-    t = torch.stack([lv, torch.tensor(float(num_tokens), dtype=torch.float64, device=lv.device)])
-    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    return float(t[0].item()) / world, int(round(float(t[1].item())))
+    vals = [num_tokens] if extra is None else list(extra)
+    t = torch.stack([lv] + [torch.as_tensor(v).detach().to(device=lv.device, dtype=torch.float64)
+                            .reshape(()) for v in vals])
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        world = dist.get_world_size(group)
+    else:
+        world = 1
+    out = t.cpu().tolist()
+    if extra is None:
+        return out[0] / world, int(round(out[1]))
+    return out[0] / world, out[1:]

@@ -77,7 +77,8 @@ class _timed:
 
 class DropoutRNG:
     """Counter-based dropout stream: every dropout site draws (seed, offset) and advances the
-    offset by the number of Philox4x32 groups it consumes, so backward regenerates the mask."""
+    offset by the number of Philox4x32 groups it consumes, so backward regenerates the mask.
+    MLMTrainer derives the seed from train.seed and the rank; checkpoints keep (seed, offset)."""
 
     def __init__(self, seed=2222):
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
@@ -135,6 +136,9 @@ class EmbeddingLN(torch.autograd.Function):
         sw = torch.empty(max(nsw // 4, 4), device=E.device, dtype=torch.float32)
         N.call("dna_embed_grad_segsum", drows.data_ptr(), sorted_ids.data_ptr(), perm.data_ptr(),
                T, d, V, 0, dE.data_ptr(), sw.data_ptr(), nsw, N.stream_ptr())
+        # the tied decoder's weight gradient may still be adding into E.grad on the wgrad side
+        # stream; AccumulateGrad adds dE into the same buffer on this stream next
+        join_side_stream()
         return None, dE, dtt, dg, db, None, None, None, None, None, None
 
 

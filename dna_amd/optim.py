@@ -56,15 +56,69 @@ class FusedAdamW:
     def zero_grad(self, set_to_none=False):
         self.flat.zero_grad()
 
-    def state_dict(self):
-        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
-                "param_groups": [dict(g) for g in self.param_groups]}
+    def _ordered_params(self):
+        """Parameters in module registration order = torch's optimizer param indices for the
+        reference's single AdamW group (train.py:462-473: list(self.parameters()))."""
+        return self.flat.params[::-1]
+
+    def state_dict(self, torch_layout=True):
+        """torch.optim.AdamW layout ({"state": {i: {step, exp_avg, exp_avg_sq}}, "param_groups"}),
+        which Lightning's checkpoint loader and torch AdamW.load_state_dict accept; per-parameter
+        moments are copied out of the flat buffers. torch_layout=False: the flat form."""
+        g = dict(self.param_groups[0])
+        if not torch_layout:
+            return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                    "param_groups": [g]}
+        params = self._ordered_params()
+        state = {}
+        if self.step_count > 0:
+            for i, p in enumerate(params):
+                o, n, shape = self.flat.slice_of(p)
+                state[i] = {"step": torch.tensor(float(self.step_count)),
+                            "exp_avg": self.exp_avg[o:o + n].view(shape).detach().cpu().clone(),
+                            "exp_avg_sq": self.exp_avg_sq[o:o + n].view(shape).detach().cpu().clone()}
+        g.setdefault("amsgrad", False)
+        g.setdefault("maximize", False)
+        g.setdefault("foreach", None)
+        g.setdefault("capturable", False)
+        g.setdefault("differentiable", False)
+        g.setdefault("fused", None)
+        g["params"] = list(range(len(params)))
+        return {"state": state, "param_groups": [g]}
 
     def load_state_dict(self, sd):
+        """Accepts the flat form and torch's AdamW layout (a Lightning checkpoint of the
+        reference: one param group, indices in registration order)."""
+        if "state" in sd:
+            params = self._ordered_params()
+            groups = sd["param_groups"]
+            n_idx = sum(len(g["params"]) for g in groups)
+            if n_idx != len(params):
+                raise ValueError(f"optimizer state holds {n_idx} parameters, model has {len(params)}")
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            step = 0
+            for i, p in enumerate(params):
+                st = sd["state"].get(i, sd["state"].get(str(i)))
+                if not st:
+                    continue
+                o, n, shape = self.flat.slice_of(p)
+                if tuple(st["exp_avg"].shape) != tuple(shape):
+                    raise ValueError(f"optimizer state {i}: shape {tuple(st['exp_avg'].shape)} "
+                                     f"!= parameter shape {tuple(shape)}")
+                self.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                step = max(step, int(float(st["step"])))
+            self.step_count = step
+            g0 = groups[0]
+            self.param_groups = [dict(lr=float(g0["lr"]), betas=tuple(g0["betas"]),
+                                      eps=float(g0["eps"]), weight_decay=float(g0["weight_decay"]),
+                                      initial_lr=float(g0.get("initial_lr", g0["lr"])))]
+            return
         self.step_count = int(sd["step"])
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
-        self.param_groups = [dict(g) for g in sd["param_groups"]]
+        self.param_groups = [{k: v for k, v in g.items() if k != "params"} for g in sd["param_groups"]]
 
 
 class LinearLRSchedulerWarmup:
@@ -106,7 +160,15 @@ class LinearLRSchedulerWarmup:
         return [g["lr"] for g in self.optimizer.param_groups]
 
     def state_dict(self):
-        return {"last_epoch": self._last_epoch}
+        """timm Scheduler.state_dict keys (the instance __dict__ minus the optimizer)."""
+        return {"_last_epoch": self._last_epoch, "t_initial": self.t_initial,
+                "warmup_t": self.warmup_t, "warmup_lr_init": self.warmup_lr_init,
+                "lr_min": self.lr_min, "t_in_epochs": self.t_in_epochs,
+                "cycle_limit": self.cycle_limit, "cycle_decay": self.cycle_decay,
+                "base_values": list(self.base_values)}
 
     def load_state_dict(self, sd):
-        self.step(epoch=sd["last_epoch"])
+        """Resumes the step counter; accepts the reference's timm layout (`_last_epoch`) and the
+        round-1 form of this file (`last_epoch`)."""
+        t = sd["_last_epoch"] if "_last_epoch" in sd else sd["last_epoch"]
+        self.step(epoch=int(t))

@@ -38,7 +38,10 @@ class Perplexity:
         self.count = torch.zeros((), dtype=torch.int64)
 
     def update(self, preds, target, loss):
-        count = target.numel()
+        self.update_count(loss, target.numel())
+
+    def update_count(self, loss, count):
+        """update() given target.numel() instead of the target tensor (no device sync)."""
         self.total_log_probs = self.total_log_probs.to(loss.device) + loss.detach().double() * count
         self.count = self.count.to(loss.device) + count
 

@@ -45,7 +45,7 @@ class DeviceBatch:
 class MLMTrainer:
     def __init__(self, model: BertForMaskedLM, device, lr=5e-4, weight_decay=1e-5,
                  betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0, scheduler=None,
-                 bucket_mb=25.0):
+                 bucket_mb=25.0, seed=None):
         self.model = model.to(device).train()
         self.device = device
         self.flat = FlatParams(self.model, device)
@@ -60,10 +60,21 @@ class MLMTrainer:
         if self.world > 1:  # DDP construction broadcast (C2 in SURVEY §2.2)
             dist.broadcast(self.flat.flat, src=0)
             self.flat.refresh_shadow()
-        # per-rank dropout streams must differ
+        # dropout stream: derived from train.seed when given, and distinct per rank
         rank = dist.get_rank() if dist.is_initialized() else 0
-        self.model.dropout_rng.seed = (self.model.dropout_rng.seed * 1000003 + rank) & (2 ** 63 - 1)
+        base = self.model.dropout_rng.seed if seed is None else int(seed) + 0x5EED
+        self.model.dropout_rng.seed = (base * 1000003 + rank) & (2 ** 63 - 1)
         self.global_step = 0
+        self.micro_losses = []  # undivided loss of each micro-batch of the last step (metrics)
+
+    def rng_state(self):
+        """Dropout stream position, saved in checkpoints so a resume does not replay masks."""
+        r = self.model.dropout_rng
+        return {"seed": int(r.seed), "offset": int(r.offset)}
+
+    def load_rng_state(self, st):
+        self.model.dropout_rng.seed = int(st["seed"])
+        self.model.dropout_rng.offset = int(st["offset"])
 
     def step(self, batch) -> torch.Tensor:
         """One optimizer step over one micro-batch or a list of them (accumulate_grad_batches:
@@ -72,11 +83,13 @@ class MLMTrainer:
         micro = batch if isinstance(batch, (list, tuple)) else [batch]
         self.opt.zero_grad()
         total = None
+        self.micro_losses = []
         for i, mb in enumerate(micro):
             last = i == len(micro) - 1
             self.reducer.prepare(sync=last)
             loss, _ = self.model.mlm_loss(mb.masked_ids, mb.mask, mb.index, mb.n_mask,
                                           mb.n_unk_masked)
+            self.micro_losses.append(loss.detach())
             if len(micro) > 1:
                 loss = loss / len(micro)
             loss.backward()

@@ -18,7 +18,7 @@ def _norm(x, sd, prefix, rms, eps):
 
 
 def mlm_logits(sd, ids, n_layer, d_state, d_conv, dt_rank, rms_norm=True, eps=1e-5,
-               strategy="add"):
+               strategy="add", scan=None):
     p0 = "caduceus.backbone."
     h = F.embedding(ids, sd[p0 + "embeddings.word_embeddings.weight"])
     residual = None
@@ -27,7 +27,8 @@ def mlm_logits(sd, ids, n_layer, d_state, d_conv, dt_rank, rms_norm=True, eps=1e
         residual = h if residual is None else h + residual
         x = _norm(residual, sd, p + "norm.", rms_norm, eps)
         msd = {k[len(p + "mixer."):]: v for k, v in sd.items() if k.startswith(p + "mixer.")}
-        h = bimamba_forward(msd, x, d_state, d_conv, dt_rank, strategy=strategy)
+        kw = {} if scan is None else {"scan": scan}
+        h = bimamba_forward(msd, x, d_state, d_conv, dt_rank, strategy=strategy, **kw)
     residual = h + residual
     h = _norm(residual, sd, p0 + "norm_f.", rms_norm, eps)
     return F.linear(h, sd["lm_head.weight"])

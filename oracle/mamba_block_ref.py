@@ -22,8 +22,9 @@ import torch.nn.functional as F
 from .selective_scan_ref import selective_scan_ref
 
 
-def mamba_forward(sd, h, d_state, d_conv, dt_rank, prefix=""):
-    """Mamba.forward (non-fused path) on h [b, l, d_model] with state_dict `sd`."""
+def mamba_forward(sd, h, d_state, d_conv, dt_rank, prefix="", scan=selective_scan_ref):
+    """Mamba.forward (non-fused path) on h [b, l, d_model] with state_dict `sd`; `scan` may be
+    oracle.selective_scan_c.selective_scan_c (same math, C loops) for long sequences."""
     b, l, _ = h.shape
     W = sd[prefix + "in_proj.weight"]
     xz = torch.einsum("ed,bld->bel", W, h)
@@ -40,20 +41,21 @@ def mamba_forward(sd, h, d_state, d_conv, dt_rank, prefix=""):
     B = B.reshape(b, l, d_state).transpose(1, 2)
     C = C.reshape(b, l, d_state).transpose(1, 2)
     A = -torch.exp(sd[prefix + "A_log"])
-    y = selective_scan_ref(x, dt, A, B, C, D=sd[prefix + "D"], z=z,
+    y = scan(x, dt, A, B, C, D=sd[prefix + "D"], z=z,
                            delta_bias=sd[prefix + "dt_proj.bias"], delta_softplus=True)
     out = F.linear(y.transpose(1, 2), sd[prefix + "out_proj.weight"], sd.get(prefix + "out_proj.bias"))
     return out
 
 
-def bimamba_forward(sd, h, d_state, d_conv, dt_rank, strategy="add", weight_tie=True):
+def bimamba_forward(sd, h, d_state, d_conv, dt_rank, strategy="add", weight_tie=True,
+                    scan=selective_scan_ref):
     """BiMambaWrapper.forward (modeling_caduceus.py:107-121)."""
-    out = mamba_forward(sd, h, d_state, d_conv, dt_rank, prefix="mamba_fwd.")
+    out = mamba_forward(sd, h, d_state, d_conv, dt_rank, prefix="mamba_fwd.", scan=scan)
     rev_sd = dict(sd)
     if weight_tie:
         for k in ("in_proj.weight", "in_proj.bias", "out_proj.weight", "out_proj.bias"):
             if "mamba_fwd." + k in sd:
                 rev_sd["mamba_rev." + k] = sd["mamba_fwd." + k]
     out_rev = mamba_forward(rev_sd, h.flip(dims=(1,)), d_state, d_conv, dt_rank,
-                            prefix="mamba_rev.").flip(dims=(1,))
+                            prefix="mamba_rev.", scan=scan).flip(dims=(1,))
     return out + out_rev if strategy == "add" else out * out_rev

@@ -295,10 +295,70 @@ def gen_model(tag, layers, d, heads, ff, b, S, pad_rows, grads, rng):
     print(f"model_{tag}: {int(sel.sum())} logit rows, task loss {task_loss.item():.6f}")
 
 
+N_SAMPLE = 1024      # sampled gradient elements per parameter (model_117m_grads.npz)
+N_LOGIT_ROWS = 64    # masked logit rows kept per precision
+
+
+def gen_model_grads(tag, layers, d, heads, ff, b, S, pad_rows, rng):
+    """The benchmarked configuration's gradients and one optimizer step, from the reference:
+    the same hash-initialised BertForMaskedLM run twice on one batch -- fp32, and under CPU
+    torch.autocast(bfloat16) (the reference trains with `precision: bf16`, i.e. Lightning's
+    bf16 autocast; dnabert2_hg38_pretrain.yaml `trainer.precision`) -- eval mode (no dropout),
+    bert_cross_entropy task loss (metrics.py:268-273). Stored: masked-row logits of both runs,
+    every parameter's gradient L2 norm in both runs, N_SAMPLE seeded elements of every gradient
+    in both runs, and the parameter change of one reference optimizer step on the fp32
+    gradients: torch clip_grad_norm_(1.0) (gradient_clip_val) + torch.optim.AdamW(lr 5e-4,
+    weight_decay 1e-5) (configs/optimizer/adamw.yaml + the experiment's overrides)."""
+    cfg = _model_cfg(layers, d, heads, ff)
+    masked, mask, labels, target = _make_batch(rng, b, S, pad_rows)
+    batch = (torch.as_tensor(masked), torch.as_tensor(mask), torch.as_tensor(labels))
+    sel = torch.as_tensor(labels).reshape(-1) > 0
+    pick = np.random.default_rng(7)
+    res = dict(masked_ids=masked.astype(np.int16), mask=mask, labels=labels.astype(np.int16),
+               target=target.astype(np.int16), config=np.bytes_(json.dumps([layers, d, heads, ff])))
+    for prec in ("32", "bf16"):
+        m, bl = _ref_model(cfg)
+        m.eval()
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=prec == "bf16"):
+            out, _ = m(batch, state=None)
+            x0 = out.logits[0].reshape(-1, VOCAB)
+            task_loss = _bert_cross_entropy([x0, out.logits[1]], torch.as_tensor(target).reshape(-1))
+        task_loss.backward()
+        res[f"logits_rows{prec}"] = x0[sel][:N_LOGIT_ROWS].detach().float().numpy()
+        res[f"task_loss{prec}"] = np.float64(task_loss.item())
+        for n, p in m.named_parameters():
+            g = p.grad.detach().float().reshape(-1).numpy()
+            if prec == "32":
+                k = min(N_SAMPLE, g.size)
+                res["gidx/" + n] = np.sort(pick.choice(g.size, k, replace=False)).astype(np.int32)
+            res[f"gradnorm{prec}/" + n] = np.float64(np.linalg.norm(g.astype(np.float64)))
+            res[f"gs{prec}/" + n] = g[res["gidx/" + n]]
+        if prec == "32":
+            before = {n: p.detach().clone() for n, p in m.named_parameters()}
+            res["clip_total_norm"] = np.float64(
+                torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0).item())
+            opt = torch.optim.AdamW(m.parameters(), lr=5e-4, weight_decay=1e-5)
+            opt.step()
+            for n, p in m.named_parameters():
+                dp = (p.detach() - before[n]).reshape(-1).numpy()
+                res["dp/" + n] = dp[res["gidx/" + n]]
+        print(f"model_{tag}: precision {prec}, task loss {task_loss.item():.6f}")
+    np.savez_compressed(os.path.join(HERE, f"model_{tag}.npz"), **res)
+
+
 def main():
     _install_shims()
     sys.path.insert(0, REF)
     torch.set_num_threads(8)
+    grads_only = "--only-grads" in sys.argv  # regenerate model_117m_grads.npz alone
+    if not grads_only:
+        main_round1()
+    # the benchmarked step (117M, S=512): fp32 and bf16-autocast gradients + one AdamW step
+    gen_model_grads("117m_grads", 12, 768, 12, 3072, 2, 512, {1: 300},
+                    np.random.default_rng(2223))
+
+
+def main_round1():
     rng = np.random.default_rng(2222)
     tok, ds514 = gen_tokenizer(rng)
     hg = _load_hg38_dataset()

@@ -190,3 +190,64 @@ def test_wgrad_side_stream_same_gradients(monkeypatch):
             loss.backward()
         grads.append(flat.grad.clone())  # read right after backward(): no explicit sync
     assert torch.equal(grads[0], grads[1])
+
+
+def test_bf16_train_step_vs_reference_fixture():
+    """The benchmarked step itself (MLMTrainer, bf16: MFMA attention, fused LN / GeGLU / CE
+    kernels, direct weight gradients, fused clip + AdamW) on the full 117M shape, S=512, against
+    the reference run in fp32 and under bf16 autocast (tests/golden/model_117m_grads.npz, made
+    by make_golden.py --only-grads). Tolerances are the reference's own bf16 error scaled by 2:
+    whatever bf16 rounding costs the reference, ours may cost at most twice that.
+      logits       max / rms |ours - ref32| <= 2x max / rms |ref_bf16 - ref32|
+      gradients    per parameter, relative L2 over 1024 sampled elements
+                   <= 2x (ref_bf16 vs ref32) + 5e-3; gradient norms within 1e-2
+      AdamW step   sign disagreements of the step vs the reference step <= 2x the reference's
+                   own bf16 sign disagreements + 0.5 % of the sampled elements."""
+    from dna_amd.bert_layers import MLMIndex
+    from dna_amd.trainer import DeviceBatch, MLMTrainer
+    z = np.load(os.path.join(GOLDEN, "model_117m_grads.npz"))
+    L, d, H, Fd = json.loads(z["config"].tobytes().decode())
+    cfg = dict(vocab_size=4096, hidden_size=d, num_hidden_layers=L, num_attention_heads=H,
+               intermediate_size=Fd, hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.0,
+               layer_norm_eps=1e-12, max_position_embeddings=512, type_vocab_size=2,
+               pad_token_id=0, alibi_starting_size=512, hidden_act="gelu",
+               initializer_range=0.02, hyena_framework=True)
+    m = _model(cfg, "bf16")
+    masked = torch.as_tensor(z["masked_ids"].astype(np.int64))
+    mask = torch.as_tensor(z["mask"])
+    labels = torch.as_tensor(z["labels"].astype(np.int64))
+    target = torch.as_tensor(z["target"].astype(np.int64))
+    # logits of the bf16 path
+    with torch.no_grad():
+        idx = MLMIndex.build(masked, labels).to(DEV)
+        logits = m.mlm_logits(masked.to(DEV), idx).float().cpu().numpy()[:z["logits_rows32"].shape[0]]
+    l32, l16 = z["logits_rows32"], z["logits_rowsbf16"]
+    ref_max, ref_rms = np.abs(l16 - l32).max(), np.sqrt(((l16 - l32) ** 2).mean())
+    assert np.abs(logits - l32).max() <= 2 * ref_max, (np.abs(logits - l32).max(), ref_max)
+    assert np.sqrt(((logits - l32) ** 2).mean()) <= 2 * ref_rms
+    tr = MLMTrainer(m, torch.device(DEV), lr=5e-4, weight_decay=1e-5, max_grad_norm=1.0)
+    m.eval()  # the fixture is eval mode (no dropout)
+    before = {n: p.detach().clone() for n, p in m.named_parameters()}
+    loss = tr.step(DeviceBatch.from_host(masked, mask, labels, target, torch.device(DEV)))
+    torch.cuda.synchronize()
+    assert abs(loss.item() - float(z["task_loss32"])) <= 2 * abs(float(z["task_lossbf16"]) -
+                                                                 float(z["task_loss32"])) + 1e-3
+    total_sq, flips, flips_ref, count = 0.0, 0, 0, 0
+    for n, p in m.named_parameters():
+        gi = z["gidx/" + n]
+        g = p.grad.detach().reshape(-1).cpu().numpy()
+        total_sq += float((g.astype(np.float64) ** 2).sum())
+        gs = g[gi]
+        g32, g16 = z["gs32/" + n], z["gsbf16/" + n]
+        nref = np.linalg.norm(g32)
+        err = np.linalg.norm(gs - g32) / nref
+        ref_err = np.linalg.norm(g16 - g32) / nref
+        assert err <= 2 * ref_err + 5e-3, (n, err, ref_err)
+        gn = float(np.linalg.norm(g.astype(np.float64)))
+        assert abs(gn - float(z["gradnorm32/" + n])) <= 1e-2 * float(z["gradnorm32/" + n]), n
+        dp = (p.detach() - before[n]).reshape(-1).cpu().numpy()[gi]
+        flips += int((np.sign(dp) != np.sign(z["dp/" + n])).sum())
+        flips_ref += int((np.sign(g16) != np.sign(g32)).sum())
+        count += gi.size
+    assert abs(math.sqrt(total_sq) - float(z["clip_total_norm"])) <= 1e-2 * float(z["clip_total_norm"])
+    assert flips <= 2 * flips_ref + 0.005 * count, (flips, flips_ref, count)

@@ -147,3 +147,35 @@ def test_lr_schedule_restatement():
     assert abs(optim_ref.linear_warmup_lr(60000, 5e-4, 120000, 2e6) - 2.5e-4) < 1e-12
     assert abs(optim_ref.linear_warmup_lr(120000, 5e-4, 120000, 2e6) - 5e-4) < 1e-12
     assert abs(optim_ref.linear_warmup_lr(1120000, 5e-4, 120000, 2e6) - 2.5e-4) < 1e-12
+
+
+def test_model_117m_grads_and_step_match_reference():
+    """The oracle at the benchmarked shape (117M, S=512) vs the reference's fp32 run: logits,
+    sampled gradient elements, gradient norms, the clip norm and one AdamW step."""
+    z, cfg, sd = _load_model("117m_grads")
+    for v in sd.values():
+        v.requires_grad_(True)
+    ids = torch.as_tensor(z["masked_ids"].astype(np.int64))
+    labels = torch.as_tensor(z["labels"].astype(np.int64))
+    logits, _, dense = bert_ref.dnabert2_forward(sd, cfg, ids, labels)
+    n_rows = z["logits_rows32"].shape[0]
+    np.testing.assert_allclose(logits.detach().numpy()[:n_rows], z["logits_rows32"], atol=1e-4, rtol=0)
+    loss = bert_ref.bert_cross_entropy(dense, torch.as_tensor(z["mask"]),
+                                       torch.as_tensor(z["target"].astype(np.int64)))
+    assert abs(loss.item() - float(z["task_loss32"])) < 1e-5
+    loss.backward()
+    gs = {n: p.grad.numpy().astype(np.float64) for n, p in sd.items()}
+    coef, total = optim_ref.clip_coef(list(gs.values()), 1.0)
+    assert abs(total - float(z["clip_total_norm"])) <= 1e-3 * float(z["clip_total_norm"])
+    for n, g in gs.items():
+        ref_norm = float(z["gradnorm32/" + n])
+        assert abs(np.linalg.norm(g) - ref_norm) <= 1e-3 * max(ref_norm, 1e-3), n
+        gi = z["gidx/" + n]
+        gf = g.reshape(-1)[gi]
+        scale = max(np.abs(z["gs32/" + n]).max(), 1e-8)
+        assert np.abs(gf - z["gs32/" + n]).max() <= 2e-3 * scale, n
+        p0 = sd[n].detach().numpy().astype(np.float64).reshape(-1)[gi]
+        p1, _, _ = optim_ref.adamw_step(p0, gf * coef, np.zeros_like(gf), np.zeros_like(gf), 1,
+                                        5e-4, weight_decay=1e-5)
+        agree = np.isclose(p1 - p0, z["dp/" + n], rtol=1e-3, atol=1e-9)
+        assert agree.mean() >= 0.99, (n, agree.mean())

@@ -67,13 +67,22 @@ def load_lightning_state(model, path, strict):
     return missing, unexpected
 
 
-def save_checkpoint(path, trainer, epoch):
+def save_checkpoint(path, trainer, epoch, batches_done=0, metrics=None):
+    """Lightning-1.8 checkpoint layout: state_dict with the "model." prefix, torch AdamW
+    optimizer state, timm scheduler state, epoch / global_step; plus this engine's dropout-stream
+    position and the count of batches already consumed in `epoch` (mid-epoch resume). Written to
+    a temporary file and renamed, so a crash never leaves a truncated last.ckpt."""
     m = trainer.model
     sd = {"model." + k: v.detach().cpu() for k, v in m.state_dict().items()}
-    torch.save({"state_dict": sd, "epoch": epoch, "global_step": trainer.global_step,
-                "optimizer_states": [{k: (v.cpu() if torch.is_tensor(v) else v)
-                                      for k, v in trainer.opt.state_dict().items()}],
-                "lr_schedulers": [trainer.sched.state_dict()] if trainer.sched else []}, path)
+    ck = {"state_dict": sd, "epoch": int(epoch), "global_step": int(trainer.global_step),
+          "pytorch-lightning_version": "1.8.0",
+          "optimizer_states": [trainer.opt.state_dict()],
+          "lr_schedulers": [trainer.sched.state_dict()] if trainer.sched else [],
+          "dna_amd": {"dropout_rng": trainer.rng_state(), "batches_done": int(batches_done),
+                      "metrics": metrics or {}}}
+    tmp = path + ".tmp"
+    torch.save(ck, tmp)
+    os.replace(tmp, path)
 
 
 def train(cfg, dry_run=False, out=sys.stdout):
@@ -128,9 +137,9 @@ def train(cfg, dry_run=False, out=sys.stdout):
                          weight_decay=float(opt.get("weight_decay", 0.0)),
                          betas=tuple(opt.get("betas", (0.9, 0.999))),
                          max_grad_norm=float(tr.get("gradient_clip_val", 0.0) or 0.0),
-                         scheduler=sched)
+                         scheduler=sched, seed=seed)
     resume = tr.get("resume_from_checkpoint") or cfg.train.get("ckpt")
-    start_epoch = 0
+    start_epoch, skip_batches, restored = 0, 0, {}
     if resume:
         if os.path.exists(resume):
             ck = torch.load(resume, map_location="cpu", weights_only=True)
@@ -142,6 +151,13 @@ def train(cfg, dry_run=False, out=sys.stdout):
                 trainer.sched.load_state_dict(ck["lr_schedulers"][0])
             trainer.global_step = int(ck.get("global_step", 0))
             start_epoch = int(ck.get("epoch", 0))
+            extra = ck.get("dna_amd") or {}
+            if extra.get("dropout_rng"):
+                trainer.load_rng_state(extra["dropout_rng"])
+                # distinct per rank, as MLMTrainer derives it
+                trainer.model.dropout_rng.seed = (trainer.model.dropout_rng.seed + rank) & (2 ** 63 - 1)
+            skip_batches = int(extra.get("batches_done", 0))
+            restored = extra.get("metrics") or {}
         else:
             warnings.warn(f"resume checkpoint {resume} not found; training from scratch")
 
@@ -157,54 +173,90 @@ def train(cfg, dry_run=False, out=sys.stdout):
     log_every = int(tr.get("log_every_n_steps", 10) or 10)
     limit = tr.get("limit_train_batches", 1.0)
     pad_id = getattr(ds.tokenizer, "pad_token_id", 3)
-    ppl_sum, ppl_cnt, num_tokens = 0.0, 0, 0
+    ck_cfg = cfg.get("callbacks", {}) or {}
+    mc = ck_cfg.get("model_checkpoint") if ck_cfg else None
+    ck_path = None
+    if rank == 0 and mc is not None:
+        d = mc.get("dirpath", "checkpoints/")
+        os.makedirs(d, exist_ok=True)
+        ck_path = os.path.join(d, "last.ckpt")
+    ck_every = int((mc.get("every_n_train_steps") if mc is not None else 0) or 1000)
+    # task torchmetrics (torchmetrics.py:24-115): Perplexity reset each epoch, NumTokens never.
+    # Both are updated per micro-batch with that micro-batch's loss and target.numel(), and
+    # SUM-reduced over ranks when logged (dist_reduce_fx="sum", sync_dist=True).
+    from dna_amd.tasks import NumTokens, Perplexity
+    ppl, ntok = Perplexity(), NumTokens()
+    ntok.count = torch.tensor(int(restored.get("num_tokens_local", 0)), dtype=torch.int64)
     t_last = time.perf_counter()
     done = False
+    epoch = start_epoch
+
+    def optimizer_step(micro):
+        loss = trainer.step([m for m, _ in micro])
+        for (_, numel), ml in zip(micro, trainer.micro_losses):
+            ppl.update_count(ml, numel)  # numel = target.numel() of that micro-batch
+            ntok.count = ntok.count + numel
+        return loss
+
+    def log_line(loss):
+        nonlocal t_last
+        step = trainer.global_step
+        lv, sums = reduce_metrics(loss, 0, extra=[ppl.total_log_probs, ppl.count, ntok.count])
+        now = time.perf_counter()
+        if rank == 0:
+            print(json.dumps({"step": step, "epoch": epoch, "train/loss": round(lv, 5),
+                              "trainer/loss": round(lv, 5),
+                              "train/perplexity": round(math.exp(sums[0] / max(sums[1], 1)), 4),
+                              "train/num_tokens": int(sums[2]),
+                              "trainer/lr": trainer.opt.param_groups[0]["lr"],
+                              "timer/step": round((now - t_last) / (log_every if step > 1 else 1), 5)}),
+                  file=out, flush=True)
+        t_last = now
+
+    def checkpoint(ep, batches_done):
+        if ck_path is not None:
+            save_checkpoint(ck_path, trainer, ep, batches_done,
+                            {"num_tokens_local": int(ntok.count)})
+
     for epoch in range(start_epoch, max_epochs):
         if sampler is not None:
             sampler.set_epoch(epoch)
+        ppl.reset()
         n_batches = len(loader)
         if isinstance(limit, float) and limit <= 1.0:
             n_batches = max(1, int(n_batches * limit))
         elif limit:
             n_batches = min(n_batches, int(limit))
         micro = []
+        bi = -1
         for bi, ((masked, mask, labels), target) in enumerate(loader):
             if bi >= n_batches:
+                bi -= 1
                 break
-            micro.append(DeviceBatch.from_host(masked, mask, labels, target, device, pad_id))
-            num_tokens += target.numel()
+            if bi < skip_batches:  # mid-epoch resume: these batches were consumed before
+                continue
+            micro.append((DeviceBatch.from_host(masked, mask, labels, target, device, pad_id),
+                          target.numel()))
             if len(micro) < accum:
                 continue
-            loss = trainer.step(micro)
+            loss = optimizer_step(micro)
             micro = []
             step = trainer.global_step
             if step % log_every == 0 or step == 1:
-                # every rank joins: rank-mean loss + global token count in one all-reduce
-                lv, tokens_all = reduce_metrics(loss, num_tokens)
-                ppl_sum += lv
-                ppl_cnt += 1
-                now = time.perf_counter()
-                if rank == 0:
-                    print(json.dumps({"step": step, "epoch": epoch, "train/loss": round(lv, 5),
-                                      "trainer/loss": round(lv, 5),
-                                      "train/perplexity": round(math.exp(ppl_sum / ppl_cnt), 4),
-                                      "train/num_tokens": tokens_all,
-                                      "trainer/lr": trainer.opt.param_groups[0]["lr"],
-                                      "timer/step": round((now - t_last) / (log_every if step > 1 else 1), 5)}),
-                          file=out, flush=True)
-                t_last = now
+                log_line(loss)  # every rank joins the metric all-reduce
+            if step % ck_every == 0:
+                checkpoint(epoch, bi + 1)
             if max_steps and step >= int(max_steps):
                 done = True
                 break
+        if micro and not done:  # Lightning steps on the epoch's last, partial accumulation
+            loss = optimizer_step(micro)
+            log_line(loss)
+        skip_batches = 0
+        # epoch finished (or max_steps reached inside it): resume starts at the next batch
+        checkpoint(epoch + 1, 0) if not done else checkpoint(epoch, bi + 1)
         if done:
             break
-    ck_cfg = cfg.get("callbacks", {}) or {}
-    mc = ck_cfg.get("model_checkpoint") if ck_cfg else None
-    if rank == 0 and mc is not None:
-        d = mc.get("dirpath", "checkpoints/")
-        os.makedirs(d, exist_ok=True)
-        save_checkpoint(os.path.join(d, "last.ckpt"), trainer, epoch)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
