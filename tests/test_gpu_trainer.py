@@ -12,6 +12,7 @@ clip + AdamW) under the reference's Lightning semantics (GPU only):
 * a torch.optim.AdamW state (a reference Lightning checkpoint's optimizer_states) continues
   exactly in FusedAdamW.
 """
+import copy
 import os
 import socket
 
@@ -113,11 +114,13 @@ def _ddp_worker(rank, world, port, precision, q):
         for step in range(3):
             tr.step(_dev(_batch(10 * step + rank, 4)))
             torch.cuda.synchronize()
-            grads.append((tr.flat.grad * tr.reducer.grad_scale).cpu())
+            grads.append((tr.flat.grad * tr.reducer.grad_scale).cpu().numpy())
             fired.append(tr.reducer.fired_in_backward)
             scales.append(tr.reducer.grad_scale)
+        # numpy, not tensors: torch's queue would share tensor storage through a file
+        # descriptor that dies with this process
         q.put((rank, dict(grads=grads, fired=fired, n_buckets=n_buckets, scales=scales,
-                          flat=tr.flat.flat.cpu())))
+                          flat=tr.flat.flat.cpu().numpy())))
     finally:
         dist.destroy_process_group()
 
@@ -142,6 +145,9 @@ def test_ddp_two_ranks_equals_single_process(precision):
         ref_grads.append(tr.flat.grad.cpu())
     ref_flat = tr.flat.flat.cpu()
     r0, r1 = res[0], res[1]
+    for r in (r0, r1):
+        r["flat"] = torch.from_numpy(r["flat"])
+        r["grads"] = [torch.from_numpy(g) for g in r["grads"]]
     assert r0["scales"] == [0.5] * 3 and r0["n_buckets"] > 4
     # step 0 learns the per-parameter contribution counts; afterwards every bucket is launched
     # from the backward's hooks / the fused wgrad notify, none left for finish()
@@ -176,7 +182,7 @@ def test_fused_adamw_continues_torch_adamw_state():
             p.grad = gr.clone()
         opt.step()
     mid = {k: v.clone() for k, v in ref.state_dict().items()}
-    sd = opt.state_dict()
+    sd = copy.deepcopy(opt.state_dict())  # state_dict() aliases the live moment tensors
     for p, gr in zip(ref.parameters(), fake[2]):
         p.grad = gr.clone()
     opt.step()
