@@ -188,7 +188,11 @@ class BertForMaskedLM(nn.Module):
         self.precision = precision
         self.dropout_rng = DF.DropoutRNG()
         self._lp_provider = None  # set by dna_amd.flat.FlatParams for a persistent bf16 copy
+        self._lpt_provider = None  # ... and for the transposed bf16 projection weights
         self._init_weights()
+        for m in self.modules():  # projection weights: keep a W^T copy for the data gradient
+            if isinstance(m, nn.Linear):
+                m.weight._dna_transpose = True
 
     # -- reference-compatible utilities ------------------------------------------------------
     def _init_weights(self):
@@ -229,6 +233,15 @@ class BertForMaskedLM(nn.Module):
             return self._lp_provider(p)
         return p.detach().to(torch.bfloat16)
 
+    def _lp_t(self, p: torch.Tensor):
+        """Transposed bf16 copy of projection weight `p` (None: the data gradient falls back)."""
+        if self.precision == "fp32" or self._lpt_provider is None:
+            return None
+        return self._lpt_provider(p)
+
+    def _linear(self, x, w, b=None):
+        return DF.linear(x, w, self._lp(w), b, w_lpt=self._lp_t(w))
+
     # -- the hot path ------------------------------------------------------------------------
     def mlm_logits(self, input_ids: torch.Tensor, index: MLMIndex) -> torch.Tensor:
         """Compact logits [M, V] of the masked rows (row-major over (b, s)), compute dtype."""
@@ -256,8 +269,7 @@ class BertForMaskedLM(nn.Module):
         L = len(self.bert.encoder.layer)
         for i, layer in enumerate(self.bert.encoder.layer):
             att = layer.attention
-            qkv = DF.linear(xin, att.self.Wqkv.weight, self._lp(att.self.Wqkv.weight),
-                            att.self.Wqkv.bias)
+            qkv = self._linear(xin, att.self.Wqkv.weight, att.self.Wqkv.bias)
             ctx = DF.alibi_attention(qkv, key_valid, slopes, b, S, H,
                                      bias_grad=att.self.Wqkv.bias is not None)
             res = x32
@@ -266,17 +278,16 @@ class BertForMaskedLM(nn.Module):
                 res = x32.index_select(0, index.subset_idx)
             n = ctx.shape[0]
             out = att.output
-            h = DF.linear(ctx, out.dense.weight, self._lp(out.dense.weight))
+            h = self._linear(ctx, out.dense.weight)
             seed, off = rng.take(n * cfg.hidden_size) if p_hidden else (0, 0)
             y32, yb = DF.FusedLayerNorm.apply(h, out.dense.bias, res, out.LayerNorm.weight,
                                               out.LayerNorm.bias, eps, 0, p_hidden, seed, off,
                                               True, bf16)
             mlp = layer.mlp
-            g = DF.linear(yb if bf16 else y32, mlp.gated_layers.weight,
-                          self._lp(mlp.gated_layers.weight))
+            g = self._linear(yb if bf16 else y32, mlp.gated_layers.weight)
             seed, off = rng.take(n * cfg.intermediate_size) if p_hidden else (0, 0)
             a = DF.GeGLU.apply(g, p_hidden, seed, off)
-            o = DF.linear(a, mlp.wo.weight, self._lp(mlp.wo.weight))
+            o = self._linear(a, mlp.wo.weight)
             x32, xb = DF.FusedLayerNorm.apply(o, mlp.wo.bias, y32, mlp.layernorm.weight,
                                               mlp.layernorm.bias, eps, 0, 0.0, 0, 0, True, bf16)
             xin = xb if bf16 else x32
@@ -284,11 +295,11 @@ class BertForMaskedLM(nn.Module):
             xin = xin.index_select(0, index.subset_idx)
         seq = xin.index_select(0, index.head_idx)
         tr = self.cls.predictions.transform
-        t = DF.linear(seq, tr.dense.weight, self._lp(tr.dense.weight))
+        t = self._linear(seq, tr.dense.weight)
         t32, tb = DF.FusedLayerNorm.apply(t, tr.dense.bias, None, tr.LayerNorm.weight,
                                           tr.LayerNorm.bias, 1e-12, 1, 0.0, 0, 0, not bf16, bf16)
         dec = self.cls.predictions.decoder
-        return DF.linear(tb if bf16 else t32, dec.weight, self._lp(dec.weight), dec.bias)
+        return self._linear(tb if bf16 else t32, dec.weight, dec.bias)
 
     def mlm_loss(self, input_ids, mask, index: MLMIndex, n_mask: Optional[int] = None,
                  n_unk_masked: Optional[int] = None):

@@ -27,6 +27,8 @@
 // weight (<= 9.4 MB, MALL-resident) streams.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace dna {
@@ -119,6 +121,8 @@ struct Args {
   int tilesM, tilesN, GM;
   int F;
   float p; uint32_t th; float ks; uint64_t seed, off;
+  int rot;                    // persistent kernel: rotate each block's K order (store spreading)
+  int dbg;                    // diagnostics (DNA_GEMM_DBG): 1 = stores dropped (OOB), 2 = no stores
 };
 
 __device__ __forceinline__ void tile_of(const Args& a, int& mt, int& nt) {
@@ -135,6 +139,39 @@ __device__ __forceinline__ void tile_of(const Args& a, int& mt, int& nt) {
 
 __device__ __forceinline__ void store_bf16x4(bf16* p, float v0, float v1, float v2, float v3) {
   *reinterpret_cast<bf16x4*>(p) = bf16x4{(bf16)v0, (bf16)v1, (bf16)v2, (bf16)v3};
+}
+
+
+// ---- branch-free epilogue I/O: raw buffer ops on a resource spanning one tile's rows
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+constexpr uint32_t kOOB = 0x7FFFFFF0u;  // past any tile resource: the access is dropped / reads 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void store_b64(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x4 v) {
+  const bf16x4 h = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), r, off, 0, 0);
+}
+__device__ __forceinline__ void store_b64h(__amdgpu_buffer_rsrc_t r, uint32_t off, bf16x4 h) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), r, off, 0, 0);
+}
+__device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void store_b128h(__amdgpu_buffer_rsrc_t r, uint32_t off, bf16x8 h) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), r, off, 0, 0);
+}
+__device__ __forceinline__ bf16x8 load_b128h(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ float g_zero4[4];  // stands in for a missing bias (zero-initialised device memory)
+// 4 bias columns starting at n (n % 4 == 0), zero past `limit` or without a bias; the load is
+// unconditional (pointer select), so no branch holds a load
+__device__ __forceinline__ f32x4 bias4(const float* bias, int n, int limit) {
+  const float* p = (bias != nullptr && n < limit) ? bias + n : g_zero4;
+  return *reinterpret_cast<const f32x4*>(p);
 }
 
 #define DNA_BARRIER()                         \
@@ -295,61 +332,86 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
   // ------------------------------------------------------------------ epilogue
   // acc[mq][nq][i][j] lane holds C[m][n .. n+3]:
   //   m = m0 + mq*128 + wr*64 + i*16 + (lane&15),  n = n0 + nq*128 + wc*32 + j*16 + 4*(lane>>4)
+  // Epilogues: every store is a raw buffer store through a resource covering exactly this tile's
+  // rows, and out-of-range lanes get an offset past its end (the hardware drops them), so no store
+  // sits under a branch; every global load (bias columns, the saved GeGLU input) is issued
+  // unconditionally ahead of the stores. A load under a divergent branch between two stores made
+  // the compiler wait `vmcnt(0)` before every store (32 serial memory round trips per tile).
   const int cq = 4 * (lane >> 4);
+  const int rows = min(a.M - m0, BM);
   if constexpr (EPI == EPI_BF16 || EPI == EPI_F32) {
+    constexpr int ES = EPI == EPI_BF16 ? 2 : 4;
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + nq * 128 + wc * 32 + j * 16 + cq;
+        const f32x4 bv = bias4(a.bias, n, a.N);
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[mq][nq][i][j] += bv;
+      }
+    char* base = reinterpret_cast<char*>(a.C) +
+                 ((EPI == EPI_F32 ? (size_t)blockIdx.y * a.M * a.ldc : 0) + (size_t)m0 * a.ldc) * ES;
+    const auto rs = out_rsrc(base, (uint32_t)((size_t)rows * a.ldc * ES));
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = m0 + mq * 128 + wr * 64 + i * 16 + (lane & 15);
-        if (m >= a.M) continue;
+        const int r = mq * 128 + wr * 64 + i * 16 + (lane & 15);
 #pragma unroll
         for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int n = n0 + nq * 128 + wc * 32 + j * 16 + cq;
-            if (n >= a.N) continue;
-            f32x4 v = acc[mq][nq][i][j];
-            if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + n);
-            if constexpr (EPI == EPI_BF16) {
-              store_bf16x4(reinterpret_cast<bf16*>(a.C) + (size_t)m * a.ldc + n, v[0], v[1], v[2], v[3]);
-            } else {
-              float* Cf = reinterpret_cast<float*>(a.C) + (size_t)blockIdx.y * a.M * a.ldc;
-              *reinterpret_cast<f32x4*>(Cf + (size_t)m * a.ldc + n) = v;
-            }
+            const uint32_t off = n < a.N ? (uint32_t)((r * a.ldc + n) * ES) : kOOB;
+            const f32x4 v = acc[mq][nq][i][j];
+            if constexpr (EPI == EPI_BF16) store_b64(rs, off, v);
+            else store_b128(rs, off, v);
           }
       }
   } else if constexpr (EPI == EPI_GEGLU) {
     // quadrant column nq=0 holds g1 columns, nq=1 the matching g2 columns
-    bf16* g = reinterpret_cast<bf16*>(a.C);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = n0 + wc * 32 + j * 16 + cq;
+      const f32x4 b1 = bias4(a.bias, c, a.F), b2 = bias4(a.bias ? a.bias + a.F : nullptr, c, a.F);
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[mq][0][i][j] += b1;
+          acc[mq][1][i][j] += b2;
+        }
+    }
+    const auto rg = out_rsrc(reinterpret_cast<bf16*>(a.C) + (size_t)m0 * 2 * a.F,
+                             (uint32_t)((size_t)rows * 2 * a.F * 2));
+    const auto ra = out_rsrc(a.aux + (size_t)m0 * a.F, (uint32_t)((size_t)rows * a.F * 2));
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = m0 + mq * 128 + wr * 64 + i * 16 + (lane & 15);
-        if (m >= a.M) continue;
+        const int r = mq * 128 + wr * 64 + i * 16 + (lane & 15);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int c = n0 + wc * 32 + j * 16 + cq;  // a column (0..F)
-          f32x4 v1 = acc[mq][0][i][j], v2 = acc[mq][1][i][j];
-          if (a.bias) {
-            v1 += *reinterpret_cast<const f32x4*>(a.bias + c);
-            v2 += *reinterpret_cast<const f32x4*>(a.bias + a.F + c);
-          }
+          const f32x4 v1 = acc[mq][0][i][j], v2 = acc[mq][1][i][j];
           const bf16x4 h1 = bf16x4{(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
           const bf16x4 h2 = bf16x4{(bf16)v2[0], (bf16)v2[1], (bf16)v2[2], (bf16)v2[3]};
-          *reinterpret_cast<bf16x4*>(g + (size_t)m * 2 * a.F + c) = h1;
-          *reinterpret_cast<bf16x4*>(g + (size_t)m * 2 * a.F + a.F + c) = h2;
-          const size_t e = (size_t)m * a.F + c;
+          const uint32_t og = (uint32_t)((r * 2 * a.F + c) * 2);
+          store_b64h(rg, og, h1);
+          store_b64h(rg, og + a.F * 2, h2);
+          const size_t e = (size_t)(m0 + r) * a.F + c;
           // c % 4 == 0: this lane's 4 columns are one half of a keep8 group
           const uint32_t keep = a.p > 0.f ? (dropout_keep8(a.seed, a.off, e >> 3, a.th) >> (e & 4)) & 0xFu : 0xFu;
-          float o[4];
+          f32x4 o;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float x = gelu_erf((float)h1[q]) * (float)h2[q];
             o[q] = a.p > 0.f ? (((keep >> q) & 1) ? x * a.ks : 0.f) : x;
           }
-          store_bf16x4(a.aux + e, o[0], o[1], o[2], o[3]);
+          store_b64(ra, (uint32_t)((r * a.F + c) * 2), o);
         }
       }
   } else {  // EPI_GEGLU_BWD
@@ -373,34 +435,389 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
           }
       }
     __syncthreads();
-    for (int it = 0; it < 16; ++it) {
-      const int idx = it * NTHR + tid;
-      const int r = idx >> 5, c = idx & 31;
-      const int m = m0 + r, n = n0 + c * 8;
-      if (m >= a.M || n >= a.F) continue;
-      const bf16x8 d = *reinterpret_cast<const bf16x8*>(T + r * 512 + ((c ^ (r & 15)) << 4));
-      const bf16* grow = a.g + (size_t)m * 2 * a.F;
-      const bf16x8 g1 = *reinterpret_cast<const bf16x8*>(grow + n);
-      const bf16x8 g2 = *reinterpret_cast<const bf16x8*>(grow + a.F + n);
-      const size_t e = (size_t)m * a.F + n;
-      uint32_t keep = 0xFFu;
-      if (a.p > 0.f) keep = dropout_keep8(a.seed, a.off, e >> 3, a.th);
-      bf16x8 o1, o2;
+    const auto rgi = out_rsrc(const_cast<bf16*>(a.g) + (size_t)m0 * 2 * a.F,
+                              (uint32_t)((size_t)rows * 2 * a.F * 2));
+    const auto rdg = out_rsrc(a.aux + (size_t)m0 * 2 * a.F, (uint32_t)((size_t)rows * 2 * a.F * 2));
+    constexpr int GB = 4;  // chunks whose g loads are in flight together
+    for (int it0 = 0; it0 < 16; it0 += GB) {
+      bf16x8 g1[GB], g2[GB];
+      uint32_t offs[GB];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float dd = (float)d[q];
-        if (a.p > 0.f) dd = ((keep >> q) & 1) ? dd * a.ks : 0.f;
-        const float x = (float)g1[q];
-        float ge, dge;
-        gelu_erf_and_grad(x, ge, dge);
-        o1[q] = (bf16)(dd * (float)g2[q] * dge);
-        o2[q] = (bf16)(dd * ge);
+      for (int u = 0; u < GB; ++u) {
+        const int idx = (it0 + u) * NTHR + tid;
+        const int r = idx >> 5, n = n0 + (idx & 31) * 8;
+        offs[u] = n < a.F ? (uint32_t)((r * 2 * a.F + n) * 2) : kOOB;
+        g1[u] = load_b128h(rgi, offs[u]);
+        g2[u] = load_b128h(rgi, offs[u] + a.F * 2);
       }
-      bf16* dg = a.aux + (size_t)m * 2 * a.F;
-      *reinterpret_cast<bf16x8*>(dg + n) = o1;
-      *reinterpret_cast<bf16x8*>(dg + a.F + n) = o2;
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        const int idx = (it0 + u) * NTHR + tid;
+        const int r = idx >> 5, c = idx & 31;
+        const int m = m0 + r, n = n0 + c * 8;
+        const bf16x8 d = *reinterpret_cast<const bf16x8*>(T + r * 512 + ((c ^ (r & 15)) << 4));
+        const size_t e = (size_t)m * a.F + n;
+        uint32_t keep = 0xFFu;
+        if (a.p > 0.f) keep = dropout_keep8(a.seed, a.off, e >> 3, a.th);
+        bf16x8 o1, o2;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float dd = (float)d[q];
+          if (a.p > 0.f) dd = ((keep >> q) & 1) ? dd * a.ks : 0.f;
+          const float x = (float)g1[u][q];
+          float ge, dge;
+          gelu_erf_and_grad(x, ge, dge);
+          o1[q] = (bf16)(dd * (float)g2[u][q] * dge);
+          o2[q] = (bf16)(dd * ge);
+        }
+        store_b128h(rdg, offs[u], o1);
+        store_b128h(rdg, offs[u] + a.F * 2, o2);
+      }
     }
   }
+}
+
+// ------------------------------------------------------------------ persistent K-major kernel
+// y[M,N] = x[M,K] . W[N,K]^T (+ bias) with both operands K-major: the forward projections, and
+// the data gradients through the transposed bf16 weight copy (dx = dy . W = dy . (W^T)^T).
+// One 512-thread block per CU walks its units (256x256 output tiles) u = i*G + L(block) with the
+// SAME 4-phase half-tile pipeline as gemm_kernel, but the K-steps of consecutive units form one
+// continuous stream: the stages of unit i+1's first two K-steps are in flight while unit i ends,
+// and unit i's epilogue (bias from LDS, branch-free buffer stores) is issued while they land. The
+// per-tile cost of the non-persistent kernel (pipeline fill from memory, block turnover, store
+// tail: ~13 us per tile at K = 768, i.e. 8 K-steps of work) is gone.
+// vmcnt accounting: the epilogue's S stores sit in the VMEM queue between the stages of the next
+// unit's K-steps 0/1 and 1/2, so the 4 phases of a unit's first K-step wait vmcnt(8 + S) instead
+// of vmcnt(8) (the stores themselves never have to complete before the wave moves on); from the
+// second K-step on the stores are older than every wait target and retire with it.
+constexpr int BIAS_LDS = 32 * 1024;  // bias row staged once per block (N <= 8192 floats)
+
+__host__ __device__ constexpr int waitcnt_imm(int vm) {  // gfx9 s_waitcnt: vmcnt=vm, others no-wait
+  return (vm & 0xF) | ((vm >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+}
+
+template <int EPI>
+__device__ __forceinline__ void unit_tile(const Args& a, int u, int& m0, int& n0) {
+  const int width = a.GM * a.tilesN;
+  const int grp = u / width, first = grp * a.GM;
+  const int gsz = min(a.tilesM - first, a.GM);
+  const int w = u - grp * width;
+  m0 = (first + w % gsz) * BM;
+  n0 = (w / gsz) * (EPI == EPI_GEGLU ? BN / 2 : BN);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
+  static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU, "persistent kernel: bf16 / GeGLU epilogues");
+  constexpr int S = EPI == EPI_BF16 ? 32 : 48;  // VMEM instructions of one epilogue (stores)
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int L = (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);  // blocks of one XCD: consecutive units
+  const int U = a.tilesM * a.tilesN;
+  const int nb = L < U ? (U - L + G - 1) / G : 0;
+  if (nb == 0) return;
+  const int KT = a.K / BK;
+  const int V = nb * KT;
+  float* bias_lds = reinterpret_cast<float*>(smem + LDS_BYTES);
+  const int nbias = EPI == EPI_GEGLU ? 2 * a.F : a.N;
+  for (int c = tid * 4; c < nbias; c += NTHR * 4)
+    *reinterpret_cast<f32x4*>(bias_lds + c) =
+        a.bias ? *reinterpret_cast<const f32x4*>(a.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  // Operands through buffer resources over the whole matrices: per-lane offsets are fixed for the
+  // kernel's life (2 VGPRs per operand), tile / K position is the scalar soffset, and rows past M
+  // read as zeros (bounds check) -- no per-lane clamping, no 64-bit addresses.
+  const int NB = EPI == EPI_GEGLU ? 2 * a.F : a.N;  // rows of the weight operand
+  const auto rA = out_rsrc(a.A, (uint32_t)((size_t)a.M * a.lda * 2));
+  const auto rB = out_rsrc(a.B, (uint32_t)((size_t)NB * a.ldb * 2));
+  uint32_t voA[2], voB[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int lr = p * 64 + wave * 8 + (lane >> 3);
+    const int ch = ((lane & 7) ^ kswz(lr)) << 4;
+    voA[p] = (uint32_t)(lr * a.lda * 2 + ch);
+    voB[p] = (uint32_t)(lr * a.ldb * 2 + ch);
+  }
+
+  // cursors over the virtual K-step stream: c0 = step being computed, c1/c2 = one / two ahead
+  struct Cur { int i, kt, m0, n0; };
+  auto cur_at = [&](int i) {
+    Cur c;
+    c.i = i;
+    c.kt = 0;
+    unit_tile<EPI>(a, min(i, nb - 1) * G + L, c.m0, c.n0);
+    return c;
+  };
+  auto advance = [&](Cur& c) {
+    if (++c.kt == KT) c = cur_at(c.i + 1);
+  };
+  auto img = [&](int v, int h) { return smem + ((v & 1) * 4 + h) * HALF; };
+  // stage half-tile h of the K-step at cursor c (virtual step v); steps past the end re-load the
+  // last unit's data into a buffer no one reads again (keeps every vmcnt count uniform)
+  // K-step order within a unit is rotated per block (k = (kt + rot) mod KT): the blocks' store
+  // bursts (one per unit) then fall on different steps instead of hitting memory all at once
+  const int rot = a.rot ? (L * 5) % KT : 0;
+  auto stage = [&](const Cur& c, int v, int h) {
+    int kk = (c.i < nb ? c.kt : KT - 1) + rot;
+    kk = kk >= KT ? kk - KT : kk;
+    const int k0 = kk * BK;
+    char* d = img(v, h);
+    int row0;
+    if (h < 2) row0 = c.m0 + h * 128;
+    else if constexpr (EPI == EPI_GEGLU) row0 = (h - 2) * a.F + c.n0;
+    else row0 = c.n0 + (h - 2) * 128;
+    const int ld = h < 2 ? a.lda : a.ldb;
+    const int soff = __builtin_amdgcn_readfirstlane((row0 * ld + k0) * 2);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rA : rB, (lds_t*)(d + (p * 64 + wave * 8) * 128),
+                                               16, h < 2 ? voA[p] : voB[p], soff, 0, 0);
+  };
+
+  f32x4 acc[2][2][4][2];  // [mq][nq][i][j]
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[q][r][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  auto readA = [&](int v, int mq) {
+    const char* im = img(v, mq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_k(im, wr * 64 + i * 16 + (lane & 15), kk * 4 + (lane >> 4));
+  };
+  auto readB = [&](int v, int nq, bf16x8 (&bf)[2][2]) {
+    const char* im = img(v, 2 + nq);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = read_k(im, wc * 32 + j * 16 + (lane & 15), kk * 4 + (lane >> 4));
+  };
+  auto mma = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = mfma(bf[j][kk], af[i][kk], acc[mq][nq][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // epilogue stores: lane part of the offset fixed, tile row block in soffset, column block in
+  // the immediate; rows past M fall outside the resource and are dropped
+  const int cq = 4 * (lane >> 4);
+  const int ldo = EPI == EPI_GEGLU ? 2 * a.F : a.ldc;
+  const auto rC = out_rsrc(a.C, (uint32_t)((size_t)a.M * ldo * 2));
+  const uint32_t voC = (uint32_t)(((wr * 64 + (lane & 15)) * ldo + wc * 32 + cq) * 2);
+  auto epilogue = [&](const Cur& c) {
+    if constexpr (EPI == EPI_BF16) {
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + j * 16 + cq);
+#pragma unroll
+          for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[mq][nq][i][j] += bv;
+        }
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int soff = __builtin_amdgcn_readfirstlane(((c.m0 + mq * 128 + i * 16) * ldo + c.n0) * 2);
+#pragma unroll
+          for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const f32x4 v = acc[mq][nq][i][j];
+              const bf16x4 h = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rC,
+                                                    voC + (nq * 128 + j * 16) * 2, soff, 0);
+            }
+        }
+    } else {  // EPI_GEGLU: quadrant column nq=0 holds g1 columns, nq=1 the matching g2 columns
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = c.n0 + wc * 32 + j * 16 + cq;
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias_lds + col);
+        const f32x4 b2 = *reinterpret_cast<const f32x4*>(bias_lds + a.F + col);
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            acc[mq][0][i][j] += b1;
+            acc[mq][1][i][j] += b2;
+          }
+      }
+      const auto ra = out_rsrc(a.aux, (uint32_t)((size_t)a.M * a.F * 2));
+      const uint32_t voa = (uint32_t)(((wr * 64 + (lane & 15)) * a.F + wc * 32 + cq) * 2);
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = c.m0 + mq * 128 + i * 16;
+          const int sg = __builtin_amdgcn_readfirstlane((row * ldo + c.n0) * 2);
+          const int sa = __builtin_amdgcn_readfirstlane((row * a.F + c.n0) * 2);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const f32x4 v1 = acc[mq][0][i][j], v2 = acc[mq][1][i][j];
+            const bf16x4 h1 = bf16x4{(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+            const bf16x4 h2 = bf16x4{(bf16)v2[0], (bf16)v2[1], (bf16)v2[2], (bf16)v2[3]};
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h1), rC, voC + j * 32, sg, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h2), rC,
+                                                  voC + j * 32 + a.F * 2, sg, 0);
+            const int col = c.n0 + wc * 32 + j * 16 + cq;
+            const size_t e = (size_t)(row + wr * 64 + (lane & 15)) * a.F + col;
+            const uint32_t keep =
+                a.p > 0.f ? (dropout_keep8(a.seed, a.off, e >> 3, a.th) >> (e & 4)) & 0xFu : 0xFu;
+            f32x4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float x = gelu_erf((float)h1[q]) * (float)h2[q];
+              o[q] = a.p > 0.f ? (((keep >> q) & 1) ? x * a.ks : 0.f) : x;
+            }
+            const bf16x4 ho = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ho), ra, voa + j * 32, sa, 0);
+          }
+        }
+    }
+  };
+
+  // BF16: a quadrant (mq, nq) is final right after its MFMAs in a unit's last K-step, so it is
+  // stored there (bias from LDS), overlapping the remaining phases. For each (row block i) the
+  // lane's two 4-column groups j = 0 / 1 are exchanged with v_permlane16_swap so that every
+  // lane holds 8 consecutive columns: one 16-B store instead of two 8-B ones (the store tail is
+  // issue-bound per instruction). After the swap, column group cg = lane >> 4 holds columns
+  // {0, 16, 8, 24}[cg] .. +7 of the wave's 32-column slab.
+  const uint32_t voQ = (uint32_t)(((wr * 64 + (lane & 15)) * a.ldc + wc * 32 +
+                                   (((lane >> 4) & 1) << 4) + (((lane >> 4) & 2) << 2)) * 2);
+  auto store_quadrant = [&](const Cur& c, int mq, int nq) {
+    const f32x4 bj0 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + cq);
+    const f32x4 bj1 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + 16 + cq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 v0 = acc[mq][nq][i][0] + bj0, v1 = acc[mq][nq][i][1] + bj1;
+      u32x2 h0 = __builtin_bit_cast(u32x2, bf16x4{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]});
+      u32x2 h1 = __builtin_bit_cast(u32x2, bf16x4{(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]});
+      const auto sx = __builtin_amdgcn_permlane16_swap(h0[0], h1[0], false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(h0[1], h1[1], false, false);
+      const u32x4 o = u32x4{sx[0], sy[0], sx[1], sy[1]};
+      const int soff = __builtin_amdgcn_readfirstlane(((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
+      if (a.dbg == 0) __builtin_amdgcn_raw_buffer_store_b128(o, rC, voQ, soff, 0);
+      else if (a.dbg == 1) __builtin_amdgcn_raw_buffer_store_b128(o, rC, kOOB, 0, 0);
+      else asm volatile("" :: "v"(o));
+      acc[mq][nq][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[mq][nq][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  Cur c0 = cur_at(0), c1 = c0, c2 = c0;
+  advance(c1);
+  advance(c2);
+  advance(c2);
+  // prologue: all four halves of step 0, the A_0 / B_0 halves of step 1
+  stage(c0, 0, 0);
+  stage(c0, 0, 2);
+  stage(c0, 0, 3);
+  stage(c0, 0, 1);
+  stage(c1, 1, 0);
+  stage(c1, 1, 2);
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
+  DNA_BARRIER();
+  if (wr == 1) DNA_BARRIER();  // stagger: waves 4-7 one barrier behind
+
+  // One copy of the K-step body; the wait immediates depend on the step's role (a scalar branch
+  // around each s_waitcnt, so the MFMA code and its accumulator registers are shared):
+  //   role 0  ordinary step: vmcnt(8) (4 half-tiles = 8 LDS-DMA pieces stay in flight)
+  //   role 1  a unit's last step (BF16): quadrant q's QS stores are issued after phase q's MFMAs,
+  //           so phase p's wait also leaves the p * QS stores issued since phase 0 in flight
+  //   role 2  a unit's first step after an epilogue: the stores issued behind the half-tiles it
+  //           waits for stay in flight -- BF16 (4 - p) * QS, GeGLU (epilogue after the last step) S
+  constexpr int QS = 4;  // 16-B stores per quadrant and lane (BF16)
+  auto wait_vm = [&](auto phase, int role) {
+    constexpr int p = decltype(phase)::value;
+    constexpr int w1 = EPI == EPI_BF16 ? 8 + p * QS : 8;
+    constexpr int w2 = EPI == EPI_BF16 ? 8 + (4 - p) * QS : 8 + S;
+    if (role == 0) __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
+    else if (role == 1) __builtin_amdgcn_s_waitcnt(waitcnt_imm(w1));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_imm(w2));
+  };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  using P2 = std::integral_constant<int, 2>;
+  using P3 = std::integral_constant<int, 3>;
+  auto kstep = [&](int v, int role) {
+    const bool st = EPI == EPI_BF16 && role == 1;
+    // phase 0: quadrant (0,0)
+    stage(c1, v + 1, 3);
+    wait_vm(P0{}, role);
+    readA(v, 0);
+    readB(v, 0, bf0);
+    DNA_BARRIER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, 0, bf0);
+    if (st) store_quadrant(c0, 0, 0);
+    DNA_BARRIER();
+    // phase 1: quadrant (0,1)
+    stage(c1, v + 1, 1);
+    wait_vm(P1{}, role);
+    readB(v, 1, bf1);
+    DNA_BARRIER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, 1, bf1);
+    if (st) store_quadrant(c0, 0, 1);
+    DNA_BARRIER();
+    // phase 2: quadrant (1,1)
+    stage(c2, v + 2, 0);
+    wait_vm(P2{}, role);
+    readA(v, 1);
+    DNA_BARRIER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1, 1, bf1);
+    if (st) store_quadrant(c0, 1, 1);
+    DNA_BARRIER();
+    // phase 3: quadrant (1,0)
+    stage(c2, v + 2, 2);
+    wait_vm(P3{}, role);
+    DNA_BARRIER();
+    mma(1, 0, bf0);
+    if (st) store_quadrant(c0, 1, 0);
+    DNA_BARRIER();
+  };
+
+  int v = 0;
+  for (int i = 0; i < nb; ++i) {
+    for (int kt = 0; kt < KT; ++kt, ++v) {
+      const int role = (kt == KT - 1 && EPI == EPI_BF16) ? 1 : (kt == 0 && i > 0) ? 2 : 0;
+      kstep(v, role);
+      advance(c1);
+      advance(c2);
+    }
+    if constexpr (EPI == EPI_GEGLU) {
+      epilogue(c0);
+      zero_acc();
+    }
+    c0 = cur_at(i + 1);
+  }
+  if (wr == 0) DNA_BARRIER();  // re-align the two wave groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the block
 }
 
 template <bool AK, bool BKM, int EPI>
@@ -412,6 +829,47 @@ int launch(Args& a, int splits, hipStream_t s, const char* name) {
   if (a.GM <= 0) a.GM = 4;
   dim3 grid(a.tilesM * a.tilesN, splits);
   hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI>), grid, dim3(NTHR), 0, s, a);
+  DNA_LAUNCH_CHECK(name);
+  return DNA_OK;
+}
+
+
+inline int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+inline bool persistent_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("DNA_GEMM_P");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
+
+template <int EPI>
+int launchp(Args& a, hipStream_t s, const char* name) {
+  a.tilesM = (a.M + BM - 1) / BM;
+  const int nper = (EPI == EPI_GEGLU ? BN / 2 : BN);
+  a.tilesN = (a.N + nper - 1) / nper;
+  if (const char* e = getenv("DNA_GEMM_GM")) a.GM = atoi(e);
+  if (a.GM <= 0) a.GM = 8;
+  const int U = a.tilesM * a.tilesN;
+  int G = num_cus();
+  if (const char* e = getenv("DNA_GEMM_GRID")) G = atoi(e);
+  G = U < G ? U : (G & ~7);
+  a.rot = 0;
+  if (const char* e = getenv("DNA_GEMM_ROT")) a.rot = atoi(e);
+  a.dbg = 0;
+  if (const char* e = getenv("DNA_GEMM_DBG")) a.dbg = atoi(e);
+  hipLaunchKernelGGL((gemmp_kernel<EPI>), dim3(G), dim3(NTHR), 0, s, a);
   DNA_LAUNCH_CHECK(name);
   return DNA_OK;
 }
@@ -439,6 +897,9 @@ extern "C" int dna_linear_fwd(const void* x, const void* w, const float* bias, i
   a.B = (const bf16*)w; a.ldb = K;
   a.C = y; a.ldc = N; a.bias = bias;
   a.M = M; a.N = N; a.K = K; a.ksplit = K;
+  if (persistent_enabled() && N <= BIAS_LDS / 4 && N % BN == 0 && K >= 2 * BK &&
+      (size_t)M * (K > N ? K : N) * 2 < (1ull << 31) && (size_t)N * K * 2 < (1ull << 31))
+    return launchp<EPI_BF16>(a, as_stream(stream), "dna_linear_fwd");
   return launch<true, true, EPI_BF16>(a, 1, as_stream(stream), "dna_linear_fwd");
 }
 
@@ -486,6 +947,9 @@ extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* b
   a.M = M; a.N = F; a.K = K; a.ksplit = K; a.F = F;
   a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed; a.off = offset;
+  if (persistent_enabled() && 2 * F <= BIAS_LDS / 4 &&
+      (size_t)M * (K > 2 * F ? K : 2 * F) * 2 < (1ull << 31))
+    return launchp<EPI_GEGLU>(a, as_stream(stream), "dna_geglu_linear_fwd");
   return launch<true, true, EPI_GEGLU>(a, 1, as_stream(stream), "dna_geglu_linear_fwd");
 }
 

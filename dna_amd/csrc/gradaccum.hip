@@ -210,3 +210,45 @@ extern "C" int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_i
   DNA_LAUNCH_CHECK("dna_embed_grad_segsum");
   return DNA_OK;
 }
+
+// bf16 transpose dst[cols][rows] = src[rows][cols]: the transposed weight copy that lets the data
+// gradient dx = dy . W run on the K-major persistent GEMM (dx = dy . (W^T)^T). 64x64 tiles through
+// LDS (row stride padded by 8 elements: the transposed 8-byte reads land on distinct banks),
+// 16-B loads and stores, 256 threads.
+namespace dna {
+namespace gacc {
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ src, int rows,
+                                                             int cols, bf16* __restrict__ dst) {
+  __shared__ bf16 t[64][72];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64, tid = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = p * 32 + (tid >> 3), c = (tid & 7) * 8;
+    bf16x8 v = {};
+    if (r0 + r < rows && c0 + c < cols) v = *reinterpret_cast<const bf16x8*>(src + (size_t)(r0 + r) * cols + c0 + c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[r][c + q] = v[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = p * 32 + (tid >> 3), r = (tid & 7) * 8;  // output row c (a source column)
+    bf16x8 v;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = t[r + q][c];
+    if (c0 + c < cols && r0 + r < rows) *reinterpret_cast<bf16x8*>(dst + (size_t)(c0 + c) * rows + r0 + r) = v;
+  }
+}
+}  // namespace gacc
+}  // namespace dna
+
+extern "C" int dna_transpose_bf16(const void* src, int rows, int cols, void* dst, void* stream) {
+  DNA_CHECK_ARG(src && dst && src != dst, "dna_transpose_bf16: bad pointers");
+  DNA_CHECK_ARG(rows > 0 && cols > 0 && rows % 8 == 0 && cols % 8 == 0,
+                "dna_transpose_bf16: rows and cols must be positive multiples of 8 (%d x %d)", rows, cols);
+  dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  hipLaunchKernelGGL(gacc::transpose_bf16_kernel, grid, dim3(256), 0, as_stream(stream),
+                     (const bf16*)src, rows, cols, (bf16*)dst);
+  DNA_LAUNCH_CHECK("dna_transpose_bf16");
+  return DNA_OK;
+}

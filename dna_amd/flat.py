@@ -39,11 +39,19 @@ class FlatParams:
                 p.grad = self.grad[o:o + n].view(shape)
                 self._index[id(p)] = (o, n, shape)
         self.shadow = None
+        # transposed bf16 copies of the projection weights (parameters flagged `_dna_transpose`
+        # by the model): the data gradient dx = dy . W runs as a K-major GEMM on W^T
+        self.transposed = [p for p in params if getattr(p, "_dna_transpose", False) and p.dim() == 2]
+        self.shadow_t = None
         if shadow_dtype is not None:
             self.shadow = torch.empty(off, dtype=shadow_dtype, device=device)
+            if self.transposed and self.shadow.is_cuda and shadow_dtype == torch.bfloat16:
+                self.shadow_t = torch.empty(off, dtype=shadow_dtype, device=device)
             self.refresh_shadow()
         if hasattr(module, "_lp_provider"):
             module._lp_provider = self.lp if self.shadow is not None else None
+        if hasattr(module, "_lpt_provider"):
+            module._lpt_provider = self.lpt if self.shadow_t is not None else None
 
     def slice_of(self, p):
         return self._index[id(p)]
@@ -52,11 +60,28 @@ class FlatParams:
         o, n, shape = self._index[id(p)]
         return self.shadow[o:o + n].view(shape)
 
+    def lpt(self, p):
+        """Transposed bf16 copy [in, out] of a flagged 2-D weight [out, in]."""
+        o, n, shape = self._index[id(p)]
+        return self.shadow_t[o:o + n].view(shape[1], shape[0])
+
     @torch.no_grad()
     def refresh_shadow(self):
         """Re-derive the bf16 copy after any parameter change made outside FusedAdamW."""
         if self.shadow is not None:
             self.shadow.copy_(self.flat)
+            self.refresh_transposed()
+
+    def refresh_transposed(self):
+        """W^T bf16 copies from the bf16 shadow (after every optimizer step: FusedAdamW calls it)."""
+        if self.shadow_t is None:
+            return
+        from . import _native as N
+        st = N.stream_ptr(self.shadow.device)
+        for p in self.transposed:
+            o, n, (r, c) = self._index[id(p)]
+            N.call("dna_transpose_bf16", self.shadow[o:o + n].data_ptr(), r, c,
+                   self.shadow_t[o:o + n].data_ptr(), st)
 
     def zero_grad(self):
         self.grad.zero_()

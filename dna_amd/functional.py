@@ -1,7 +1,8 @@
 """Autograd Functions over the dna_amd C ABI (HIP kernels on the current torch stream).
 
-Each Function is one fused HIP op with a hand-written backward; GEMMs are the only work left to
-the vendor library (hipBLASLt through torch.mm), with fp32 weight-gradient outputs.
+Each Function is one fused HIP op with a hand-written backward; the forward and data-gradient
+GEMMs run the MFMA kernels of csrc/gemm.hip, the fp32 weight gradients (split-K) are the only
+work left to the vendor library (hipBLASLt through torch.bmm).
 No CPU fallback: every op raises if the native library is missing or a tensor is not on a GPU.
 """
 import math
@@ -310,24 +311,50 @@ class MaskedCrossEntropy(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------------- GEMM
+def _gemm_impl():
+    """"hip" (default): forward and data-gradient GEMMs on csrc/gemm.hip; "torch": hipBLASLt
+    through torch.mm (A/B switch, DNA_GEMM_IMPL)."""
+    return os.environ.get("DNA_GEMM_IMPL", "hip")
+
+
+def _hip_gemm_ok(x, w_lp, n_out, k_red):
+    return (x.dtype == torch.bfloat16 and w_lp.dtype == torch.bfloat16 and x.is_cuda
+            and k_red % 64 == 0 and n_out % 8 == 0 and _gemm_impl() == "hip")
+
+
+def _hip_linear(x, w_nk, bias):
+    """y[M, N] = x[M, K] . w_nk[N, K]^T (+ fp32 bias): the persistent MFMA GEMM (dna_linear_fwd)."""
+    x = x.contiguous()
+    M, K = x.shape
+    Nn = w_nk.shape[0]
+    y = torch.empty(M, Nn, device=x.device, dtype=torch.bfloat16)
+    N.call("dna_linear_fwd", x.data_ptr(), w_nk.data_ptr(), _p(bias), M, Nn, K, y.data_ptr(),
+           N.stream_ptr())
+    return y
+
+
 class Linear(torch.autograd.Function):
     """y = x @ w_lp^T (+ b): forward and dgrad on the compute dtype copy `w_lp` of the fp32
-    master weight `w`; wgrad produced directly in fp32 (hipBLASLt, out_dtype=float32)."""
+    master weight `w` -- bf16: the hand-written MFMA kernel (csrc/gemm.hip), the data gradient
+    on the transposed copy `w_lpt` (dx = dy . w = dy . (w^T)^T, both operands K-major); wgrad
+    produced directly in fp32 (hipBLASLt split-K, out_dtype=float32)."""
 
     @staticmethod
-    def forward(ctx, x, w, w_lp, b):
-        ctx.save_for_backward(x, w_lp)
+    def forward(ctx, x, w, w_lp, b, w_lpt):
+        ctx.save_for_backward(x, w_lp, w_lpt)
         ctx.weight = w
         ctx.has_b = b is not None
         flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
         with _timed("gemm", flops):
+            if _hip_gemm_ok(x, w_lp, w_lp.shape[0], w_lp.shape[1]):
+                return _hip_linear(x, w_lp, b if (b is None or b.dtype == torch.float32) else b.float())
             if b is not None:
                 return torch.addmm(b.to(x.dtype), x, w_lp.t())
             return torch.mm(x, w_lp.t())
 
     @staticmethod
     def backward(ctx, dy):
-        x, w_lp = ctx.saved_tensors
+        x, w_lp, w_lpt = ctx.saved_tensors
         colsum = getattr(dy, "_dna_colsum", None)
         dy = dy.contiguous()
         if colsum is not None:
@@ -336,7 +363,10 @@ class Linear(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             with _timed("gemm", flops):
-                dx = torch.mm(dy, w_lp)
+                if w_lpt is not None and _hip_gemm_ok(dy, w_lpt, w_lpt.shape[0], w_lpt.shape[1]):
+                    dx = _hip_linear(dy, w_lpt, None)
+                else:
+                    dx = torch.mm(dy, w_lp)
         w = ctx.weight
         direct = getattr(w, "_dna_direct", False) and w.grad is not None and x.dtype != torch.float32
         side = _side_stream() if direct else None
@@ -368,7 +398,7 @@ class Linear(torch.autograd.Function):
             db = getattr(dy, "_dna_colsum", None)  # fused upstream (AlibiAttention.backward)
             if db is None:
                 db = dy.sum(0, dtype=torch.float32)
-        return dx, dw, None, db
+        return dx, dw, None, db, None
 
 
 # ------------------------------------------------------------------ weight-gradient side stream
@@ -457,5 +487,5 @@ def wgrad_accumulate(dy, x, grad):
     N.call("dna_sum_slices_accum", parts.data_ptr(), s, m * n, grad.data_ptr(), N.stream_ptr())
 
 
-def linear(x, w, w_lp, b=None):
-    return Linear.apply(x, w, w_lp if w_lp is not None else w, b)
+def linear(x, w, w_lp, b=None, w_lpt=None):
+    return Linear.apply(x, w, w_lp if w_lp is not None else w, b, w_lpt)

@@ -52,6 +52,7 @@ class FusedAdamW:
                g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self.step_count,
                self._sumsq.data_ptr() if clip else None,
                float(self.max_grad_norm or 0.0), float(grad_scale), N.stream_ptr())
+        self.flat.refresh_transposed()
 
     def zero_grad(self, set_to_none=False):
         self.flat.zero_grad()

@@ -165,6 +165,11 @@ int dna_linear_fwd(const void* x, const void* w, const float* bias, int M, int N
 int dna_linear_dgrad(const void* dy, const void* w, int M, int N, int K, void* dx, void* stream);
 int dna_linear_wgrad(const void* dy, const void* x, int M, int N, int K, int splits,
                      float* partials, void* stream);
+/* dst[cols][rows] = src[rows][cols] (bf16; rows, cols % 8 == 0): the transposed weight copy kept
+ * beside the bf16 weights, so the data gradient dx = dy . w runs as
+ * dna_linear_fwd(dy, w^T, NULL, M, K, N, dx) on both-operands-K-major MFMA tiles (replaces the
+ * dgrad half of torch.nn.Linear's autograd backward, bert_layers.py:158/:214/:292/:297/:560). */
+int dna_transpose_bf16(const void* src, int rows, int cols, void* dst, void* stream);
 /* gated_layers + GeGLU + dropout in one launch (bert_layers.py:292-296):
  *   g[M, 2F] = x[M,K] . wg^T + bias (bias fp32 [2F] or NULL),
  *   out[M, F] = dropout(gelu_erf(g[:, :F]) * g[:, F:])   -- same Philox mask as dna_geglu_fwd.
