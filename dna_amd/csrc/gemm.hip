@@ -496,6 +496,13 @@ __host__ __device__ constexpr int waitcnt_imm(int vm) {  // gfx9 s_waitcnt: vmcn
   return (vm & 0xF) | ((vm >> 4) << 14) | (0x7 << 4) | (0xF << 8);
 }
 
+// bijective blockIdx -> unit-order remap (blocks are dispatched to XCDs round-robin, b % 8): the
+// blocks of one XCD get consecutive indices, for any grid size
+__device__ __forceinline__ int xcd_remap(int b, int G) {
+  const int xcd = b & 7, q = G >> 3, r = G & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 template <int EPI>
 __device__ __forceinline__ void unit_tile(const Args& a, int u, int& m0, int& n0) {
   const int width = a.GM * a.tilesN;
@@ -515,7 +522,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int G = gridDim.x, b = blockIdx.x;
-  const int L = (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);  // blocks of one XCD: consecutive units
+  const int L = xcd_remap(b, G);  // blocks of one XCD: consecutive units
   const int U = a.tilesM * a.tilesN;
   const int nb = L < U ? (U - L + G - 1) / G : 0;
   if (nb == 0) return;
@@ -820,6 +827,209 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the block
 }
 
+// ------------------------------------------------------------------ persistent weight gradient
+// dW[Nw][Kw] partial slices: part[c][n][k] = sum_{t in chunk c} dy[t][n] x[t][k], both operands
+// token-major ([T][*], as the forward left them: no transposed activation copies). A unit is
+// (chunk c, 256x256 tile); units are ordered chunk-major so the blocks of one XCD work on the same
+// token chunk at once (dy / x panels shared through L2), and the chunk count s is chosen on the
+// host so that the unit count fills the grid evenly. Operands are staged like the [K][N] halves
+// of gemm_kernel (64 token rows x 128 columns, 256-B rows, LDS-DMA through buffer resources;
+// rows past T read as zeros) and read with ds_read_b64_tr_b16 (read_n). The same 4-phase
+// pipeline and role-dependent waits as gemmp_kernel; a quadrant's fp32 partial (QS = 8 16-B
+// stores per lane) is written right after its MFMAs in the unit's last K-step. The s slices are
+// folded into the fp32 gradient by dna_sum_slices_accum (deterministic order).
+struct WArgs {
+  const bf16* dy; int ldy;  // [T][Nw]
+  const bf16* x; int ldx;   // [T][Kw]
+  float* part;              // [s][Nw][Kw]
+  int T, Nw, Kw, tilesM, tilesN, s, KTtot;
+};
+
+__global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
+  constexpr int QS = 8;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int L = xcd_remap(b, G);  // blocks of one XCD: consecutive units
+  const int tiles = a.tilesM * a.tilesN;
+  const int U = tiles * a.s;
+  const int nb = L < U ? (U - L + G - 1) / G : 0;
+  if (nb == 0) return;
+
+  const auto rA = out_rsrc(a.dy, (uint32_t)((size_t)a.T * a.ldy * 2));
+  const auto rB = out_rsrc(a.x, (uint32_t)((size_t)a.T * a.ldx * 2));
+  uint32_t voA[2], voB[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = p * 32 + wave * 4 + (lane >> 4);
+    const int ch = ((lane & 15) ^ nswz(r)) * 16;
+    voA[p] = (uint32_t)(r * a.ldy * 2 + ch);
+    voB[p] = (uint32_t)(r * a.ldx * 2 + ch);
+  }
+
+  struct Cur { int i, kt, len, t0, m0, n0, c; };  // kt within the unit, t0 its first K-step
+  auto cur_at = [&](int i) {
+    Cur c;
+    c.i = i;
+    c.kt = 0;
+    const int u = min(i, nb - 1) * G + L;
+    c.c = u / tiles;
+    const int tl = u - c.c * tiles;
+    c.m0 = (tl / a.tilesN) * BM;
+    c.n0 = (tl % a.tilesN) * BN;
+    const int s0 = (int)((long long)c.c * a.KTtot / a.s), s1 = (int)((long long)(c.c + 1) * a.KTtot / a.s);
+    c.t0 = s0;
+    c.len = s1 - s0;
+    return c;
+  };
+  auto advance = [&](Cur& c) {
+    if (++c.kt == c.len) c = cur_at(c.i + 1);
+  };
+  auto img = [&](int v, int h) { return smem + ((v & 1) * 4 + h) * HALF; };
+  auto stage = [&](const Cur& c, int v, int h) {
+    const int step = c.t0 + (c.i < nb ? c.kt : c.len - 1);
+    const int trow = step * BK;
+    char* d = img(v, h);
+    const bool isA = h < 2;
+    const int col0 = isA ? c.m0 + h * 128 : c.n0 + (h - 2) * 128;
+    const int ld = isA ? a.ldy : a.ldx;
+    const int soff = __builtin_amdgcn_readfirstlane((trow * ld + col0) * 2);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, (lds_t*)(d + (p * 32 + wave * 4) * 256),
+                                               16, isA ? voA[p] : voB[p], soff, 0, 0);
+  };
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[q][r][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  auto readA = [&](int v, int mq) {
+    const char* im = img(v, mq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_n(im, kk * 32, wr * 64 + i * 16, lane);
+  };
+  auto readB = [&](int v, int nq, bf16x8 (&bf)[2][2]) {
+    const char* im = img(v, 2 + nq);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = read_n(im, kk * 32, wc * 32 + j * 16, lane);
+  };
+  auto mma = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = mfma(bf[j][kk], af[i][kk], acc[mq][nq][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int cq = 4 * (lane >> 4);
+  const auto rC = out_rsrc(a.part, (uint32_t)min((size_t)a.s * a.Nw * a.Kw * 4, (size_t)0xFFFFFFF0u));
+  const uint32_t voC = (uint32_t)(((wr * 64 + (lane & 15)) * a.Kw + wc * 32 + cq) * 4);
+  auto store_quadrant = [&](const Cur& c, int mq, int nq) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int soff = __builtin_amdgcn_readfirstlane(
+          (int)((((size_t)c.c * a.Nw + c.m0 + mq * 128 + i * 16) * a.Kw + c.n0 + nq * 128) * 4));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mq][nq][i][j]), rC,
+                                               voC + j * 64, soff, 0);
+        acc[mq][nq][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  Cur c0 = cur_at(0), c1 = c0, c2 = c0;
+  advance(c1);
+  advance(c2);
+  advance(c2);
+  stage(c0, 0, 0);
+  stage(c0, 0, 2);
+  stage(c0, 0, 3);
+  stage(c0, 0, 1);
+  stage(c1, 1, 0);
+  stage(c1, 1, 2);
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
+  DNA_BARRIER();
+  if (wr == 1) DNA_BARRIER();
+
+  auto wait_vm = [&](auto phase, int role) {
+    constexpr int p = decltype(phase)::value;
+    if (role == 0) __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
+    else if (role == 1) __builtin_amdgcn_s_waitcnt(waitcnt_imm(8 + p * QS));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_imm(8 + (4 - p) * QS));
+  };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  using P2 = std::integral_constant<int, 2>;
+  using P3 = std::integral_constant<int, 3>;
+  auto kstep = [&](int v, int role) {
+    const bool st = role == 1;
+    stage(c1, v + 1, 3);
+    wait_vm(P0{}, role);
+    readA(v, 0);
+    readB(v, 0, bf0);
+    DNA_BARRIER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, 0, bf0);
+    if (st) store_quadrant(c0, 0, 0);
+    DNA_BARRIER();
+    stage(c1, v + 1, 1);
+    wait_vm(P1{}, role);
+    readB(v, 1, bf1);
+    DNA_BARRIER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, 1, bf1);
+    if (st) store_quadrant(c0, 0, 1);
+    DNA_BARRIER();
+    stage(c2, v + 2, 0);
+    wait_vm(P2{}, role);
+    readA(v, 1);
+    DNA_BARRIER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1, 1, bf1);
+    if (st) store_quadrant(c0, 1, 1);
+    DNA_BARRIER();
+    stage(c2, v + 2, 2);
+    wait_vm(P3{}, role);
+    DNA_BARRIER();
+    mma(1, 0, bf0);
+    if (st) store_quadrant(c0, 1, 0);
+    DNA_BARRIER();
+  };
+
+  int v = 0;
+  for (int i = 0; i < nb; ++i) {
+    for (int kt = 0; kt < c0.len; ++kt, ++v) {
+      const int role = kt == c0.len - 1 ? 1 : (kt == 0 && i > 0) ? 2 : 0;
+      kstep(v, role);
+      advance(c1);
+      advance(c2);
+    }
+    c0 = cur_at(i + 1);
+  }
+  if (wr == 0) DNA_BARRIER();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <bool AK, bool BKM, int EPI>
 int launch(Args& a, int splits, hipStream_t s, const char* name) {
   a.tilesM = (a.M + BM - 1) / BM;
@@ -872,6 +1082,22 @@ int launchp(Args& a, hipStream_t s, const char* name) {
   hipLaunchKernelGGL((gemmp_kernel<EPI>), dim3(G), dim3(NTHR), 0, s, a);
   DNA_LAUNCH_CHECK(name);
   return DNA_OK;
+}
+
+
+// chunk count for dna_linear_wgrad_p: minimise the modelled time in K-step units --
+//   ceil(tiles*s / G) rounds x (KTtot/s steps + ~3 steps of per-unit store tail)
+//   + the fp32 partial round trip of the slice sum (s*N*K*8 bytes at ~6 TB/s, ~1.6 us a step)
+// with each chunk >= 4 K-steps and s <= 64
+inline int wgrad_chunks(int tiles, int KTtot, int G, double nk) {
+  int best = 1;
+  double best_cost = 1e30;
+  for (int s = 1; s <= 64 && KTtot / s >= 4; ++s) {
+    const int rounds = (tiles * s + G - 1) / G;
+    const double cost = rounds * ((double)KTtot / s + 3.0) + s * nk * 8.0 / (6e12 * 1.6e-6);
+    if (cost < best_cost - 1e-9) { best_cost = cost; best = s; }
+  }
+  return best;
 }
 
 inline Args base_args() {
@@ -968,4 +1194,32 @@ extern "C" int dna_geglu_linear_dgrad(const void* dy, const void* w, const void*
   a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed; a.off = offset;
   return launch<true, false, EPI_GEGLU_BWD>(a, 1, as_stream(stream), "dna_geglu_linear_dgrad");
+}
+
+extern "C" int dna_linear_wgrad_p_splits(int M, int N, int K) {
+  if (M <= 0 || N % BM || K % BN) return 1;
+  return wgrad_chunks((N / BM) * (K / BN), (M + BK - 1) / BK, num_cus() & ~7, (double)N * K);
+}
+
+extern "C" int dna_linear_wgrad_p(const void* dy, const void* x, int M, int N, int K, int splits,
+                                  float* partials, void* stream) {
+  DNA_CHECK_ARG(dy && x && partials, "dna_linear_wgrad_p: null pointer");
+  DNA_CHECK_ARG(M > 0 && N % BM == 0 && K % BN == 0,
+                "dna_linear_wgrad_p: N, K %% 256 required (N=%d K=%d)", N, K);
+  const int KTtot = (M + BK - 1) / BK;
+  DNA_CHECK_ARG(splits >= 1 && KTtot / splits >= 2, "dna_linear_wgrad_p: bad splits %d", splits);
+  DNA_CHECK_ARG((size_t)M * (N > K ? N : K) * 2 < (1ull << 31) && (size_t)splits * N * K * 4 < (1ull << 32),
+                "dna_linear_wgrad_p: operands too large for 32-bit buffer offsets");
+  WArgs a{};
+  a.dy = (const bf16*)dy; a.ldy = N;
+  a.x = (const bf16*)x; a.ldx = K;
+  a.part = partials;
+  a.T = M; a.Nw = N; a.Kw = K;
+  a.tilesM = N / BM; a.tilesN = K / BN; a.s = splits; a.KTtot = KTtot;
+  const int U = a.tilesM * a.tilesN * splits;
+  int G = num_cus() & ~7;
+  G = U < G ? U : G;
+  hipLaunchKernelGGL(wgradp_kernel, dim3(G), dim3(NTHR), 0, as_stream(stream), a);
+  DNA_LAUNCH_CHECK("dna_linear_wgrad_p");
+  return DNA_OK;
 }

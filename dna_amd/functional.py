@@ -459,10 +459,41 @@ def wgrad_splits(rows, m, n, target_tiles=512, max_splits=None):
     return s
 
 
+def _hip_wgrad_ok(dy, x):
+    """The persistent token-major wgrad kernel is opt-in (DNA_WGRAD_IMPL=hip): at the bench shapes
+    it reaches ~0.5 PF/s against hipBLASLt's 0.8-1.0 (its waves wait on HBM 77 % of the time:
+    one K-step of LDS-DMA lookahead is too short for first-touch token panels), so the default
+    stays hipBLASLt's split-K batched GEMM."""
+    rows, m = dy.shape
+    n = x.shape[1]
+    return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.is_cuda
+            and m % 256 == 0 and n % 256 == 0 and _gemm_impl() == "hip"
+            and os.environ.get("DNA_WGRAD_IMPL", "torch") == "hip")
+
+
+def _hip_wgrad_parts(dy, x):
+    """fp32 split-K partials [s, m, n] of dy^T x from the persistent MFMA kernel (token-major
+    operands read in place; s chosen by the library to fill the grid)."""
+    dy, x = dy.contiguous(), x.contiguous()
+    rows, m = dy.shape
+    n = x.shape[1]
+    s = N.lib().dna_linear_wgrad_p_splits(rows, m, n)
+    parts = torch.empty(s, m, n, device=dy.device, dtype=torch.float32)
+    N.call("dna_linear_wgrad_p", dy.data_ptr(), x.data_ptr(), rows, m, n, s, parts.data_ptr(),
+           N.stream_ptr())
+    return parts, s
+
+
 def wgrad(dy, x):
-    """fp32 dW [m, n] = dy[rows, m]^T x[rows, n] (split-K batched GEMM + fp32 sum for bf16)."""
+    """fp32 dW [m, n] = dy[rows, m]^T x[rows, n] (split-K partials + fp32 sum for bf16)."""
     if x.dtype == torch.float32:
         return torch.mm(dy.t(), x)
+    if _hip_wgrad_ok(dy, x):
+        parts, s = _hip_wgrad_parts(dy, x)
+        out = torch.zeros(parts.shape[1:], device=dy.device, dtype=torch.float32)
+        N.call("dna_sum_slices_accum", parts.data_ptr(), s, out.numel(), out.data_ptr(),
+               N.stream_ptr())
+        return out
     rows, m = dy.shape
     n = x.shape[1]
     s = wgrad_splits(rows, m, n)
@@ -474,10 +505,15 @@ def wgrad(dy, x):
 
 
 def wgrad_accumulate(dy, x, grad):
-    """grad[m, n] += dy^T x: split-K partials from hipBLASLt folded in by one native pass."""
+    """grad[m, n] += dy^T x: split-K partials (the persistent MFMA kernel; hipBLASLt batched GEMM
+    for shapes it does not take, or with DNA_WGRAD_IMPL=torch) folded in by one native pass."""
     rows, m = dy.shape
     n = x.shape[1]
     assert grad.is_contiguous() and grad.dtype == torch.float32 and grad.shape == (m, n)
+    if _hip_wgrad_ok(dy, x):
+        parts, s = _hip_wgrad_parts(dy, x)
+        N.call("dna_sum_slices_accum", parts.data_ptr(), s, m * n, grad.data_ptr(), N.stream_ptr())
+        return
     s = wgrad_splits(rows, m, n)
     if s == 1:
         parts = torch.mm(dy.t(), x, out_dtype=torch.float32)

@@ -170,6 +170,14 @@ int dna_linear_wgrad(const void* dy, const void* x, int M, int N, int K, int spl
  * dna_linear_fwd(dy, w^T, NULL, M, K, N, dx) on both-operands-K-major MFMA tiles (replaces the
  * dgrad half of torch.nn.Linear's autograd backward, bert_layers.py:158/:214/:292/:297/:560). */
 int dna_transpose_bf16(const void* src, int rows, int cols, void* dst, void* stream);
+/* Weight gradient on the persistent MFMA kernel, operands token-major as the forward left them:
+ * partials[s][N][K] = sum over token chunk s of dy[t][N]^T x[t][K] (chunks of ceil(M/64)/splits
+ * 64-token steps; N, K % 256 == 0; rows past M read as zero). splits from
+ * dna_linear_wgrad_p_splits (fills the grid evenly); fold with dna_sum_slices_accum. Replaces
+ * the weight half of torch.nn.Linear's autograd backward at the same call sites. */
+int dna_linear_wgrad_p_splits(int M, int N, int K);
+int dna_linear_wgrad_p(const void* dy, const void* x, int M, int N, int K, int splits,
+                       float* partials, void* stream);
 /* gated_layers + GeGLU + dropout in one launch (bert_layers.py:292-296):
  *   g[M, 2F] = x[M,K] . wg^T + bias (bias fp32 [2F] or NULL),
  *   out[M, F] = dropout(gelu_erf(g[:, :F]) * g[:, F:])   -- same Philox mask as dna_geglu_fwd.

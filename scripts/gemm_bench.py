@@ -80,6 +80,12 @@ def check(M=4096):
         part = torch.empty(s, n, k, device="cuda")
         ours_wgrad(dy, x, s, part)
         e3 = rel(part.sum(0), dy.float().t() @ x.float())
+        sp = N.lib().dna_linear_wgrad_p_splits(M, n, k)
+        partp = torch.empty(sp, n, k, device="cuda")
+        N.call("dna_linear_wgrad_p", dy.data_ptr(), x.data_ptr(), M, n, k, sp, partp.data_ptr(), st())
+        e4 = rel(partp.sum(0), dy.float().t() @ x.float())
+        print(f"check {name}: wgrad_p (s={sp}) {e4:.2e}", flush=True)
+        ok &= e4 < 1e-5
         print(f"check {name}: fwd {e1:.2e} dgrad {e2:.2e} wgrad {e3:.2e}", flush=True)
         ok &= max(e1, e2) < 1e-2 and e3 < 1e-5
     # odd M (tail rows)
@@ -138,10 +144,16 @@ def bench(M, iters):
         fl = 2.0 * M * n * k
         s = wgrad_splits(M, n, k)
         part = torch.empty(s, n, k, device="cuda")
+        sp = N.lib().dna_linear_wgrad_p_splits(M, n, k)
+        partp = torch.empty(sp, n, k, device="cuda")
         bb = b.bfloat16()
         rows = [
             ("fwd", lambda: ours_fwd(x, w, b, y), lambda: torch.addmm(bb, x, w.t())),
             ("dgrad", lambda: ours_dgrad(dy, w, dx), lambda: torch.mm(dy, w)),
+            (f"wgradP/s{sp}", lambda: N.call("dna_linear_wgrad_p", dy.data_ptr(), x.data_ptr(), M, n, k, sp,
+                                            partp.data_ptr(), st()),
+             lambda: torch.bmm(dy.view(s, M // s, n).transpose(1, 2), x.view(s, M // s, k),
+                               out_dtype=torch.float32)),
             (f"wgrad/s{s}", lambda: ours_wgrad(dy, x, s, part),
              lambda: torch.bmm(dy.view(s, M // s, n).transpose(1, 2), x.view(s, M // s, k),
                                out_dtype=torch.float32)),
@@ -184,8 +196,12 @@ def only(M, iters, name, tag):
     dx = torch.empty(M, k, device="cuda", dtype=torch.bfloat16)
     s = wgrad_splits(M, n, k)
     part = torch.empty(s, n, k, device="cuda")
+    sp = N.lib().dna_linear_wgrad_p_splits(M, n, k)
+    partp = torch.empty(sp, n, k, device="cuda")
     fn = {"fwd": lambda: ours_fwd(x, w, None, y), "dgrad": lambda: ours_dgrad(dy, w, dx),
-          "wgrad": lambda: ours_wgrad(dy, x, s, part)}[tag]
+          "wgrad": lambda: ours_wgrad(dy, x, s, part),
+          "wgradp": lambda: N.call("dna_linear_wgrad_p", dy.data_ptr(), x.data_ptr(), M, n, k, sp,
+                                   partp.data_ptr(), st())}[tag]
     t = timeit(fn, iters)
     print(f"{name} {tag}: {t:.1f} us {2.0 * M * n * k / t / 1e6:.0f} TF", flush=True)
 
