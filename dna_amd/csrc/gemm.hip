@@ -483,13 +483,13 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
 // One 512-thread block per CU walks its units (256x256 output tiles) u = i*G + L(block) with the
 // SAME 4-phase half-tile pipeline as gemm_kernel, but the K-steps of consecutive units form one
 // continuous stream: the stages of unit i+1's first two K-steps are in flight while unit i ends,
-// and unit i's epilogue (bias from LDS, branch-free buffer stores) is issued while they land. The
-// per-tile cost of the non-persistent kernel (pipeline fill from memory, block turnover, store
-// tail: ~13 us per tile at K = 768, i.e. 8 K-steps of work) is gone.
-// vmcnt accounting: the epilogue's S stores sit in the VMEM queue between the stages of the next
-// unit's K-steps 0/1 and 1/2, so the 4 phases of a unit's first K-step wait vmcnt(8 + S) instead
-// of vmcnt(8) (the stores themselves never have to complete before the wave moves on); from the
-// second K-step on the stores are older than every wait target and retire with it.
+// and unit i's outputs are stored (bias from LDS, branch-free 16-B buffer stores) piecewise in its
+// last K-step, each quadrant / row half right after the MFMAs that finish it. The per-tile cost
+// of the non-persistent kernel (pipeline fill from memory, block turnover, an 8-B store tail of
+// 7 B/cycle/CU: ~13 us per tile at K = 768, i.e. 8 K-steps of work) drops to ~2-5 us.
+// vmcnt accounting: stores issued in a unit's last K-step sit in the VMEM queue between LDS-DMA
+// stages, so the waits of that step and of the next unit's first step leave them in flight
+// (role-dependent immediates, see wait_vm); they retire with the waits of the step after.
 constexpr int BIAS_LDS = 32 * 1024;  // bias row staged once per block (N <= 8192 floats)
 
 __host__ __device__ constexpr int waitcnt_imm(int vm) {  // gfx9 s_waitcnt: vmcnt=vm, others no-wait
@@ -516,7 +516,6 @@ __device__ __forceinline__ void unit_tile(const Args& a, int u, int& m0, int& n0
 template <int EPI>
 __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU, "persistent kernel: bf16 / GeGLU epilogues");
-  constexpr int S = EPI == EPI_BF16 ? 32 : 48;  // VMEM instructions of one epilogue (stores)
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -629,81 +628,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   const int ldo = EPI == EPI_GEGLU ? 2 * a.F : a.ldc;
   const auto rC = out_rsrc(a.C, (uint32_t)((size_t)a.M * ldo * 2));
   const uint32_t voC = (uint32_t)(((wr * 64 + (lane & 15)) * ldo + wc * 32 + cq) * 2);
-  auto epilogue = [&](const Cur& c) {
-    if constexpr (EPI == EPI_BF16) {
-#pragma unroll
-      for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + j * 16 + cq);
-#pragma unroll
-          for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[mq][nq][i][j] += bv;
-        }
-#pragma unroll
-      for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int soff = __builtin_amdgcn_readfirstlane(((c.m0 + mq * 128 + i * 16) * ldo + c.n0) * 2);
-#pragma unroll
-          for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const f32x4 v = acc[mq][nq][i][j];
-              const bf16x4 h = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rC,
-                                                    voC + (nq * 128 + j * 16) * 2, soff, 0);
-            }
-        }
-    } else {  // EPI_GEGLU: quadrant column nq=0 holds g1 columns, nq=1 the matching g2 columns
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = c.n0 + wc * 32 + j * 16 + cq;
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias_lds + col);
-        const f32x4 b2 = *reinterpret_cast<const f32x4*>(bias_lds + a.F + col);
-#pragma unroll
-        for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            acc[mq][0][i][j] += b1;
-            acc[mq][1][i][j] += b2;
-          }
-      }
-      const auto ra = out_rsrc(a.aux, (uint32_t)((size_t)a.M * a.F * 2));
-      const uint32_t voa = (uint32_t)(((wr * 64 + (lane & 15)) * a.F + wc * 32 + cq) * 2);
-#pragma unroll
-      for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = c.m0 + mq * 128 + i * 16;
-          const int sg = __builtin_amdgcn_readfirstlane((row * ldo + c.n0) * 2);
-          const int sa = __builtin_amdgcn_readfirstlane((row * a.F + c.n0) * 2);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const f32x4 v1 = acc[mq][0][i][j], v2 = acc[mq][1][i][j];
-            const bf16x4 h1 = bf16x4{(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
-            const bf16x4 h2 = bf16x4{(bf16)v2[0], (bf16)v2[1], (bf16)v2[2], (bf16)v2[3]};
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h1), rC, voC + j * 32, sg, 0);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h2), rC,
-                                                  voC + j * 32 + a.F * 2, sg, 0);
-            const int col = c.n0 + wc * 32 + j * 16 + cq;
-            const size_t e = (size_t)(row + wr * 64 + (lane & 15)) * a.F + col;
-            const uint32_t keep =
-                a.p > 0.f ? (dropout_keep8(a.seed, a.off, e >> 3, a.th) >> (e & 4)) & 0xFu : 0xFu;
-            f32x4 o;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float x = gelu_erf((float)h1[q]) * (float)h2[q];
-              o[q] = a.p > 0.f ? (((keep >> q) & 1) ? x * a.ks : 0.f) : x;
-            }
-            const bf16x4 ho = bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, ho), ra, voa + j * 32, sa, 0);
-          }
-        }
-    }
-  };
-
   // BF16: a quadrant (mq, nq) is final right after its MFMAs in a unit's last K-step, so it is
   // stored there (bias from LDS), overlapping the remaining phases. For each (row block i) the
   // lane's two 4-column groups j = 0 / 1 are exchanged with v_permlane16_swap so that every
@@ -712,7 +636,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   // {0, 16, 8, 24}[cg] .. +7 of the wave's 32-column slab.
   const uint32_t voQ = (uint32_t)(((wr * 64 + (lane & 15)) * a.ldc + wc * 32 +
                                    (((lane >> 4) & 1) << 4) + (((lane >> 4) & 2) << 2)) * 2);
-  auto store_quadrant = [&](const Cur& c, int mq, int nq) {
+  auto store_quadrant = [&](const Cur& c, int mq, int nq) __attribute__((always_inline)) {
     const f32x4 bj0 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + cq);
     const f32x4 bj1 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + 16 + cq);
 #pragma unroll
@@ -729,6 +653,53 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       else asm volatile("" :: "v"(o));
       acc[mq][nq][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
       acc[mq][nq][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  // GeGLU: the rows of half mq are final once both column quadrants (mq, 0) = g1 and (mq, 1) = g2
+  // are (phase 1 for mq = 0, phase 3 for mq = 1 of a unit's last K-step): bias, bf16 g1 / g2
+  // stores, then a = dropout(gelu(g1) * g2) from the rounded values -- all three widened to
+  // 16-B stores by the same permlane16 exchange; one Philox keep8 draw per 8 columns.
+  const auto rAux = out_rsrc(a.aux, (uint32_t)((size_t)a.M * a.F * 2));
+  const int colq = wc * 32 + (((lane >> 4) & 1) << 4) + (((lane >> 4) & 2) << 2);  // after the swap
+  const uint32_t voG = (uint32_t)(((wr * 64 + (lane & 15)) * 2 * a.F + colq) * 2);
+  const uint32_t voAx = (uint32_t)(((wr * 64 + (lane & 15)) * a.F + colq) * 2);
+  auto swap8 = [&](f32x4 v0, f32x4 v1) __attribute__((always_inline)) {  // two 4-column groups -> this lane's 8 columns (bf16)
+    u32x2 h0 = __builtin_bit_cast(u32x2, bf16x4{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]});
+    u32x2 h1 = __builtin_bit_cast(u32x2, bf16x4{(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]});
+    const auto sx = __builtin_amdgcn_permlane16_swap(h0[0], h1[0], false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(h0[1], h1[1], false, false);
+    return u32x4{sx[0], sy[0], sx[1], sy[1]};
+  };
+  auto store_geglu_half = [&](const Cur& c, int mq) __attribute__((always_inline)) {
+    const f32x4 b10 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + wc * 32 + cq);
+    const f32x4 b11 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + wc * 32 + 16 + cq);
+    const f32x4 b20 = *reinterpret_cast<const f32x4*>(bias_lds + a.F + c.n0 + wc * 32 + cq);
+    const f32x4 b21 = *reinterpret_cast<const f32x4*>(bias_lds + a.F + c.n0 + wc * 32 + 16 + cq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u32x4 g1 = swap8(acc[mq][0][i][0] + b10, acc[mq][0][i][1] + b11);
+      const u32x4 g2 = swap8(acc[mq][1][i][0] + b20, acc[mq][1][i][1] + b21);
+      const int row = c.m0 + mq * 128 + i * 16;
+      // row-block offsets added per lane (soffset 0): keeps this epilogue's scalar footprint small
+      const uint32_t og = voG + (uint32_t)((row * 2 * a.F + c.n0) * 2);
+      const uint32_t oa = voAx + (uint32_t)((row * a.F + c.n0) * 2);
+      __builtin_amdgcn_raw_buffer_store_b128(g1, rC, og, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(g2, rC, og + a.F * 2, 0, 0);
+      const bf16x8 h1 = __builtin_bit_cast(bf16x8, g1), h2 = __builtin_bit_cast(bf16x8, g2);
+      const size_t e = (size_t)(row + wr * 64 + (lane & 15)) * a.F + c.n0 + colq;  // e % 8 == 0
+      const uint32_t keep = a.p > 0.f ? dropout_keep8(a.seed, a.off, e >> 3, a.th) : 0xFFu;
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float x = gelu_erf((float)h1[q]) * (float)h2[q];
+        o[q] = (bf16)(a.p > 0.f ? (((keep >> q) & 1) ? x * a.ks : 0.f) : x);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rAux, oa, 0, 0);
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
 
@@ -755,10 +726,12 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   //   role 2  a unit's first step after an epilogue: the stores issued behind the half-tiles it
   //           waits for stay in flight -- BF16 (4 - p) * QS, GeGLU (epilogue after the last step) S
   constexpr int QS = 4;  // 16-B stores per quadrant and lane (BF16)
+  constexpr int GS = 12;  // GeGLU: 16-B stores per half (g1, g2, a x 4 row blocks)
   auto wait_vm = [&](auto phase, int role) {
     constexpr int p = decltype(phase)::value;
-    constexpr int w1 = EPI == EPI_BF16 ? 8 + p * QS : 8;
-    constexpr int w2 = EPI == EPI_BF16 ? 8 + (4 - p) * QS : 8 + S;
+    // GeGLU: half 0 stored after phase 1's MFMAs, half 1 after phase 3's
+    constexpr int w1 = EPI == EPI_BF16 ? 8 + p * QS : 8 + (p >= 2 ? GS : 0);
+    constexpr int w2 = EPI == EPI_BF16 ? 8 + (4 - p) * QS : 8 + (p < 2 ? 2 * GS : GS);
     if (role == 0) __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
     else if (role == 1) __builtin_amdgcn_s_waitcnt(waitcnt_imm(w1));
     else __builtin_amdgcn_s_waitcnt(waitcnt_imm(w2));
@@ -769,6 +742,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   using P3 = std::integral_constant<int, 3>;
   auto kstep = [&](int v, int role) {
     const bool st = EPI == EPI_BF16 && role == 1;
+    const bool sg = EPI == EPI_GEGLU && role == 1;
     // phase 0: quadrant (0,0)
     stage(c1, v + 1, 3);
     wait_vm(P0{}, role);
@@ -789,6 +763,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     __builtin_amdgcn_sched_barrier(0);
     mma(0, 1, bf1);
     if (st) store_quadrant(c0, 0, 1);
+    if (sg) store_geglu_half(c0, 0);
     DNA_BARRIER();
     // phase 2: quadrant (1,1)
     stage(c2, v + 2, 0);
@@ -806,20 +781,17 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     DNA_BARRIER();
     mma(1, 0, bf0);
     if (st) store_quadrant(c0, 1, 0);
+    if (sg) store_geglu_half(c0, 1);
     DNA_BARRIER();
   };
 
   int v = 0;
   for (int i = 0; i < nb; ++i) {
     for (int kt = 0; kt < KT; ++kt, ++v) {
-      const int role = (kt == KT - 1 && EPI == EPI_BF16) ? 1 : (kt == 0 && i > 0) ? 2 : 0;
+      const int role = kt == KT - 1 ? 1 : (kt == 0 && i > 0) ? 2 : 0;
       kstep(v, role);
       advance(c1);
       advance(c2);
-    }
-    if constexpr (EPI == EPI_GEGLU) {
-      epilogue(c0);
-      zero_acc();
     }
     c0 = cur_at(i + 1);
   }
@@ -940,7 +912,7 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
   const int cq = 4 * (lane >> 4);
   const auto rC = out_rsrc(a.part, (uint32_t)min((size_t)a.s * a.Nw * a.Kw * 4, (size_t)0xFFFFFFF0u));
   const uint32_t voC = (uint32_t)(((wr * 64 + (lane & 15)) * a.Kw + wc * 32 + cq) * 4);
-  auto store_quadrant = [&](const Cur& c, int mq, int nq) {
+  auto store_quadrant = [&](const Cur& c, int mq, int nq) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int soff = __builtin_amdgcn_readfirstlane(
@@ -1173,7 +1145,7 @@ extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* b
   a.M = M; a.N = F; a.K = K; a.ksplit = K; a.F = F;
   a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed; a.off = offset;
-  if (persistent_enabled() && 2 * F <= BIAS_LDS / 4 &&
+  if (persistent_enabled() && 2 * F <= BIAS_LDS / 4 && K >= 2 * BK &&
       (size_t)M * (K > 2 * F ? K : 2 * F) * 2 < (1ull << 31))
     return launchp<EPI_GEGLU>(a, as_stream(stream), "dna_geglu_linear_fwd");
   return launch<true, true, EPI_GEGLU>(a, 1, as_stream(stream), "dna_geglu_linear_fwd");
