@@ -80,12 +80,13 @@ def make_batches(n_batches, batch, rank, device):
     return out
 
 
-def cpu_baseline(seconds_budget=20.0, threads=None, cfg=None, seq=None, batch=2, max_seq=64,
+def cpu_baseline(seconds_budget=10.0, threads=None, cfg=None, seq=None, batch=2, max_seq=100000,
                  label="DNABERT-2-117M S=512"):
     """Oracle restatement (PyTorch CPU fp32, oracle/bert_ref.py, pinned to the reference) timing
     the same step (fwd + bert_cross_entropy + bwd + clip + AdamW, dropout 0.1) on a bounded sample."""
     from oracle import bert_ref
-    threads = threads or min(os.cpu_count() or 1, 16)
+    from dna_amd.hg38 import host_threads
+    threads = threads or min(host_threads(), 16)
     prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
@@ -116,7 +117,7 @@ def cpu_baseline(seconds_budget=20.0, threads=None, cfg=None, seq=None, batch=2,
 
     step(1)  # warmup
     b, n_seq, t_used = batch, 0, 0.0
-    while t_used < seconds_budget * 0.5 and n_seq < max_seq:
+    while (t_used < seconds_budget and n_seq < max_seq) or n_seq == 0:
         t0 = time.perf_counter()
         step(b)
         t_used += time.perf_counter() - t0
@@ -125,7 +126,8 @@ def cpu_baseline(seconds_budget=20.0, threads=None, cfg=None, seq=None, batch=2,
     return {"value": round(n_seq / t_used, 4), "unit": "sequences/s", "cores": threads,
             "kind": "port",
             "sample": f"{n_seq} sequences (batches of {b}) of {label} fp32 train steps "
-                      f"(fwd+loss+bwd+clip+AdamW) with the oracle restatement on {threads} threads"}
+                      f"(fwd+loss+bwd+clip+AdamW) with the oracle restatement on {threads} threads, "
+                      f"{t_used:.1f} s timed"}
 
 
 # BASELINE configs[0] / SURVEY §8(d) config A: 2 layers, d_model 128, 2 heads, S = 128, batch 8
@@ -136,12 +138,13 @@ CONFIG_A = dict(vocab_size=4096, hidden_size=128, num_hidden_layers=2, num_atten
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=100)   # 100 timed, 20 warm-up
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("DNA_BENCH_BATCH", 256)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-b64", action="store_true", help="skip the extra per-GPU b=64 measurement")
+    ap.add_argument("--no-data-pipeline", action="store_true", help="skip the host data-path timing")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,10 +167,25 @@ def main():
     t_data = time.perf_counter()
     batches = make_batches(4, args.batch, rank, device)
     t_data = time.perf_counter() - t_data
-    data_pipeline = {"seq_per_s": round(4 * args.batch / t_data, 1),
-                     "threads": min(16, os.cpu_count() or 1),
-                     "what": "host tokenize (native BPE, multithreaded) + BERT masking + H2D copy of "
-                             "4096-bp windows, timed before the GPU region (not part of value)"}
+    data_pipeline = None
+    if rank == 0 and not args.no_data_pipeline:
+        # train.py's own data path, timed before the GPU region (not part of value): registry
+        # dataset bert_hg38 over a synthetic FASTA/BED -> torch DataLoader (batched __getitems__:
+        # FASTA -> native multithreaded BPE -> native masking; 8 worker processes sharing this
+        # rank's host threads) -> DeviceBatch.from_host (row bookkeeping + pinned H2D copy)
+        from dna_amd.hg38 import host_threads
+        from scripts.data_pipeline_bench import measure, synthetic_root
+        root = synthetic_root(n_chroms=8, chrom_len=16_777_216)
+        workers = 8
+        data_pipeline = {"seq_per_s": round(measure(root, workers, args.batch, 60, device=device), 1),
+                         "threads": host_threads(), "workers": workers,
+                         "bench_batch_prep_seq_per_s": round(4 * args.batch / t_data, 1),
+                         "what": "train.py data path: BertHG38 DataLoader (FASTA -> native BPE -> "
+                                 "masking, 8 workers) + DeviceBatch.from_host (pinned H2D) over "
+                                 "4096-bp synthetic hg38 windows, steady state over 60 batches; "
+                                 "not part of value"}
+        import shutil
+        shutil.rmtree(root, ignore_errors=True)
 
     for i in range(args.warmup):
         trainer.step(batches[i % len(batches)])
@@ -254,12 +272,12 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
-        one = cpu_baseline(seconds_budget=12.0, threads=1)  # the reference forces OMP_NUM_THREADS=1
+        one = cpu_baseline(seconds_budget=10.0, threads=1)  # the reference forces OMP_NUM_THREADS=1
         cpu["single_thread"] = {"value": one["value"], "cores": 1, "sample": one["sample"]}
         ca = {}
         for th in (None, 1):
-            r = cpu_baseline(seconds_budget=4.0, threads=th, cfg=CONFIG_A, seq=128, batch=8,
-                             max_seq=4096, label="config A (2 layers, d=128, S=128)")
+            r = cpu_baseline(seconds_budget=10.0, threads=th, cfg=CONFIG_A, seq=128, batch=8,
+                             label="config A (2 layers, d=128, S=128)")
             ca["single_thread" if th == 1 else "all_threads"] = {k: r[k] for k in ("value", "cores", "sample")}
         cpu["config_a"] = ca
 

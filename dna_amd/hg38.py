@@ -179,6 +179,35 @@ class BertHG38Dataset(torch.utils.data.Dataset):
             raise NotImplementedError(f"tokenizer {self.tokenizer_name!r} (bpe / char)")
         return torch.LongTensor(ids)
 
+    # ---- batched fetch (torch DataLoader calls __getitems__ with a whole batch of indices):
+    # FASTA windows -> one multithreaded native BPE call for the batch -> native BERT masking with
+    # Philox draws keyed by (mask_seed, dataset index) -- reproducible for any worker layout, the
+    # same mask statistics as the reference's torch-RNG draws; __getitem__ keeps the
+    # reference's exact torch draw order for the parity tests. bpe + stdmlm only; any other
+    # configuration falls back to per-item __getitem__.
+    mask_seed = 2222
+    bpe_threads = 0  # 0: all cores (set per worker by BertHG38 when it starts several workers)
+
+    def __getitems__(self, indices):
+        if not (self.tokenizer_name == "bpe" and self.objective == "stdmlm" and self.use_tokenizer
+                and not self.replace_N_token and hasattr(self.tokenizer, "encode_windows")):
+            return [self[i] for i in indices]
+        wins = []
+        for i in indices:
+            chr_name, start, end = self.rows[i]
+            wins.append(self.fasta(chr_name, start, end, max_length=self.max_length,
+                                   return_augs=self.return_augs))
+        tok = self.tokenizer
+        ids = torch.from_numpy(tok.encode_windows(wins, self.pad_max_length, add_eos=self.add_eos,
+                                                  nthreads=self.bpe_threads))
+        out = []
+        for j, i in enumerate(indices):
+            target = ids[j]
+            data = bert_mask_fast(target, tok.mask_token_id, tok.pad_token_id, tok.vocab_size,
+                                  tok.all_special_ids, seed=self.mask_seed, sample_id=int(i))
+            out.append((data, target))
+        return out
+
     def __getitem__(self, idx):
         chr_name, start, end = self.rows[idx]
         seq = self.fasta(chr_name, start, end, max_length=self.max_length,
@@ -199,6 +228,16 @@ class BertHG38Dataset(torch.utils.data.Dataset):
             return bert_mask(data, tok.mask_token_id, tok.pad_token_id, tok.vocab_size,
                              special_token_ids=tok.all_special_ids), target
         return random_mask(data, tok.mask_token_id), target
+
+
+def host_threads():
+    """CPU threads this process may use: the affinity set, capped by OMP_NUM_THREADS when the
+    launcher sets it (a GPU host shares its cores among the GPUs' processes)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
 
 
 class SequenceDataset:
@@ -274,10 +313,14 @@ class BertHG38(SequenceDataset):
                                  [self.max_length, self.max_length_val, self.max_length_test])]
 
     def _data_loader(self, dataset, batch_size, shuffle=False, sampler=None):
+        # each worker tokenises whole batches with the native multithreaded BPE: split the cores
+        cores = host_threads()
+        dataset.bpe_threads = max(1, cores // max(1, self.num_workers)) if self.num_workers else 0
         return torch.utils.data.DataLoader(dataset, batch_size=batch_size,
                                            num_workers=self.num_workers, shuffle=shuffle,
                                            sampler=sampler, drop_last=self.drop_last,
-                                           pin_memory=self.pin_memory)
+                                           pin_memory=self.pin_memory,
+                                           persistent_workers=self.num_workers > 0)
 
     def train_dataloader(self, sampler=None, **kwargs):
         return self._data_loader(self.dataset_train, self.batch_size,
