@@ -175,8 +175,9 @@ class BertHG38Dataset(torch.utils.data.Dataset):
         elif self.tokenizer_name == "char":
             ids = self.tokenizer(seq, add_special_tokens=bool(self.add_eos), padding="max_length",
                                  max_length=self.max_length, truncation=True)["input_ids"]
-        else:
-            raise NotImplementedError(f"tokenizer {self.tokenizer_name!r} (bpe / char)")
+        else:  # the reference's __getitem__ has no kmer branch either (hg38_dataset.py:357-380)
+            raise NotImplementedError(f"items for tokenizer {self.tokenizer_name!r}: the reference "
+                                      "dataset tokenises bpe / char only (kmer: tokenizer only)")
         return torch.LongTensor(ids)
 
     # ---- batched fetch (torch DataLoader calls __getitems__ with a whole batch of indices):
@@ -294,10 +295,11 @@ class BertHG38(SequenceDataset):
             from .tokenizer import CharacterTokenizer
             self.tokenizer = CharacterTokenizer(characters=["A", "C", "G", "T", "N"],
                                                 model_max_length=self.max_length + 2)
+        elif self.tokenizer_name == "kmer":  # genomics.py:1142-1144 (NT-v2 6-mer EsmTokenizer)
+            from .tokenizer import KmerTokenizer
+            self.tokenizer = KmerTokenizer(model_max_length=2048)
         else:
-            raise NotImplementedError(f"tokenizer_name={self.tokenizer_name!r}: bpe / char "
-                                      "(kmer cannot produce items in the reference's "
-                                      "BertHG38Dataset either, hg38_dataset.py:358-375)")
+            raise NotImplementedError(f"tokenizer_name={self.tokenizer_name!r}: bpe / char / kmer")
         self.vocab_size = len(self.tokenizer)
         self.init_datasets()
 

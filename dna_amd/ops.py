@@ -1,0 +1,199 @@
+"""The hot-path HIP kernels as PyTorch operators: `torch.ops.dna_amd.<op>` (SURVEY §8(b) kernel
+boundary).
+
+Each op wraps one C-ABI entry point of include/dna_amd.h, runs on the current torch HIP stream,
+writes into caller-allocated outputs (declared as mutated arguments), and raises a Python
+exception on dtype / shape / contiguity / device errors -- the checks the reference's Triton slot
+asserts (flash_attn_triton.py:849-855) -- instead of letting a kernel read out of bounds.
+
+    torch.ops.dna_amd.attn_fwd(qkv, key_valid, slopes, b, S, H, scale, out, lse)
+    torch.ops.dna_amd.attn_bwd(qkv, out, dout, lse, key_valid, slopes, b, S, H, scale, dqkv)
+    torch.ops.dna_amd.linear_fwd(x, w, bias, y)                   y = x w^T (+ bias), bf16 MFMA
+    torch.ops.dna_amd.geglu_fwd(g, p, seed, offset, a)            a = dropout(gelu(g1) g2)
+    torch.ops.dna_amd.geglu_bwd(da, g, p, seed, offset, dg)
+    torch.ops.dna_amd.xent_fwd(logits, target, loss, lse)         per-row CE
+    torch.ops.dna_amd.transpose_bf16(src, dst)
+and the functional slot of the reference's FlashAttention call site (bert_layers.py:167-178 ->
+flash_attn_qkvpacked_func, flash_attn_triton.py:1077-1130), autograd included:
+
+    out, lse = torch.ops.dna_amd.flash_attn_qkvpacked(qkv[b,S,3,H,D], slopes[H],
+                                                      key_valid[b,S] | None, softmax_scale)
+    out = dna_amd.ops.flash_attn_qkvpacked_func(qkv, slopes, key_valid, softmax_scale)
+The ALiBi + key-pad bias enters as (slopes, key_valid) instead of a materialised [b,H,S,S] bias
+tensor: bias[h,i,j] = -slopes[h]*|i-j| + (key j pad ? -10000 : 0), exactly what
+bert_layers.py:421-448 builds. The model's own autograd Functions (dna_amd.functional) call the
+same C ABI directly (no per-call dispatcher overhead on the ~300 launches of a step).
+"""
+import math
+
+import torch
+
+from . import _native as N
+
+_DT = {torch.float32: N.F32, torch.bfloat16: N.BF16}
+
+
+def _check(cond, msg):
+    if not cond:
+        raise RuntimeError(f"dna_amd: {msg}")
+
+
+def _cuda_contig(name, t, dtypes=None):
+    _check(t.is_cuda, f"{name} must be on the GPU (no CPU fallback), got {t.device}")
+    _check(t.is_contiguous(), f"{name} must be contiguous")
+    if dtypes is not None:
+        _check(t.dtype in dtypes, f"{name} dtype {t.dtype} not in {dtypes}")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+# ------------------------------------------------------------------------------- attention
+@torch.library.custom_op("dna_amd::attn_fwd", mutates_args=("out", "lse"))
+def attn_fwd(qkv: torch.Tensor, key_valid: torch.Tensor | None, slopes: torch.Tensor, b: int,
+             S: int, H: int, scale: float, out: torch.Tensor, lse: torch.Tensor) -> None:
+    _cuda_contig("qkv", qkv, (torch.bfloat16, torch.float32))
+    _check(qkv.dim() == 2 and qkv.shape[0] == b * S and qkv.shape[1] % (3 * H) == 0,
+           f"qkv must be [b*S, 3*H*D], got {tuple(qkv.shape)}")
+    D = qkv.shape[1] // (3 * H)
+    _cuda_contig("out", out, (qkv.dtype,))
+    _check(tuple(out.shape) == (b * S, H * D), "out must be [b*S, H*D]")
+    _cuda_contig("lse", lse, (torch.float32,))
+    _check(lse.numel() == b * H * S, "lse must hold b*H*S floats")
+    _cuda_contig("slopes", slopes, (torch.float32,))
+    if key_valid is not None:
+        _cuda_contig("key_valid", key_valid, (torch.uint8, torch.bool))
+        _check(key_valid.numel() == b * S, "key_valid must hold b*S entries")
+    N.call("dna_attn_fwd", qkv.data_ptr(), _p(key_valid), slopes.data_ptr(), b, S, H, D,
+           _DT[qkv.dtype], scale, out.data_ptr(), lse.data_ptr(), N.stream_ptr())
+
+
+@torch.library.custom_op("dna_amd::attn_bwd", mutates_args=("dqkv",))
+def attn_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor,
+             key_valid: torch.Tensor | None, slopes: torch.Tensor, b: int, S: int, H: int,
+             scale: float, dqkv: torch.Tensor) -> None:
+    for n, t in (("qkv", qkv), ("out", out), ("dout", dout), ("dqkv", dqkv)):
+        _cuda_contig(n, t, (qkv.dtype,))
+    _cuda_contig("lse", lse, (torch.float32,))
+    _check(dqkv.shape == qkv.shape and dout.shape == out.shape, "dqkv / dout shapes")
+    D = qkv.shape[1] // (3 * H)
+    delta = torch.empty(b * H * S, device=qkv.device, dtype=torch.float32)
+    N.call("dna_attn_bwd", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+           _p(key_valid), slopes.data_ptr(), b, S, H, D, _DT[qkv.dtype], scale, dqkv.data_ptr(),
+           delta.data_ptr(), N.stream_ptr())
+
+
+@torch.library.custom_op("dna_amd::flash_attn_qkvpacked", mutates_args=())
+def flash_attn_qkvpacked(qkv: torch.Tensor, slopes: torch.Tensor, key_valid: torch.Tensor | None,
+                         softmax_scale: float | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """-> (out [b, S, H, D], lse [b, H, S] fp32 natural-log softmax normaliser)."""
+    _check(qkv.dim() == 5 and qkv.shape[2] == 3, f"qkv must be [b, S, 3, H, D], got {tuple(qkv.shape)}")
+    b, S, _, H, D = qkv.shape
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    packed = qkv.contiguous().view(b * S, 3 * H * D)
+    out = torch.empty(b * S, H * D, device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty(b, H, S, device=qkv.device, dtype=torch.float32)
+    kv = None if key_valid is None else key_valid.to(torch.uint8).contiguous()
+    attn_fwd(packed, kv, slopes.float().contiguous(), b, S, H, scale, out, lse)
+    return out.view(b, S, H, D), lse
+
+
+@flash_attn_qkvpacked.register_fake
+def _(qkv, slopes, key_valid, softmax_scale=None):
+    b, S, _, H, D = qkv.shape
+    return qkv.new_empty(b, S, H, D), qkv.new_empty(b, H, S, dtype=torch.float32)
+
+
+def _fa_setup(ctx, inputs, output):
+    qkv, slopes, key_valid, softmax_scale = inputs
+    out, lse = output
+    ctx.save_for_backward(qkv, slopes, key_valid if key_valid is not None else torch.empty(0),
+                          out, lse)
+    ctx.has_kv = key_valid is not None
+    ctx.scale = softmax_scale
+
+
+def _fa_backward(ctx, dout, dlse):
+    qkv, slopes, key_valid, out, lse = ctx.saved_tensors
+    b, S, _, H, D = qkv.shape
+    scale = ctx.scale if ctx.scale is not None else 1.0 / math.sqrt(D)
+    packed = qkv.contiguous().view(b * S, 3 * H * D)
+    kv = key_valid.to(torch.uint8).contiguous() if ctx.has_kv else None
+    dqkv = torch.empty_like(packed)
+    attn_bwd(packed, out.contiguous().view(b * S, H * D), dout.contiguous().view(b * S, H * D),
+             lse, kv, slopes.float().contiguous(), b, S, H, scale, dqkv)
+    return dqkv.view(qkv.shape), None, None, None
+
+
+flash_attn_qkvpacked.register_autograd(_fa_backward, setup_context=_fa_setup)
+
+
+def flash_attn_qkvpacked_func(qkv, slopes, key_valid=None, softmax_scale=None):
+    """Drop-in for flash_attn_qkvpacked_func at bert_layers.py:167-178 (returns out only); the
+    bias argument is replaced by the ALiBi slopes and the key-valid mask it is built from."""
+    return torch.ops.dna_amd.flash_attn_qkvpacked(qkv, slopes, key_valid, softmax_scale)[0]
+
+
+# ------------------------------------------------------------------------------- GEMM
+@torch.library.custom_op("dna_amd::linear_fwd", mutates_args=("y",))
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, y: torch.Tensor) -> None:
+    _cuda_contig("x", x, (torch.bfloat16,))
+    _cuda_contig("w", w, (torch.bfloat16,))
+    _cuda_contig("y", y, (torch.bfloat16,))
+    M, K = x.shape
+    Nn = w.shape[0]
+    _check(w.shape[1] == K and tuple(y.shape) == (M, Nn), "shapes: x[M,K], w[N,K], y[M,N]")
+    _check(K % 64 == 0 and Nn % 8 == 0, f"K % 64 and N % 8 required (K={K}, N={Nn})")
+    if bias is not None:
+        _cuda_contig("bias", bias, (torch.float32,))
+        _check(bias.numel() == Nn, "bias must hold N floats")
+    N.call("dna_linear_fwd", x.data_ptr(), w.data_ptr(), _p(bias), M, Nn, K, y.data_ptr(),
+           N.stream_ptr())
+
+
+@torch.library.custom_op("dna_amd::transpose_bf16", mutates_args=("dst",))
+def transpose_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
+    _cuda_contig("src", src, (torch.bfloat16,))
+    _cuda_contig("dst", dst, (torch.bfloat16,))
+    r, c = src.shape
+    _check(tuple(dst.shape) == (c, r), "dst must be src transposed")
+    N.call("dna_transpose_bf16", src.data_ptr(), r, c, dst.data_ptr(), N.stream_ptr())
+
+
+# ------------------------------------------------------------------------------- elementwise
+@torch.library.custom_op("dna_amd::geglu_fwd", mutates_args=("a",))
+def geglu_fwd(g: torch.Tensor, p: float, seed: int, offset: int, a: torch.Tensor) -> None:
+    _cuda_contig("g", g, (torch.bfloat16, torch.float32))
+    _cuda_contig("a", a, (g.dtype,))
+    n, f2 = g.shape
+    _check(tuple(a.shape) == (n, f2 // 2), "a must be [rows, F] for g [rows, 2F]")
+    N.call("dna_geglu_fwd", g.data_ptr(), _DT[g.dtype], n, f2 // 2, p, seed, offset, a.data_ptr(),
+           N.stream_ptr())
+
+
+@torch.library.custom_op("dna_amd::geglu_bwd", mutates_args=("dg",))
+def geglu_bwd(da: torch.Tensor, g: torch.Tensor, p: float, seed: int, offset: int,
+              dg: torch.Tensor) -> None:
+    _cuda_contig("g", g, (torch.bfloat16, torch.float32))
+    _cuda_contig("da", da, (g.dtype,))
+    _cuda_contig("dg", dg, (g.dtype,))
+    n, f2 = g.shape
+    _check(tuple(da.shape) == (n, f2 // 2) and dg.shape == g.shape, "da [rows, F], dg like g")
+    N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), _DT[g.dtype], n, f2 // 2, p, seed, offset,
+           dg.data_ptr(), N.stream_ptr())
+
+
+@torch.library.custom_op("dna_amd::xent_fwd", mutates_args=("loss", "lse"))
+def xent_fwd(logits: torch.Tensor, target: torch.Tensor, loss: torch.Tensor,
+             lse: torch.Tensor) -> None:
+    _cuda_contig("logits", logits, (torch.bfloat16, torch.float32))
+    _cuda_contig("target", target, (torch.int64,))
+    M, V = logits.shape
+    _check(target.numel() == M and loss.numel() == M and lse.numel() == M, "row counts")
+    N.call("dna_xent_fwd", logits.data_ptr(), _DT[logits.dtype], target.data_ptr(), M, V,
+           loss.data_ptr(), lse.data_ptr(), N.stream_ptr())
+
+
+OPS = ("attn_fwd", "attn_bwd", "flash_attn_qkvpacked", "linear_fwd", "transpose_bf16",
+       "geglu_fwd", "geglu_bwd", "xent_fwd")
