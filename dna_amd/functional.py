@@ -345,9 +345,10 @@ class Linear(torch.autograd.Function):
         ctx.weight = w
         ctx.has_b = b is not None
         flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
-        with _timed("gemm", flops):
-            if _hip_gemm_ok(x, w_lp, w_lp.shape[0], w_lp.shape[1]):
+        if _hip_gemm_ok(x, w_lp, w_lp.shape[0], w_lp.shape[1]):
+            with _timed("gemm_hip", flops):
                 return _hip_linear(x, w_lp, b if (b is None or b.dtype == torch.float32) else b.float())
+        with _timed("gemm", flops):
             if b is not None:
                 return torch.addmm(b.to(x.dtype), x, w_lp.t())
             return torch.mm(x, w_lp.t())
@@ -362,10 +363,11 @@ class Linear(torch.autograd.Function):
         flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
         dx = None
         if ctx.needs_input_grad[0]:
-            with _timed("gemm", flops):
-                if w_lpt is not None and _hip_gemm_ok(dy, w_lpt, w_lpt.shape[0], w_lpt.shape[1]):
+            if w_lpt is not None and _hip_gemm_ok(dy, w_lpt, w_lpt.shape[0], w_lpt.shape[1]):
+                with _timed("gemm_hip", flops):
                     dx = _hip_linear(dy, w_lpt, None)
-                else:
+            else:
+                with _timed("gemm", flops):
                     dx = torch.mm(dy, w_lp)
         w = ctx.weight
         direct = getattr(w, "_dna_direct", False) and w.grad is not None and x.dtype != torch.float32
@@ -374,7 +376,7 @@ class Linear(torch.autograd.Function):
             # wgrad beside the rest of the backward; dy / x must outlive it on the side stream
             side.wait_stream(torch.cuda.current_stream())
             _KEEP.append((dy, x))  # (record_stream instead made the allocator thrash)
-            with torch.cuda.stream(side), _timed("gemm", flops):
+            with torch.cuda.stream(side), _timed("gemm_wgrad", flops):
                 wgrad_accumulate(dy, x, w.grad)
             _queue_join()
             notify = getattr(w, "_dna_notify", None)
@@ -382,7 +384,7 @@ class Linear(torch.autograd.Function):
                 notify(w)
             dw = None
         else:
-          with _timed("gemm", flops):
+          with _timed("gemm_wgrad", flops):
             if direct:
                 # write straight into the flat fp32 gradient buffer (dna_amd.flat) and tell the
                 # gradient-bucket reducer, instead of returning dW to AccumulateGrad

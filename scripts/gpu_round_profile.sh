@@ -4,7 +4,7 @@
 # then the default bench line (which reads profiles/<round>/traffic.json). Outputs under
 # gpurun_out/<round>/; copy them into profiles/<round>/ afterwards.
 set -e
-R=${ROUND:-r01}
+R=${ROUND:-r02}
 BATCH=${BATCH:-256}
 ROOT=$GRAFT_REPO_ROOT
 OUT=$ROOT/gpurun_out/$R

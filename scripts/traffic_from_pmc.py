@@ -17,7 +17,8 @@ import sys
 
 # family -> (regex selecting its kernels, regex selecting the one kernel counted per op launch)
 FAMILIES = {
-    "gemm": (r"Cijk_|sum_slices_kernel", r"Cijk_"),
+    "gemm_hip": (r"gemmp_kernel|gemm_kernel", r"gemmp_kernel|gemm_kernel"),  # csrc/gemm.hip
+    "gemm_wgrad": (r"Cijk_|sum_slices_kernel|wgradp_kernel", r"Cijk_|wgradp_kernel"),
     "attn_fwd": (r"attn::fwd2?_bf16_kernel|attn4fwd_bf16|attn16fwd2_bf16",
                  r"attn::fwd2?_bf16_kernel|attn4fwd_bf16|attn16fwd2_bf16"),
     "attn_bwd": (r"attn::(dq|dkdv)2?_bf16_kernel|attn(2dq|4dkdv)_bf16|dq2_bf16|dkdv2_bf16",
