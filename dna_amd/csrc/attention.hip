@@ -1327,6 +1327,353 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void dq2_bf16_kernel(
   }
 }
 
+// ----------------------------------------------------------------------------- bf16 backward, v3
+// One fused kernel, one workgroup per (batch, head) for S = 128*KB: 4 waves, wave w owns keys
+// [w*32*KB, (w+1)*32*KB) and keeps their dK^T / dV^T in 4*KB f32x16 accumulators for the whole
+// pass, so dK and dV need no sum across workgroups. The workgroup sweeps the queries in slices of
+// 32 (Q, dO and the row constants of a slice double-buffered in LDS, K resident in LDS):
+//  phase 1 (per wave, per 32-key block, keys on the lane as in dkdv2): S' and dP' started from
+//    the row constants, P = exp2(S' c + U), dS = P dP', dV^T += dO^T P, dK^T += Q^T dS, and dS
+//    written transposed ([key][q]) to an LDS image;
+//  phase 2: dQ^T = K^T dS^T over all S keys, split over the 4 waves as (32-d half) x (key half);
+//    the two key-half partials are summed in a fixed order through LDS (deterministic).
+// S and dP are computed once per score block (five MFMA products instead of the seven of the
+// dq2 + dkdv2 pair), and Q, dO, O and LSE are read once per (batch, head).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
+                                                               0xF, 0xF, false));
+}
+// sum over the 32 lanes of a wave half (every lane of the half gets the total)
+__device__ __forceinline__ float sum32(float x) {
+  x += dppf<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dppf<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dppf<0x141>(x);  // row_half_mirror
+  x += dppf<0x140>(x);  // row_mirror
+  return x + __shfl_xor(x, 16, 64);
+}
+
+// dst += A B with the accumulator pinned to AGPRs: the 4*KB dK^T / dV^T tiles of a wave fill the
+// accumulator file, every other MFMA of the kernel is in VGPR form (attention.hip is built with
+// -mllvm -amdgpu-mfma-vgpr-form=1). hipcc pads nothing inside asm: s_nop 1 covers a VALU write
+// (bf16 packing of P / dS) or v_accvgpr_write (zero init) of an operand just before; the chain
+// on one accumulator needs no wait states; readers of the result wait via acc_fence().
+__device__ __forceinline__ void mfma_acc(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// wait states between the last MFMA writing `acc` and any other reader of it (16-pass XDL)
+__device__ __forceinline__ void acc_fence(f32x16& x, f32x16& y) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(x), "+a"(y));
+}
+
+template <int KB>
+constexpr size_t bwd3_lds() {
+  return (size_t)128 * KB * D * 2 + 4 * 32 * D * 2 + (size_t)128 * KB * 32 * 2 + 2 * 4 * 32 * 4 +
+         2 * 1024 * 4;
+}
+
+template <int KB>
+__global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ out, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, const uint8_t* __restrict__ key_valid,
+    const float* __restrict__ slopes, int H, float c, float scale, bf16* __restrict__ dqkv,
+    float* __restrict__ dbias_part) {
+  constexpr int S = 128 * KB;   // keys = queries of one (batch, head)
+  constexpr int KPW = 32 * KB;  // keys per wave
+  constexpr int NS = S / 32;    // query slices
+  constexpr int KS2 = S / 32;   // 16-key steps of one key half (phase 2)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Kimg = reinterpret_cast<bf16*>(smem);          // [S][64] swz
+  bf16* Qimg = Kimg + S * D;                            // [2][32][64] swz
+  bf16* Oimg = Qimg + 2 * 32 * D;                       // [2][32][64] dO, swz
+  bf16* dST = Oimg + 2 * 32 * D;                        // [S][32] dS^T, 8-B chunks XOR (row>>2)
+  float* rc = reinterpret_cast<float*>(dST + S * 32);  // [2][4][32] row constants (as dkdv2)
+  float* red = rc + 2 * 4 * 32;                         // [2][1024] dQ^T partials of key half 1
+
+  const int bh = blockIdx.x, h = bh % H, b = bh / H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kl = lane & 31, hh = lane >> 5;
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int ld = 3 * H * D;
+  const bf16* base = qkv + (size_t)b * S * ld;
+  const size_t obase = (size_t)b * S * (H * D) + h * D;
+  const float slope2 = slopes[h] * LOG2E;
+  const float invc = 1.f / c;
+  const float sl_t = slope2 * invc;
+  const float* lse_bh = lse + ((size_t)b * H + h) * S;
+
+  {  // K image of all S keys
+    constexpr int NCH = S * 8 / 256;
+    bf16x8 kt[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cc = tid + 256 * i;
+      kt[i] = *reinterpret_cast<const bf16x8*>(base + (size_t)(cc >> 3) * ld + H * D + h * D + (cc & 7) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cc = tid + 256 * i;
+      *reinterpret_cast<bf16x8*>(Kimg + swz(cc >> 3, (cc & 7) * 8)) = kt[i];
+    }
+  }
+  bf16x8 vf[KB][4];  // V of this wave's keys as the B operand of dP' (key on the lane)
+  unsigned padm = 0;  // bit kb: key wave*KPW + 32kb + kl is a pad key
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const int kj = wave * KPW + 32 * kb + kl;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      vf[kb][s] = *reinterpret_cast<const bf16x8*>(base + (size_t)kj * ld + 2 * H * D + h * D + 16 * s + 8 * hh);
+    if (key_valid && !key_valid[(size_t)b * S + kj]) padm |= 1u << kb;
+  }
+
+  // query-slice staging: thread -> (row sr, 16-B chunk sc) of Q, dO and O
+  struct SRegs { bf16x8 q, o, d; float l; };
+  const int sr = tid >> 3, sc = tid & 7;
+  auto load_slice = [&](int t, SRegs& x) {
+    const int q = 32 * t + sr;
+    x.q = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + sc * 8);
+    x.o = *reinterpret_cast<const bf16x8*>(out + obase + (size_t)q * (H * D) + sc * 8);
+    x.d = *reinterpret_cast<const bf16x8*>(dout + obase + (size_t)q * (H * D) + sc * 8);
+    x.l = lse_bh[q];
+  };
+  auto store_slice = [&](int buf, int t, const SRegs& x) {
+    *reinterpret_cast<bf16x8*>(Qimg + buf * 32 * D + swz(sr, sc * 8)) = x.q;
+    *reinterpret_cast<bf16x8*>(Oimg + buf * 32 * D + swz(sr, sc * 8)) = x.d;
+    float dl = 0.f;  // delta = rowsum(dO * O) over the row's 8 chunks (8 consecutive lanes)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl = fmaf((float)x.d[j], (float)x.o[j], dl);
+    dl += __shfl_xor(dl, 1, 64);
+    dl += __shfl_xor(dl, 2, 64);
+    dl += __shfl_xor(dl, 4, 64);
+    if (sc == 0) {
+      const float l2 = x.l * LOG2E, sq = slope2 * (float)(32 * t + sr);
+      float* R = rc + buf * 128 + sr;
+      R[0] = (-l2 - sq) * invc;  // query after the key block
+      R[32] = (-l2 + sq) * invc; // query before
+      R[64] = -l2 * invc;        // diagonal block
+      R[96] = -dl;
+    }
+  };
+
+  f32x16 dk[KB][2], dv[KB][2];
+  // sig[kb] = sum over the queries this lane holds of dS[q][key]: the dQ column sums of the
+  // bias gradient are sum_key K[key][d] * sum_q dS[q][key] (accumulated per key, summed in the
+  // epilogue), so no per-slice cross-lane reduction
+  float sig[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    sig[kb] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { dk[kb][0][i] = dk[kb][1][i] = dv[kb][0][i] = dv[kb][1][i] = 0.f; }
+  }
+  const int dth = wave & 1, kh2 = wave >> 1;  // phase-2 role: 32-d half, key half
+  const bf16* Kw = Kimg + wave * KPW * D;     // this wave's keys in the K image
+  bf16* dSTw = dST + wave * KPW * 32;         // ... and in the dS^T image
+  const bf16* Kh = Kimg + kh2 * (S / 2) * D;  // phase-2 key half
+  const bf16* dSTh = dST + kh2 * (S / 2) * 32;
+  {
+    SRegs x;
+    load_slice(0, x);
+    store_slice(0, 0, x);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < NS; ++t) {
+    const int buf = t & 1;
+    SRegs nx;
+    if (t + 1 < NS) load_slice(t + 1, nx);
+    const bf16* Q = Qimg + buf * 32 * D;
+    const bf16* O = Oimg + buf * 32 * D;
+    const float* RC = rc + buf * 128;
+    const int qb = 32 * t;
+    // ---- phase 1
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      // keep the scheduler from hoisting the next block's loads and MFMAs into this one: the
+      // 4*KB resident accumulators leave no registers for two blocks in flight
+      __builtin_amdgcn_sched_barrier(0);
+      const int kbase = wave * KPW + 32 * kb;  // uniform
+      const bool after = qb > kbase, before = qb < kbase;
+      const int sel = after ? 0 : (before ? 1 : 2);
+      f32x16 sa, pa;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(RC + sel * 32 + 8 * g4 + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 96 + 8 * g4 + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { sa[4 * g4 + e] = l4[e]; pa[4 * g4 + e] = d4[e]; }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        // kbase is a multiple of 32, so swz(kbase + kl, c) = kbase*D + swz(kl, c): written this
+        // way the block offset folds into the ds_read immediate instead of costing a register
+        const bf16x8 kr = *reinterpret_cast<const bf16x8*>(Kw + kb * 32 * D + swz(kl, 16 * s + 8 * hh));
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + swz(kl, 16 * s + 8 * hh));
+        const bf16x8 oa = *reinterpret_cast<const bf16x8*>(O + swz(kl, 16 * s + 8 * hh));
+        sa = mfma(qa, kr, sa);         // (S - LSE2 -+ slope2 q) / c   [q][key]
+        pa = mfma(oa, vf[kb][s], pa);  // dP - delta
+      }
+      const float kbias = ((padm >> kb) & 1) ? PAD_BIAS * LOG2E : 0.f;
+      float U = kbias;
+      if (after || before) {
+        U = fmaf(after ? slope2 : -slope2, (float)(kbase + kl), kbias);
+      } else {
+        // diagonal block (qb == kbase): q - k at register offset 0 is 4hh - kl. Opaque to the
+        // optimizer, which would otherwise keep the 16 loop-invariant |q - k| in registers
+        float lq = (float)(4 * hh - kl);
+        asm volatile("" : "+v"(lq));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sa[r] = fmaf(-sl_t, fabsf(lq + (float)aoff(r)), sa[r]);
+      }
+      bf16x8 pb[2], sb[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = ex2(fmaf(sa[r], c, U));
+        const float ds = p * pa[r];
+        pb[r >> 3][r & 7] = (bf16)p;
+        sb[r >> 3][r & 7] = (bf16)ds;
+        if (dbias_part) sig[kb] += ds;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int qrow = 16 * s2 + 4 * (g16 >> 1) + (i16 >> 2);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
+          const bf16x8 ao = cat(tr_read(O + swz(qrow, dcol)), tr_read(O + swz(qrow + 8, dcol)));
+          const bf16x8 aq = cat(tr_read(Q + swz(qrow, dcol)), tr_read(Q + swz(qrow + 8, dcol)));
+          mfma_acc(dv[kb][dt], ao, pb[s2]);
+          mfma_acc(dk[kb][dt], aq, sb[s2]);
+        }
+      }
+      // dS^T image: register group g holds q = 8g + 4hh + 0..3 of key kbase + kl (the chunk
+      // swizzle ((key >> 2) & 7) depends on kl only, kbase being a multiple of 32)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bf16x8& src = sb[g >> 1];
+        const bf16x4 v = {src[4 * (g & 1)], src[4 * (g & 1) + 1], src[4 * (g & 1) + 2], src[4 * (g & 1) + 3]};
+        *reinterpret_cast<bf16x4*>(dSTw + kb * 32 * 32 + kl * 32 + 4 * ((2 * g + hh) ^ ((kl >> 2) & 7))) = v;
+      }
+    }
+    __syncthreads();
+    // ---- phase 2: dQ^T[32 dth + d][q] over keys [kh2*S/2, (kh2+1)*S/2)
+    f32x16 dq;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[i] = 0.f;
+    {
+      const int dcol = 32 * dth + 16 * (g16 & 1) + 4 * (i16 & 3);
+      const int qc = 4 * (g16 & 1) + (i16 & 3);  // 8-B chunk of q = 16(g16&1) + 4(i16&3)
+      // rows 16ks + r (r = 4hh + (i16>>2), and + 8): swz(16ks + r, c) = 16ks*D + swz(r, c); the
+      // dS^T chunk swizzle ((row >> 2) & 7) = (4ks + (r >> 2)) & 7 alternates with ks & 1
+      const int rr = 4 * (g16 >> 1) + (i16 >> 2);
+      const int ka0 = swz(rr, dcol), ka1 = swz(rr + 8, dcol);
+      int sa0[2], sa1[2];
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        sa0[par] = rr * 32 + 4 * (qc ^ ((4 * par + (rr >> 2)) & 7));
+        sa1[par] = (rr + 8) * 32 + 4 * (qc ^ ((4 * par + ((rr + 8) >> 2)) & 7));
+      }
+#pragma unroll 2
+      for (int ks = 0; ks < KS2; ++ks) {
+        const int par = ks & 1;
+        const bf16x8 a = cat(tr_read(Kh + 16 * ks * D + ka0), tr_read(Kh + 16 * ks * D + ka1));
+        const bf16x8 bb = cat(tr_read(dSTh + 16 * ks * 32 + sa0[par]), tr_read(dSTh + 16 * ks * 32 + sa1[par]));
+        dq = mfma(a, bb, dq);
+      }
+    }
+    float* rw = red + dth * 1024;
+    if (kh2 == 1) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(rw + g * 256 + lane * 4) = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+    }
+    if (t + 1 < NS) store_slice(buf ^ 1, t + 1, nx);
+    __syncthreads();
+    if (kh2 == 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(rw + g * 256 + lane * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dq[4 * g + e] = (dq[4 * g + e] + v[e]) * scale;
+      }
+      bf16* row = dqkv + ((size_t)b * S + qb + kl) * ld + h * D + 32 * dth;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (bf16)dq[4 * g + e];
+        *reinterpret_cast<bf16x4*>(row + 8 * g + 4 * hh) = v;
+      }
+    }
+  }
+
+  // ---- dK, dV rows of this wave's keys
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) acc_fence(dk[kb][dt], dv[kb][dt]);
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    bf16* row = dqkv + ((size_t)b * S + wave * KPW + 32 * kb + kl) * ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 vk, vv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vk[e] = (bf16)(dk[kb][dt][4 * g + e] * scale);
+          vv[e] = (bf16)dv[kb][dt][4 * g + e];
+        }
+        *reinterpret_cast<bf16x4*>(row + H * D + 32 * dt + 8 * g + 4 * hh) = vk;
+        *reinterpret_cast<bf16x4*>(row + 2 * H * D + 32 * dt + 8 * g + 4 * hh) = vv;
+      }
+  }
+  if (dbias_part) {  // column sums per 128 keys: per-wave sums via LDS, then 4/KB waves per row
+    __syncthreads();  // the last slice's dQ partials in `red` have been read
+    float* cs = red;            // [wave][dQ, dK, dV][64]
+    float* sg = red + 4 * 192;  // [S] sum_q dS[q][key]
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const float tot = sig[kb] + __shfl_xor(sig[kb], 32, 64);
+      if (hh == 0) sg[wave * KPW + 32 * kb + kl] = tot;
+    }
+    __syncthreads();
+    {  // dQ part: lane = d, over this wave's keys: sum_key K[key][d] * sg[key]
+      float acc = 0.f;
+      for (int k = 0; k < KPW; ++k) {
+        const int key = wave * KPW + k;
+        acc = fmaf((float)Kimg[swz(key, lane)], sg[key], acc);
+      }
+      cs[(wave * 3) * 64 + lane] = acc * scale;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float xk = 0.f, xv = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) { xk += dk[kb][dt][r]; xv += dv[kb][dt][r]; }
+        xk = sum32(xk);
+        xv = sum32(xv);
+        if (kl == 0) {
+          cs[(wave * 3 + 1) * 64 + 32 * dt + aoff(r) + 4 * hh] = xk * scale;
+          cs[(wave * 3 + 2) * 64 + 32 * dt + aoff(r) + 4 * hh] = xv;
+        }
+      }
+    __syncthreads();
+    for (int i = tid; i < KB * 192; i += 256) {
+      const int j = i / 192, ts = (i >> 6) % 3, d = i & 63;
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4 / KB; ++w) sum += cs[((j * 4 / KB + w) * 3 + ts) * 64 + d];
+      dbias_part[((size_t)b * KB + j) * ld + ts * H * D + h * D + d] = sum;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- fp32 path
 // One thread per query (forward, dQ) or per key (dK/dV); K/V (or Q/dO) tiles staged in LDS.
 constexpr int F32_TILE = 64;
@@ -1539,6 +1886,21 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
   return DNA_OK;
 }
 
+template <int KB>
+static void launch_bwd3(const void* qkv, const void* out, const void* dout, const float* lse,
+                        const uint8_t* key_valid, const float* slopes, int batch, int heads, float c,
+                        float scale, void* dqkv, float* dbias_part, hipStream_t s) {
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((bwd3_bf16_kernel<KB>), dim3(batch * heads), dim3(256), bwd3_lds<KB>(), s,
+                     (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, key_valid, slopes,
+                     heads, c, scale, (bf16*)dqkv, dbias_part);
+}
+
 extern "C" int dna_attn_bwd_ex(const void* qkv, const void* out, const void* dout,
                                const float* lse, const uint8_t* key_valid, const float* slopes,
                                int batch, int seqlen, int heads, int head_dim, int dtype,
@@ -1550,8 +1912,19 @@ extern "C" int dna_attn_bwd_ex(const void* qkv, const void* out, const void* dou
   hipStream_t s = as_stream(stream);
   const int rows = batch * seqlen;
   const int nd = (rows * heads + 255) / 256;
-  static const bool bwd_v1 = getenv("DNA_ATTN_BWD") && atoi(getenv("DNA_ATTN_BWD")) == 1;
-  if (dtype == DNA_BF16 && !bwd_v1) {
+  // DNA_ATTN_BWD: 3 (default) fused one-workgroup-per-(batch, head) kernel where S is 128, 256
+  // or 512, else the v2 pair; 2 forces the v2 pair, 1 the v1 pair (benchmarks / A/B)
+  static const int bwd_ver = getenv("DNA_ATTN_BWD") ? atoi(getenv("DNA_ATTN_BWD")) : 3;
+  const bool bwd_v1 = bwd_ver == 1;
+  if (dtype == DNA_BF16 && bwd_ver == 3 && (seqlen == 128 || seqlen == 256 || seqlen == 512)) {
+    const float c = softmax_scale * LOG2E;
+    if (seqlen == 512)
+      launch_bwd3<4>(qkv, out, dout, lse, key_valid, slopes, batch, heads, c, softmax_scale, dqkv, dbias_part, s);
+    else if (seqlen == 256)
+      launch_bwd3<2>(qkv, out, dout, lse, key_valid, slopes, batch, heads, c, softmax_scale, dqkv, dbias_part, s);
+    else
+      launch_bwd3<1>(qkv, out, dout, lse, key_valid, slopes, batch, heads, c, softmax_scale, dqkv, dbias_part, s);
+  } else if (dtype == DNA_BF16 && !bwd_v1) {
     // dQ kernel also produces delta = rowsum(dO*O), consumed by the dK/dV kernel after it.
     // 8-wave workgroups (256 queries / keys each) when the sequence fills them: half the
     // K/V and Q/dO re-streaming of 4-wave ones. Colsum scratch: NW*32 rows x 64 floats.
