@@ -1366,18 +1366,33 @@ __device__ __forceinline__ void acc_fence(f32x16& x, f32x16& y) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(x), "+a"(y));
 }
 
+// LDS: K image, Q/dO images, dS^T image, row constants, then (at >= 64 KiB, past the epilogue's
+// 64 KiB dK/dV staging that reuses the start) the dQ partials and the dS row sums
+template <int KB>
+constexpr size_t bwd3_red_off() {
+  constexpr size_t a = (size_t)128 * KB * D * 2 + 4 * 32 * D * 2 + (size_t)128 * KB * 32 * 2 + 2 * 4 * 32 * 4;
+  return a > 65536 ? a : 65536;
+}
+constexpr int CS_LD = 36;  // colsum staging row stride in floats ([d][key], 16-B aligned rows)
 template <int KB>
 constexpr size_t bwd3_lds() {
-  return (size_t)128 * KB * D * 2 + 4 * 32 * D * 2 + (size_t)128 * KB * 32 * 2 + 2 * 4 * 32 * 4 +
-         2 * 1024 * 4;
+  return bwd3_red_off<KB>() + 2 * 1024 * 4 + 4 * 64 * CS_LD * 4;
 }
 
-template <int KB>
+#ifndef DNA_BWD3_PIPE_SB
+#define DNA_BWD3_PIPE_SB 0
+#endif
+constexpr bool PIPE_SB = DNA_BWD3_PIPE_SB;  // per-step sched_barriers in the pipelined phase 1
+
+template <int KB, int DBV>
 __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ out, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const uint8_t* __restrict__ key_valid,
     const float* __restrict__ slopes, int H, float c, float scale, bf16* __restrict__ dqkv,
     float* __restrict__ dbias_part) {
+  constexpr bool DB = DBV == 1;          // fused bias-gradient column sums
+  constexpr bool DBL = DB || DBV == 2;   // (DBV 2 / 3: timing variants, loop part / epilogue part)
+  constexpr bool DBE = DB || DBV == 3;
   constexpr int S = 128 * KB;   // keys = queries of one (batch, head)
   constexpr int KPW = 32 * KB;  // keys per wave
   constexpr int NS = S / 32;    // query slices
@@ -1388,7 +1403,8 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
   bf16* Oimg = Qimg + 2 * 32 * D;                       // [2][32][64] dO, swz
   bf16* dST = Oimg + 2 * 32 * D;                        // [S][32] dS^T, 8-B chunks XOR (row>>2)
   float* rc = reinterpret_cast<float*>(dST + S * 32);  // [2][4][32] row constants (as dkdv2)
-  float* red = rc + 2 * 4 * 32;                         // [2][1024] dQ^T partials of key half 1
+  float* red = reinterpret_cast<float*>(smem + bwd3_red_off<KB>());  // [2][1024] dQ^T partials
+                                                                      // of key half 1
 
   const int bh = blockIdx.x, h = bh % H, b = bh / H;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1430,23 +1446,26 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
 
   // query-slice staging: thread -> (row sr, 16-B chunk sc) of Q, dO and O
   struct SRegs { bf16x8 q, o, d; float l; };
-  const int sr = tid >> 3, sc = tid & 7;
-  auto load_slice = [&](int t, SRegs& x) {
+  // the staging indices come from an opaque copy of tid per slice (see `tid_t` in the loop):
+  // otherwise the compiler keeps every per-lane 64-bit row address live across the whole loop
+  auto load_slice = [&](int t, SRegs& x, int tid_t) {
+    const int sr = tid_t >> 3, sc = tid_t & 7;
     const int q = 32 * t + sr;
     x.q = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + sc * 8);
     x.o = *reinterpret_cast<const bf16x8*>(out + obase + (size_t)q * (H * D) + sc * 8);
     x.d = *reinterpret_cast<const bf16x8*>(dout + obase + (size_t)q * (H * D) + sc * 8);
     x.l = lse_bh[q];
   };
-  auto store_slice = [&](int buf, int t, const SRegs& x) {
+  auto store_slice = [&](int buf, int t, const SRegs& x, int tid_t) {
+    const int sr = tid_t >> 3, sc = tid_t & 7;
     *reinterpret_cast<bf16x8*>(Qimg + buf * 32 * D + swz(sr, sc * 8)) = x.q;
     *reinterpret_cast<bf16x8*>(Oimg + buf * 32 * D + swz(sr, sc * 8)) = x.d;
     float dl = 0.f;  // delta = rowsum(dO * O) over the row's 8 chunks (8 consecutive lanes)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dl = fmaf((float)x.d[j], (float)x.o[j], dl);
-    dl += __shfl_xor(dl, 1, 64);
-    dl += __shfl_xor(dl, 2, 64);
-    dl += __shfl_xor(dl, 4, 64);
+    dl += dppf<0xB1>(dl);   // quad_perm [1,0,3,2]
+    dl += dppf<0x4E>(dl);   // quad_perm [2,3,0,1]: quad sum in every lane
+    dl += dppf<0x141>(dl);  // row_half_mirror: + the other quad of the 8-lane row group
     if (sc == 0) {
       const float l2 = x.l * LOG2E, sq = slope2 * (float)(32 * t + sr);
       float* R = rc + buf * 128 + sr;
@@ -1458,9 +1477,9 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
   };
 
   f32x16 dk[KB][2], dv[KB][2];
-  // sig[kb] = sum over the queries this lane holds of dS[q][key]: the dQ column sums of the
-  // bias gradient are sum_key K[key][d] * sum_q dS[q][key] (accumulated per key, summed in the
-  // epilogue), so no per-slice cross-lane reduction
+  // sig[kb] = sum over the queries this lane holds of dS[q][key]: the dQ column sums of the bias
+  // gradient are sum_key K[key][d] * sum_q dS[q][key] (per-key sums, contracted with K in the
+  // epilogue), so the loop carries KB floats instead of per-slice cross-lane reductions
   float sig[KB];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
@@ -1475,86 +1494,115 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
   const bf16* dSTh = dST + kh2 * (S / 2) * 32;
   {
     SRegs x;
-    load_slice(0, x);
-    store_slice(0, 0, x);
+    load_slice(0, x, tid);
+    store_slice(0, 0, x, tid);
   }
   __syncthreads();
 
   for (int t = 0; t < NS; ++t) {
     const int buf = t & 1;
+    int tid_t = tid;  // opaque per slice: lane-derived values are recomputed, not kept live
+    asm volatile("" : "+v"(tid_t));
+    const int kl_t = tid_t & 31;
+    unsigned padm_t = padm;
+    asm volatile("" : "+v"(padm_t));
     SRegs nx;
-    if (t + 1 < NS) load_slice(t + 1, nx);
+    if (t + 1 < NS) load_slice(t + 1, nx, tid_t);
     const bf16* Q = Qimg + buf * 32 * D;
     const bf16* O = Oimg + buf * 32 * D;
     const float* RC = rc + buf * 128;
     const int qb = 32 * t;
-    // ---- phase 1
+    // ---- phase 1, software-pipelined over the key blocks: iteration kb computes S'/dP' of block
+    // kb (8 MFMAs), then issues the 8 dV/dK MFMAs of block kb-1 one per step, each followed by
+    // the exp / dS work of two scores of block kb, so the softmax tail runs under the matrix pipe
+    // (one wave per SIMD: overlap has to come from this wave's own instruction order; the
+    // sched_barriers keep the compiler from regrouping it)
+    bf16x8 pbp[2], sbp[2];  // P and dS (bf16) of the previous block
+    const int tq = 4 * (g16 >> 1) + (i16 >> 2);  // tr-read row of lane
+    auto tr_pair = [&](const bf16* img, int j) {  // A operand (dO^T or Q^T) of pair j = (s2, dt)
+      const int qrow = 16 * (j >> 1) + tq;
+      const int dcol = 32 * (j & 1) + 16 * (g16 & 1) + 4 * (i16 & 3);
+      return cat(tr_read(img + swz(qrow, dcol)), tr_read(img + swz(qrow + 8, dcol)));
+    };
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      // keep the scheduler from hoisting the next block's loads and MFMAs into this one: the
-      // 4*KB resident accumulators leave no registers for two blocks in flight
+    for (int kb = 0; kb <= KB; ++kb) {
       __builtin_amdgcn_sched_barrier(0);
       const int kbase = wave * KPW + 32 * kb;  // uniform
       const bool after = qb > kbase, before = qb < kbase;
-      const int sel = after ? 0 : (before ? 1 : 2);
       f32x16 sa, pa;
+      float U = 0.f;
+      if (kb < KB) {
+        const int sel = after ? 0 : (before ? 1 : 2);
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(RC + sel * 32 + 8 * g4 + 4 * hh);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 96 + 8 * g4 + 4 * hh);
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(RC + sel * 32 + 8 * g4 + 4 * hh);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 96 + 8 * g4 + 4 * hh);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { sa[4 * g4 + e] = l4[e]; pa[4 * g4 + e] = d4[e]; }
-      }
+          for (int e = 0; e < 4; ++e) { sa[4 * g4 + e] = l4[e]; pa[4 * g4 + e] = d4[e]; }
+        }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        // kbase is a multiple of 32, so swz(kbase + kl, c) = kbase*D + swz(kl, c): written this
-        // way the block offset folds into the ds_read immediate instead of costing a register
-        const bf16x8 kr = *reinterpret_cast<const bf16x8*>(Kw + kb * 32 * D + swz(kl, 16 * s + 8 * hh));
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + swz(kl, 16 * s + 8 * hh));
-        const bf16x8 oa = *reinterpret_cast<const bf16x8*>(O + swz(kl, 16 * s + 8 * hh));
-        sa = mfma(qa, kr, sa);         // (S - LSE2 -+ slope2 q) / c   [q][key]
-        pa = mfma(oa, vf[kb][s], pa);  // dP - delta
-      }
-      const float kbias = ((padm >> kb) & 1) ? PAD_BIAS * LOG2E : 0.f;
-      float U = kbias;
-      if (after || before) {
-        U = fmaf(after ? slope2 : -slope2, (float)(kbase + kl), kbias);
-      } else {
-        // diagonal block (qb == kbase): q - k at register offset 0 is 4hh - kl. Opaque to the
-        // optimizer, which would otherwise keep the 16 loop-invariant |q - k| in registers
-        float lq = (float)(4 * hh - kl);
-        asm volatile("" : "+v"(lq));
+        for (int s = 0; s < 4; ++s) {
+          // kbase is a multiple of 32, so swz(kbase + kl, c) = kbase*D + swz(kl, c): written this
+          // way the block offset folds into the ds_read immediate instead of costing a register
+          const bf16x8 kr = *reinterpret_cast<const bf16x8*>(Kw + kb * 32 * D + swz(kl, 16 * s + 8 * hh));
+          const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + swz(kl, 16 * s + 8 * hh));
+          const bf16x8 oa = *reinterpret_cast<const bf16x8*>(O + swz(kl, 16 * s + 8 * hh));
+          sa = mfma(qa, kr, sa);         // (S - LSE2 -+ slope2 q) / c   [q][key]
+          pa = mfma(oa, vf[kb][s], pa);  // dP - delta
+        }
+        const float kbias = ((padm_t >> kb) & 1) ? PAD_BIAS * LOG2E : 0.f;
+        U = (after || before) ? fmaf(after ? slope2 : -slope2, (float)(kbase + kl_t), kbias) : kbias;
+        if (!after && !before) {
+          // diagonal block (qb == kbase): q - k at register offset 0 is 4hh - kl. Opaque to the
+          // optimizer, which would otherwise keep the 16 loop-invariant |q - k| in registers
+          float lq = (float)(4 * hh - kl);
+          asm volatile("" : "+v"(lq));
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sa[r] = fmaf(-sl_t, fabsf(lq + (float)aoff(r)), sa[r]);
-      }
-      bf16x8 pb[2], sb[2];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = ex2(fmaf(sa[r], c, U));
-        const float ds = p * pa[r];
-        pb[r >> 3][r & 7] = (bf16)p;
-        sb[r >> 3][r & 7] = (bf16)ds;
-        if (dbias_part) sig[kb] += ds;
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int qrow = 16 * s2 + 4 * (g16 >> 1) + (i16 >> 2);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const int dcol = 32 * dt + 16 * (g16 & 1) + 4 * (i16 & 3);
-          const bf16x8 ao = cat(tr_read(O + swz(qrow, dcol)), tr_read(O + swz(qrow + 8, dcol)));
-          const bf16x8 aq = cat(tr_read(Q + swz(qrow, dcol)), tr_read(Q + swz(qrow + 8, dcol)));
-          mfma_acc(dv[kb][dt], ao, pb[s2]);
-          mfma_acc(dk[kb][dt], aq, sb[s2]);
+          for (int r = 0; r < 16; ++r) sa[r] = fmaf(-sl_t, fabsf(lq + (float)aoff(r)), sa[r]);
         }
       }
-      // dS^T image: register group g holds q = 8g + 4hh + 0..3 of key kbase + kl (the chunk
-      // swizzle ((key >> 2) & 7) depends on kl only, kbase being a multiple of 32)
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 pb[2], sb[2];
+      bf16x8 ao, aq;
+      float ssum = 0.f;
+      if (kb > 0) { ao = tr_pair(O, 0); aq = tr_pair(Q, 0); }
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const bf16x8& src = sb[g >> 1];
-        const bf16x4 v = {src[4 * (g & 1)], src[4 * (g & 1) + 1], src[4 * (g & 1) + 2], src[4 * (g & 1) + 3]};
-        *reinterpret_cast<bf16x4*>(dSTw + kb * 32 * 32 + kl * 32 + 4 * ((2 * g + hh) ^ ((kl >> 2) & 7))) = v;
+      for (int i = 0; i < 8; ++i) {
+        if (kb > 0) {  // dV/dK MFMA i of block kb-1: pair j = i >> 1 = (s2, dt), dV then dK
+          const int j = i >> 1;
+          if ((i & 1) == 0) {
+            mfma_acc(dv[kb - 1][j & 1], ao, pbp[j >> 1]);
+          } else {
+            mfma_acc(dk[kb - 1][j & 1], aq, sbp[j >> 1]);
+            if (j < 3) { ao = tr_pair(O, j + 1); aq = tr_pair(Q, j + 1); }
+          }
+        }
+        if (kb < KB) {  // scores 2i, 2i+1 of block kb
+#pragma unroll
+          for (int r = 2 * i; r < 2 * i + 2; ++r) {
+            const float pr = ex2(fmaf(sa[r], c, U));
+            const float ds = pr * pa[r];
+            pb[r >> 3][r & 7] = (bf16)pr;
+            sb[r >> 3][r & 7] = (bf16)ds;
+            if (DBL) ssum += ds;
+          }
+        }
+        if (PIPE_SB) __builtin_amdgcn_sched_barrier(0);
+      }
+      if (kb > 0) {
+        // dS^T image of block kb-1: register group g holds q = 8g + 4hh + 0..3 of key kl (the
+        // chunk swizzle ((key >> 2) & 7) depends on kl only, blocks being 32-aligned)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const bf16x8& src = sbp[g >> 1];
+          const bf16x4 v = {src[4 * (g & 1)], src[4 * (g & 1) + 1], src[4 * (g & 1) + 2], src[4 * (g & 1) + 3]};
+          *reinterpret_cast<bf16x4*>(dSTw + (kb - 1) * 32 * 32 + kl * 32 + 4 * ((2 * g + hh) ^ ((kl >> 2) & 7))) = v;
+        }
+      }
+      if (kb < KB) {
+        if (DBL) sig[kb] += ssum;
+        pbp[0] = pb[0]; pbp[1] = pb[1];
+        sbp[0] = sb[0]; sbp[1] = sb[1];
       }
     }
     __syncthreads();
@@ -1589,7 +1637,7 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<f32x4*>(rw + g * 256 + lane * 4) = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
     }
-    if (t + 1 < NS) store_slice(buf ^ 1, t + 1, nx);
+    if (t + 1 < NS) store_slice(buf ^ 1, t + 1, nx, tid_t);
     __syncthreads();
     if (kh2 == 0) {
 #pragma unroll
@@ -1631,38 +1679,63 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
         *reinterpret_cast<bf16x4*>(row + 2 * H * D + 32 * dt + 8 * g + 4 * hh) = vv;
       }
   }
-  if (dbias_part) {  // column sums per 128 keys: per-wave sums via LDS, then 4/KB waves per row
+  if (DBE) {  // column sums per 128 keys: per-wave sums via LDS, then 4/KB waves per row
+    // re-read the accumulators below instead of keeping the 256 values read for the stores live
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) asm volatile("" : "+a"(dk[kb][dt]), "+a"(dv[kb][dt]));
     __syncthreads();  // the last slice's dQ partials in `red` have been read
-    float* cs = red;            // [wave][dQ, dK, dV][64]
-    float* sg = red + 4 * 192;  // [S] sum_q dS[q][key]
+    // lane ids opaque here, so no epilogue address is computed (and kept live) before the loop
+    int lane_e = lane;
+    asm volatile("" : "+v"(lane_e));
+    const int kl_e = lane_e & 31, hh_e = lane_e >> 5;
+    float* cs = red;  // [wave][dQ, dK, dV][64]
+    // per tensor: each lane_e writes its per-key partials (key kl_e) into a wave-private [64 d][key]
+    // image, then lane_e = d sums its row of 32 keys (LDS is in order within a wave: no barriers)
+    float* st = red + 2 * 1024 + wave * 64 * CS_LD;
+    auto rowsum = [&](float* dst) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(st + lane_e * CS_LD);
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      const float tot = sig[kb] + __shfl_xor(sig[kb], 32, 64);
-      if (hh == 0) sg[wave * KPW + 32 * kb + kl] = tot;
-    }
-    __syncthreads();
-    {  // dQ part: lane = d, over this wave's keys: sum_key K[key][d] * sg[key]
-      float acc = 0.f;
-      for (int k = 0; k < KPW; ++k) {
-        const int key = wave * KPW + k;
-        acc = fmaf((float)Kimg[swz(key, lane)], sg[key], acc);
+      for (int k = 4; k < 32; k += 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(st + lane_e * CS_LD + k);
+        a[0] += v[0]; a[1] += v[1]; a[2] += v[2]; a[3] += v[3];
       }
-      cs[(wave * 3) * 64 + lane] = acc * scale;
-    }
+      *dst = (a[0] + a[1]) + (a[2] + a[3]);
+    };
+    {  // dQ part: sum_kb K[key][d] * sigma[key] over this lane_e's half of d; sigma needs both lane_e
+       // halves' query rows
+      float sgm[KB];
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+      for (int kb = 0; kb < KB; ++kb) sgm[kb] = sig[kb] + __shfl_xor(sig[kb], 32, 64);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float xk = 0.f, xv = 0.f;
+      for (int cc = 0; cc < 4; ++cc) {
+        float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) { xk += dk[kb][dt][r]; xv += dv[kb][dt][r]; }
-        xk = sum32(xk);
-        xv = sum32(xv);
-        if (kl == 0) {
-          cs[(wave * 3 + 1) * 64 + 32 * dt + aoff(r) + 4 * hh] = xk * scale;
-          cs[(wave * 3 + 2) * 64 + 32 * dt + aoff(r) + 4 * hh] = xv;
+        for (int kb = 0; kb < KB; ++kb) {
+          const int r = wave * KPW + 32 * kb + kl_e;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(Kimg + r * D + (((4 * hh_e + cc) ^ swz_key(r)) << 3));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], sgm[kb], a8[e]);
         }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) st[(32 * hh_e + 8 * cc + e) * CS_LD + kl_e] = a8[e] * scale;
       }
+      rowsum(cs + (wave * 3) * 64 + lane_e);
+    }
+#pragma unroll
+    for (int ts = 0; ts < 2; ++ts) {  // dK (scaled), dV
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float sum = 0.f;
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) sum += ts == 0 ? dk[kb][dt][r] : dv[kb][dt][r];
+          st[(32 * dt + aoff(r) + 4 * hh_e) * CS_LD + kl_e] = ts == 0 ? sum * scale : sum;
+        }
+      rowsum(cs + (wave * 3 + 1 + ts) * 64 + lane_e);
+    }
     __syncthreads();
     for (int i = tid; i < KB * 192; i += 256) {
       const int j = i / 192, ts = (i >> 6) % 3, d = i & 63;
@@ -1891,14 +1964,29 @@ static void launch_bwd3(const void* qkv, const void* out, const void* dout, cons
                         const uint8_t* key_valid, const float* slopes, int batch, int heads, float c,
                         float scale, void* dqkv, float* dbias_part, hipStream_t s) {
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB>,
+    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB, 0>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
+    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
+    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
+    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB, 3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
     return true;
   }();
   (void)attr;
-  hipLaunchKernelGGL((bwd3_bf16_kernel<KB>), dim3(batch * heads), dim3(256), bwd3_lds<KB>(), s,
-                     (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, key_valid, slopes,
-                     heads, c, scale, (bf16*)dqkv, dbias_part);
+  // DNA_ATTN_DBV (timing only): 2 / 3 run the loop / epilogue part of the bias-gradient sums
+  static const int dbv = getenv("DNA_ATTN_DBV") ? atoi(getenv("DNA_ATTN_DBV")) : 1;
+  const dim3 grid(batch * heads);
+  const size_t lds = bwd3_lds<KB>();
+  auto args = [&](auto kern, float* part) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, (const bf16*)qkv, (const bf16*)out,
+                       (const bf16*)dout, lse, key_valid, slopes, heads, c, scale, (bf16*)dqkv, part);
+  };
+  if (!dbias_part) args(bwd3_bf16_kernel<KB, 0>, nullptr);
+  else if (dbv == 2) args(bwd3_bf16_kernel<KB, 2>, dbias_part);
+  else if (dbv == 3) args(bwd3_bf16_kernel<KB, 3>, dbias_part);
+  else args(bwd3_bf16_kernel<KB, 1>, dbias_part);
 }
 
 extern "C" int dna_attn_bwd_ex(const void* qkv, const void* out, const void* dout,
