@@ -1374,11 +1374,30 @@ constexpr size_t bwd3_red_off() {
   return a > 65536 ? a : 65536;
 }
 constexpr int CS_LD = 36;  // colsum staging row stride in floats ([d][key], 16-B aligned rows)
+// epilogue staging: for KB = 4 it reuses the Q/dO/dS^T images (48 KiB, dead by then), else it
+// gets its own region after the dS row sums
+template <int KB>
+constexpr bool bwd3_stage_alias() { return (size_t)4 * 32 * D * 2 + (size_t)128 * KB * 32 * 2 >= 4 * 64 * CS_LD * 4; }
 template <int KB>
 constexpr size_t bwd3_lds() {
-  return bwd3_red_off<KB>() + 2 * 1024 * 4 + 4 * 64 * CS_LD * 4;
+  return bwd3_red_off<KB>() + 2 * 1024 * 4 + (size_t)128 * KB * 2 * 4 +
+         (bwd3_stage_alias<KB>() ? 0 : 4 * 64 * CS_LD * 4);
 }
 
+#ifndef DNA_BWD3_STAMP
+#define DNA_BWD3_STAMP 0
+#endif
+#if DNA_BWD3_STAMP
+// timing probe (debug builds only): s_memtime at phase boundaries of block 0's waves
+__device__ unsigned long long g_bwd3_stamps[4][16][6];
+#define BWD3_STAMP(t, k)                                                              \
+  do {                                                                                \
+    const unsigned long long ts_ = __builtin_amdgcn_s_memtime();                     \
+    if (blockIdx.x == 0 && lane == 0 && (t) < 16) g_bwd3_stamps[wave][(t)][(k)] = ts_; \
+  } while (0)
+#else
+#define BWD3_STAMP(t, k) do {} while (0)
+#endif
 #ifndef DNA_BWD3_PIPE_SB
 #define DNA_BWD3_PIPE_SB 0
 #endif
@@ -1480,10 +1499,13 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
   // sig[kb] = sum over the queries this lane holds of dS[q][key]: the dQ column sums of the bias
   // gradient are sum_key K[key][d] * sum_q dS[q][key] (per-key sums, contracted with K in the
   // epilogue), so the loop carries KB floats instead of per-slice cross-lane reductions
-  float sig[KB];
+  // (kept in LDS, sigl[key][hh], read early in each block and written back by the owner lane:
+  // four loop-carried registers more push the loop over the register file)
+  float* sigl = red + 2 * 1024;
+  if (DBL)
+    for (int i = tid; i < 2 * S; i += 256) sigl[i] = 0.f;
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
-    sig[kb] = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) { dk[kb][0][i] = dk[kb][1][i] = dv[kb][0][i] = dv[kb][1][i] = 0.f; }
   }
@@ -1500,6 +1522,7 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
   __syncthreads();
 
   for (int t = 0; t < NS; ++t) {
+    BWD3_STAMP(t, 0);
     const int buf = t & 1;
     int tid_t = tid;  // opaque per slice: lane-derived values are recomputed, not kept live
     asm volatile("" : "+v"(tid_t));
@@ -1565,6 +1588,7 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
       bf16x8 pb[2], sb[2];
       bf16x8 ao, aq;
       float ssum = 0.f;
+      const float sold = (DBL && kb < KB) ? sigl[2 * (kbase + kl_t) + hh] : 0.f;
       if (kb > 0) { ao = tr_pair(O, 0); aq = tr_pair(Q, 0); }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -1600,12 +1624,14 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
         }
       }
       if (kb < KB) {
-        if (DBL) sig[kb] += ssum;
+        if (DBL) sigl[2 * (kbase + kl_t) + hh] = sold + ssum;
         pbp[0] = pb[0]; pbp[1] = pb[1];
         sbp[0] = sb[0]; sbp[1] = sb[1];
       }
     }
+    BWD3_STAMP(t, 1);
     __syncthreads();
+    BWD3_STAMP(t, 2);
     // ---- phase 2: dQ^T[32 dth + d][q] over keys [kh2*S/2, (kh2+1)*S/2)
     f32x16 dq;
 #pragma unroll
@@ -1623,38 +1649,48 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
         sa0[par] = rr * 32 + 4 * (qc ^ ((4 * par + (rr >> 2)) & 7));
         sa1[par] = (rr + 8) * 32 + 4 * (qc ^ ((4 * par + ((rr + 8) >> 2)) & 7));
       }
-#pragma unroll 2
-      for (int ks = 0; ks < KS2; ++ks) {
+      // operands of step ks + PF are read while step ks multiplies (LDS latency off the chain)
+      constexpr int PF = KS2 < 4 ? KS2 : 4;
+      bf16x8 ra[PF], rb[PF];
+      auto rd = [&](int ks, bf16x8& a, bf16x8& bb) {
         const int par = ks & 1;
-        const bf16x8 a = cat(tr_read(Kh + 16 * ks * D + ka0), tr_read(Kh + 16 * ks * D + ka1));
-        const bf16x8 bb = cat(tr_read(dSTh + 16 * ks * 32 + sa0[par]), tr_read(dSTh + 16 * ks * 32 + sa1[par]));
-        dq = mfma(a, bb, dq);
+        a = cat(tr_read(Kh + 16 * ks * D + ka0), tr_read(Kh + 16 * ks * D + ka1));
+        bb = cat(tr_read(dSTh + 16 * ks * 32 + sa0[par]), tr_read(dSTh + 16 * ks * 32 + sa1[par]));
+      };
+#pragma unroll
+      for (int ks = 0; ks < PF; ++ks) rd(ks, ra[ks], rb[ks]);
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks) {
+        dq = mfma(ra[ks % PF], rb[ks % PF], dq);
+        if (ks + PF < KS2) rd(ks + PF, ra[ks % PF], rb[ks % PF]);
       }
     }
+    // key-half partials: the two waves of a 32-d half each finish two of the four register
+    // groups (g = 2*kh2, 2*kh2 + 1), exchanging the other two through LDS; own + partner is the
+    // same fp32 sum either way round (a + b == b + a), so dQ stays deterministic
     float* rw = red + dth * 1024;
-    if (kh2 == 1) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<f32x4*>(rw + g * 256 + lane * 4) = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+    for (int g2 = 0; g2 < 2; ++g2) {
+      const int g = 2 * (1 - kh2) + g2;
+      *reinterpret_cast<f32x4*>(rw + g * 256 + lane * 4) = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
     }
+    BWD3_STAMP(t, 3);
     if (t + 1 < NS) store_slice(buf ^ 1, t + 1, nx, tid_t);
     __syncthreads();
-    if (kh2 == 0) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(rw + g * 256 + lane * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dq[4 * g + e] = (dq[4 * g + e] + v[e]) * scale;
-      }
+    BWD3_STAMP(t, 4);
+    {
       bf16* row = dqkv + ((size_t)b * S + qb + kl) * ld + h * D + 32 * dth;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 v;
+      for (int g2 = 0; g2 < 2; ++g2) {
+        const int g = 2 * kh2 + g2;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(rw + g * 256 + lane * 4);
+        bf16x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (bf16)dq[4 * g + e];
-        *reinterpret_cast<bf16x4*>(row + 8 * g + 4 * hh) = v;
+        for (int e = 0; e < 4; ++e) o[e] = (bf16)((dq[4 * g + e] + v[e]) * scale);
+        *reinterpret_cast<bf16x4*>(row + 8 * g + 4 * hh) = o;
       }
     }
+    BWD3_STAMP(t, 5);
   }
 
   // ---- dK, dV rows of this wave's keys
@@ -1693,7 +1729,8 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
     float* cs = red;  // [wave][dQ, dK, dV][64]
     // per tensor: each lane_e writes its per-key partials (key kl_e) into a wave-private [64 d][key]
     // image, then lane_e = d sums its row of 32 keys (LDS is in order within a wave: no barriers)
-    float* st = red + 2 * 1024 + wave * 64 * CS_LD;
+    float* st = (bwd3_stage_alias<KB>() ? reinterpret_cast<float*>(Qimg)
+                                        : red + 2 * 1024 + 2 * S) + wave * 64 * CS_LD;
     auto rowsum = [&](float* dst) {
       f32x4 a = *reinterpret_cast<const f32x4*>(st + lane_e * CS_LD);
 #pragma unroll
@@ -1707,7 +1744,10 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
        // halves' query rows
       float sgm[KB];
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) sgm[kb] = sig[kb] + __shfl_xor(sig[kb], 32, 64);
+      for (int kb = 0; kb < KB; ++kb) {
+        const int key = wave * KPW + 32 * kb + kl_e;
+        sgm[kb] = sigl[2 * key] + sigl[2 * key + 1];
+      }
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
         float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -2072,6 +2112,12 @@ extern "C" int dna_attn_bwd(const void* qkv, const void* out, const void* dout, 
   return dna_attn_bwd_ex(qkv, out, dout, lse, key_valid, slopes, batch, seqlen, heads, head_dim,
                          dtype, softmax_scale, dqkv, delta_ws, nullptr, stream);
 }
+
+#if DNA_BWD3_STAMP
+extern "C" int dna_attn_debug_stamps(unsigned long long* out) {  // debug builds only
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd3_stamps), sizeof(g_bwd3_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int dna_attn_dbias_part_rows(int batch, int seqlen) {
   return batch * ((seqlen + BQ - 1) / BQ);
