@@ -33,8 +33,9 @@ def main():
             print(f"  {c:28s} {cs[c]:16.4g}")
         g = cs.get("GRBM_GUI_ACTIVE")
         if g and "SQ_VALU_MFMA_BUSY_CYCLES" in cs:
-            # MFMA busy is summed over SIMDs (4 per CU, 256 CUs)
-            print(f"  -> MFMA busy frac          {cs['SQ_VALU_MFMA_BUSY_CYCLES'] / (g * 1024):.3f}")
+            # MFMA busy is summed over SIMDs (4 per CU, 256 CUs); GRBM_GUI_ACTIVE over the 8 XCDs
+            # (the forward GEMM's ratio x 8 matches its HIP-event TF/s at the measured clock)
+            print(f"  -> MFMA busy frac          {cs['SQ_VALU_MFMA_BUSY_CYCLES'] / (g / 8 * 1024):.3f}")
         if cs.get("SQ_LDS_IDX_ACTIVE"):
             print(f"  -> LDS bank-conflict share {cs.get('SQ_LDS_BANK_CONFLICT', 0) / cs['SQ_LDS_IDX_ACTIVE']:.3f}")
         if cs.get("SQ_WAVE_CYCLES"):
