@@ -64,6 +64,32 @@ def main():
           f"kernels {own:.1f} ms ({own / (dt * 1e3):.0%}): "
           + ", ".join(f"{k} {t:.3f} ms x{n / a.steps:.0f}" for k, (n, t, u, kind) in summ.items()),
           flush=True)
+    # one JSON line in bench.py's format: HBM roofline of the dominant HIP kernel family
+    # (algorithmic bytes per launch from the op's own accounting / HIP-event average duration)
+    kernels = {}
+    for k, (n, t, u, kind) in summ.items():
+        rate = u / (t * 1e-3)
+        kernels[k] = {"launches_per_step": n / a.steps, "avg_ms": round(t, 4),
+                      "share_of_step": round(n * t / a.steps / (dt * 1e3), 4)}
+        if kind == "flop":
+            kernels[k].update(bound="mfma", achieved_tflops=round(rate / 1e12, 1), frac=round(rate / 2.5e15, 4))
+        else:
+            kernels[k].update(bound="hbm", achieved_gbs=round(rate / 1e9, 1), frac=round(rate / 8e12, 4))
+    dom = max(summ, key=lambda k: summ[k][0] * summ[k][1]) if summ else None
+    roof = None
+    if dom:
+        n, t, u, kind = summ[dom]
+        roof = {"kernel": dom, "bound": kernels[dom]["bound"], "avg_ms": round(t, 4),
+                "algorithmic_per_launch": u, "frac": kernels[dom]["frac"],
+                "achieved": kernels[dom].get("achieved_gbs", kernels[dom].get("achieved_tflops")),
+                "peak": 8000.0 if kind != "flop" else 2500.0,
+                "unit": "GB/s" if kind != "flop" else "TFLOP/s"}
+    import json
+    print(json.dumps({"metric": "HyenaDNA-small MLM train step (BASELINE config D)", "value": round(a.B / dt, 3),
+                      "unit": "sequences/s", "tokens_per_s": round(a.B * a.L / dt), "ms_per_step": round(dt * 1e3, 2),
+                      "steps": a.steps, "dtype": "bf16", "data": "synthetic uniform ACGT, random init",
+                      "config": {"workload": f"HyenaDNA-small d256 x{a.layers} L={a.L}", "batch": a.B,
+                                 "seq_len": a.L}, "roofline": roof, "kernels": kernels}), flush=True)
 
 
 if __name__ == "__main__":

@@ -21,8 +21,9 @@ FAMILIES = {
     "gemm_wgrad": (r"Cijk_|sum_slices_kernel|wgradp_kernel", r"Cijk_|wgradp_kernel"),
     "attn_fwd": (r"attn::fwd2?_bf16_kernel|attn4fwd_bf16|attn16fwd2_bf16",
                  r"attn::fwd2?_bf16_kernel|attn4fwd_bf16|attn16fwd2_bf16"),
-    "attn_bwd": (r"attn::(dq|dkdv)2?_bf16_kernel|attn(2dq|4dkdv)_bf16|dq2_bf16|dkdv2_bf16",
-                 r"attn::dq2?_bf16_kernel|attn2dq_bf16|dq2_bf16"),
+    # the fused backward (bwd3) is one launch per op; the two-kernel pair counts its dQ kernel
+    "attn_bwd": (r"attn::(dq|dkdv)2?_bf16_kernel|attn(2dq|4dkdv)_bf16|dq2_bf16|dkdv2_bf16|bwd3_bf16_kernel",
+                 r"attn::dq2?_bf16_kernel|attn2dq_bf16|dq2_bf16|bwd3_bf16_kernel"),
     "geglu_fwd": (r"geglu10fwd_kernel|geglu::fwd_kernel", r"geglu10fwd_kernel|geglu::fwd_kernel"),
     "geglu_bwd": (r"geglu10bwd_kernel|geglu::bwd_kernel", r"geglu10bwd_kernel|geglu::bwd_kernel"),
     "ln_fwd": (r"2ln10fwd_kernel|ln::fwd_kernel", r"2ln10fwd_kernel|ln::fwd_kernel"),
