@@ -1398,20 +1398,18 @@ __device__ unsigned long long g_bwd3_stamps[4][16][6];
 #else
 #define BWD3_STAMP(t, k) do {} while (0)
 #endif
-#ifndef DNA_BWD3_PIPE_SB
-#define DNA_BWD3_PIPE_SB 0
-#endif
-constexpr bool PIPE_SB = DNA_BWD3_PIPE_SB;  // per-step sched_barriers in the pipelined phase 1
-
-template <int KB, int DBV>
+// V bit 0: fused bias-gradient column sums; bit 1: per-step sched_barriers in the pipelined
+// phase 1 (keeps the softmax tail between the previous block's dV/dK MFMAs; A/B via
+// DNA_ATTN_BWD3_SB)
+template <int KB, int V>
 __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
     const bf16* __restrict__ qkv, const bf16* __restrict__ out, const bf16* __restrict__ dout,
     const float* __restrict__ lse, const uint8_t* __restrict__ key_valid,
     const float* __restrict__ slopes, int H, float c, float scale, bf16* __restrict__ dqkv,
     float* __restrict__ dbias_part) {
-  constexpr bool DB = DBV == 1;          // fused bias-gradient column sums
-  constexpr bool DBL = DB || DBV == 2;   // (DBV 2 / 3: timing variants, loop part / epilogue part)
-  constexpr bool DBE = DB || DBV == 3;
+  constexpr bool DB = V & 1;  // fused bias-gradient column sums
+  constexpr bool DBL = DB, DBE = DB;
+  constexpr bool PIPE_SB = (V & 2) != 0;
   constexpr int S = 128 * KB;   // keys = queries of one (batch, head)
   constexpr int KPW = 32 * KB;  // keys per wave
   constexpr int NS = S / 32;    // query slices
@@ -2004,29 +2002,28 @@ static void launch_bwd3(const void* qkv, const void* out, const void* dout, cons
                         const uint8_t* key_valid, const float* slopes, int batch, int heads, float c,
                         float scale, void* dqkv, float* dbias_part, hipStream_t s) {
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB, 0>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
-    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
-    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
-    (void)hipFuncSetAttribute((const void*)bwd3_bf16_kernel<KB, 3>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
+    const void* ks[] = {(const void*)bwd3_bf16_kernel<KB, 0>, (const void*)bwd3_bf16_kernel<KB, 1>,
+                        (const void*)bwd3_bf16_kernel<KB, 2>, (const void*)bwd3_bf16_kernel<KB, 3>};
+    for (const void* k : ks)
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd3_lds<KB>());
     return true;
   }();
   (void)attr;
-  // DNA_ATTN_DBV (timing only): 2 / 3 run the loop / epilogue part of the bias-gradient sums
-  static const int dbv = getenv("DNA_ATTN_DBV") ? atoi(getenv("DNA_ATTN_DBV")) : 1;
+  // DNA_ATTN_BWD3_SB=1 (A/B): per-step sched_barriers in the software-pipelined phase 1
+  static const bool sb = getenv("DNA_ATTN_BWD3_SB") && atoi(getenv("DNA_ATTN_BWD3_SB")) == 1;
   const dim3 grid(batch * heads);
   const size_t lds = bwd3_lds<KB>();
   auto args = [&](auto kern, float* part) {
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, (const bf16*)qkv, (const bf16*)out,
                        (const bf16*)dout, lse, key_valid, slopes, heads, c, scale, (bf16*)dqkv, part);
   };
-  if (!dbias_part) args(bwd3_bf16_kernel<KB, 0>, nullptr);
-  else if (dbv == 2) args(bwd3_bf16_kernel<KB, 2>, dbias_part);
-  else if (dbv == 3) args(bwd3_bf16_kernel<KB, 3>, dbias_part);
-  else args(bwd3_bf16_kernel<KB, 1>, dbias_part);
+  if (!dbias_part) {
+    if (sb) args(bwd3_bf16_kernel<KB, 2>, nullptr);
+    else args(bwd3_bf16_kernel<KB, 0>, nullptr);
+  } else {
+    if (sb) args(bwd3_bf16_kernel<KB, 3>, dbias_part);
+    else args(bwd3_bf16_kernel<KB, 1>, dbias_part);
+  }
 }
 
 extern "C" int dna_attn_bwd_ex(const void* qkv, const void* out, const void* dout,
