@@ -1539,6 +1539,13 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
     // (one wave per SIMD: overlap has to come from this wave's own instruction order; the
     // sched_barriers keep the compiler from regrouping it)
     bf16x8 pbp[2], sbp[2];  // P and dS (bf16) of the previous block
+    f32x16 negd;            // -delta of this slice's rows: the dP' initial accumulator of every block
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 96 + 8 * g4 + 4 * hh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) negd[4 * g4 + e] = d4[e];
+    }
     const int tq = 4 * (g16 >> 1) + (i16 >> 2);  // tr-read row of lane
     auto tr_pair = [&](const bf16* img, int j) {  // A operand (dO^T or Q^T) of pair j = (s2, dt)
       const int qrow = 16 * (j >> 1) + tq;
@@ -1557,10 +1564,10 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const f32x4 l4 = *reinterpret_cast<const f32x4*>(RC + sel * 32 + 8 * g4 + 4 * hh);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 96 + 8 * g4 + 4 * hh);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) { sa[4 * g4 + e] = l4[e]; pa[4 * g4 + e] = d4[e]; }
+          for (int e = 0; e < 4; ++e) sa[4 * g4 + e] = l4[e];
         }
+        pa = negd;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           // kbase is a multiple of 32, so swz(kbase + kl, c) = kbase*D + swz(kl, c): written this
