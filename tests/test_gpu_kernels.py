@@ -108,6 +108,43 @@ def test_attention_backward_fused_bias_grad(b, S, H, pads):
     assert (cs - ref).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("S", [128, 256, 512])
+def test_attention_backward_deterministic(S):
+    """The fused backward (one workgroup per (batch, head) at S = 128/256/512) sums the two
+    key-half dQ partials in a fixed order and keeps dK/dV and the bias-gradient partial rows
+    per workgroup: dqkv and the partial rows are bit-identical run to run."""
+    import math
+    from dna_amd import _native as N
+    from dna_amd.config import alibi_slopes
+    b, H = 3, 4
+    qkv, kv = _qkv(b, S, H, torch.bfloat16, [(1, S - 37)], seed=7)
+    slopes = torch.tensor(alibi_slopes(H), device=DEV)
+    T = b * S
+    out = torch.empty(T, H * 64, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(b, H, S, device=DEV)
+    st = N.stream_ptr()
+    N.call("dna_attn_fwd", qkv.data_ptr(), kv.data_ptr(), slopes.data_ptr(), b, S, H, 64, 1,
+           1 / math.sqrt(64), out.data_ptr(), lse.data_ptr(), st)
+    g = torch.Generator(device="cpu").manual_seed(8)
+    dout = (torch.randn(T, H * 64, generator=g) * kv.cpu()[:, None].float()).to(DEV).bfloat16()
+    rows = N.lib().dna_attn_dbias_part_rows(b, S)
+    res = []
+    for _ in range(2):
+        dqkv = torch.full_like(qkv, float("nan"))
+        part = torch.full((rows, 3 * H * 64), float("nan"), device=DEV)
+        delta = torch.empty(b * H * S, device=DEV)
+        N.call("dna_attn_bwd_ex", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(),
+               kv.data_ptr(), slopes.data_ptr(), b, S, H, 64, 1, 1 / math.sqrt(64),
+               dqkv.data_ptr(), delta.data_ptr(), part.data_ptr(), st)
+        res.append((dqkv, part))
+    (d1, p1), (d2, p2) = res
+    assert torch.isfinite(d1.float()).all() and torch.isfinite(p1).all()  # every element written
+    assert torch.equal(d1, d2) and torch.equal(p1, p2)
+    # the partial rows sum to dqkv's column sums (pre-rounding fp32 vs rounded bf16 values)
+    ref = d1.float().sum(0)
+    assert (p1.sum(0) - ref).abs().max().item() < 1e-2 * ref.abs().max().item() + 1e-3
+
+
 def test_colsum_f32_deterministic_and_exact():
     from dna_amd import _native as N
     g = torch.Generator(device="cpu").manual_seed(5)
