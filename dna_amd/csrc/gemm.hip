@@ -122,7 +122,9 @@ struct Args {
   int F;
   float p; uint32_t th; float ks; uint64_t seed, off;
   int rot;                    // persistent kernel: rotate each block's K order (store spreading)
-  int dbg;                    // diagnostics (DNA_GEMM_DBG): 1 = stores dropped (OOB), 2 = no stores
+  int dbg;                    // diagnostics (DNA_GEMM_DBG): 1 = stores dropped (OOB), 2 = no stores,
+                              // 4 = output stores with the sc0 cache policy (A/B)
+  int nt;                     // persistent kernel: non-temporal output stores (DNA_GEMM_NT, default 0)
 };
 
 __device__ __forceinline__ void tile_of(const Args& a, int& mt, int& nt) {
@@ -648,7 +650,12 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       const auto sy = __builtin_amdgcn_permlane16_swap(h0[1], h1[1], false, false);
       const u32x4 o = u32x4{sx[0], sy[0], sx[1], sy[1]};
       const int soff = __builtin_amdgcn_readfirstlane(((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
-      if (a.dbg == 0) __builtin_amdgcn_raw_buffer_store_b128(o, rC, voQ, soff, 0);
+      // DNA_GEMM_NT=1 streams the output tiles with the non-temporal policy (aux 2): +2-9 % on
+      // isolated K = 768 GEMMs, but -1 % on the training step (the next kernel reads them), so off
+      if (a.dbg == 0) {
+        if (a.nt) __builtin_amdgcn_raw_buffer_store_b128(o, rC, voQ, soff, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(o, rC, voQ, soff, 0);
+      } else if (a.dbg == 4) __builtin_amdgcn_raw_buffer_store_b128(o, rC, voQ, soff, 1);  // sc0
       else if (a.dbg == 1) __builtin_amdgcn_raw_buffer_store_b128(o, rC, kOOB, 0, 0);
       else asm volatile("" :: "v"(o));
       acc[mq][nq][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1051,6 +1058,8 @@ int launchp(Args& a, hipStream_t s, const char* name) {
   if (const char* e = getenv("DNA_GEMM_ROT")) a.rot = atoi(e);
   a.dbg = 0;
   if (const char* e = getenv("DNA_GEMM_DBG")) a.dbg = atoi(e);
+  a.nt = 0;
+  if (const char* e = getenv("DNA_GEMM_NT")) a.nt = atoi(e);
   hipLaunchKernelGGL((gemmp_kernel<EPI>), dim3(G), dim3(NTHR), 0, s, a);
   DNA_LAUNCH_CHECK(name);
   return DNA_OK;
