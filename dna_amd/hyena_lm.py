@@ -9,8 +9,10 @@ The Block / Mlp / GPT2Embeddings modules come from flash_attn in the reference (
 here), so their forward is restated from flash_attn's published code (prenorm Block with
 residual_in_fp32) with the same parameter names -- parity of the backbone is unpinned; the
 Hyena operator inside is pinned (oracle/hyena_operator_ref.py). The long convolution and the
-operator's data movement run on HIP kernels; embeddings, LayerNorm, MLP and head are torch ops.
+operator's data movement and the LayerNorms run on HIP kernels; embeddings, MLP and head are
+torch ops.
 """
+import os
 from collections import namedtuple
 from functools import partial
 
@@ -45,6 +47,33 @@ class GPT2Embeddings(nn.Module):
         return h
 
 
+_LN_COLS = {64, 128, 192, 256, 512, 768, 1024}  # widths dna_ln_fwd/bwd are instantiated for
+_TORCH_LN = os.environ.get("DNA_HYENA_TORCH_LN", "0") == "1"  # A/B switch: torch's LayerNorm
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (the Block's norm1 / norm2 and LMBackbone.ln_f; same parameters and
+    state_dict) on the HIP kernels `dna_ln_fwd` / `dna_ln_bwd` (fp32 statistics, no bias /
+    dropout / residual terms). Under CUDA bf16 autocast the reference's layer_norm runs in fp32
+    and the next op (a Linear: in_proj, fc1, lm_head) casts its output to bf16; the kernel writes
+    that bf16 rounding directly, so one cast pass and the fp32 activation disappear. Widths the
+    kernels are not built for stay on torch's GPU LayerNorm; CPU tensors raise (no CPU path)."""
+
+    def forward(self, x):
+        d = x.shape[-1]
+        if _TORCH_LN or not (self.elementwise_affine and self.bias is not None and d in _LN_COLS
+                and x.dtype in (torch.float32, torch.bfloat16)
+                and self.weight.dtype == torch.float32):
+            return super().forward(x)
+        from . import functional as DF
+        bf16_out = (torch.is_autocast_enabled("cuda")
+                    and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        y32, yb = DF.FusedLayerNorm.apply(x.reshape(-1, d), None, None, self.weight, self.bias,
+                                          self.eps, 0, 0.0, 0, 0, not bf16_out, bf16_out)
+        y = yb if bf16_out else y32
+        return y.view(*x.shape[:-1], d)
+
+
 class Mlp(nn.Module):
     """flash_attn.modules.mlp.Mlp: fc2(act(fc1(x)))."""
 
@@ -70,10 +99,10 @@ class Block(nn.Module):
         super().__init__()
         self.mixer = mixer
         self.dropout1 = nn.Dropout(resid_dropout1)
-        self.norm1 = nn.LayerNorm(dim, eps=norm_eps)
+        self.norm1 = LayerNorm(dim, eps=norm_eps)
         self.mlp = mlp
         self.dropout2 = nn.Dropout(resid_dropout2)
-        self.norm2 = nn.LayerNorm(dim, eps=norm_eps)
+        self.norm2 = LayerNorm(dim, eps=norm_eps)
         self.residual_in_fp32 = residual_in_fp32
 
     def forward(self, hidden_states, residual=None):
@@ -132,7 +161,7 @@ class LMBackbone(nn.Module):
                   resid_dropout2=resid_dropout, residual_in_fp32=residual_in_fp32)
             for i in range(n_layer)])
         self.drop_f = nn.Dropout(resid_dropout)
-        self.ln_f = nn.LayerNorm(d_model, eps=layer_norm_epsilon)
+        self.ln_f = LayerNorm(d_model, eps=layer_norm_epsilon)
         self.apply(partial(_init_weights, n_layer=n_layer, **(initializer_cfg or {})))
 
     def forward(self, input_ids, position_ids=None):

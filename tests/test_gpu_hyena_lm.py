@@ -46,3 +46,35 @@ def test_hyena_lm_vs_oracle(d_model, L, bi):
             pre = n[: n.index("implicit_filter.")]
             r = sum(sd[k].grad for k in sd if k.startswith(pre) and k.endswith("freq"))
         assert _rel(p.grad, r) < 2e-3, n
+
+
+@pytest.mark.parametrize("d", [64, 256, 32])
+def test_hip_layernorm_module(d):
+    """hyena_lm.LayerNorm (dna_ln_fwd/bwd) vs torch's fp32 layer_norm: fp32 out of autocast,
+    and under bf16 autocast the bf16 rounding of the fp32 result (what the reference's next
+    autocast Linear feeds its GEMM); d=32 is not a kernel width and stays on torch."""
+    from dna_amd.hyena_lm import LayerNorm
+    g = torch.Generator().manual_seed(d)
+    ln = LayerNorm(d).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.1 * torch.randn(d, generator=g))
+        ln.bias.copy_(0.1 * torch.randn(d, generator=g))
+    x = (torch.randn(3, 70, d, generator=g) * 2 + 0.5).to(DEV).requires_grad_(True)
+    dy = torch.randn(3, 70, d, generator=g).to(DEV)
+    xr = x.detach().double().requires_grad_(True)
+    wr, br = ln.weight.detach().double().requires_grad_(True), ln.bias.detach().double().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (d,), wr, br, 1e-5)
+    y = ln(x)
+    assert y.dtype == torch.float32 and _rel(y, yr) < 1e-5
+    y.backward(dy)
+    yr.backward(dy.double())
+    for a, b in ((x.grad, xr.grad), (ln.weight.grad, wr.grad), (ln.bias.grad, br.grad)):
+        assert _rel(a, b) < 1e-5
+    x.grad = None
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = ln(x)
+    assert yb.dtype == torch.bfloat16
+    # bf16 rounding of an fp32 result that differs from torch's by ulps: <= 1 bf16 ulp apart
+    assert (yb.float() - yr.float().bfloat16().float()).abs().max() <= 2 ** -7 * yr.abs().max()
+    yb.backward(dy.bfloat16())
+    assert _rel(x.grad, xr.grad) < 1e-2
