@@ -10,12 +10,17 @@ mamba_ssm (Mamba, Block, RMSNorm) is not vendored: their forward is restated, pa
 The RC-equivariant variant (rcps=True: RCPSEmbedding / RCPSMambaBlock / RCPSLMHead) is not built.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import functional as DF
+from .hyena_lm import _LN_COLS, LayerNorm
 from .mamba import BiMambaWrapper
+
+_TORCH_NORM = os.environ.get("DNA_CADUCEUS_TORCH_NORM", "0") == "1"  # A/B switch: torch norms
 
 
 class RMSNorm(nn.Module):
@@ -28,8 +33,20 @@ class RMSNorm(nn.Module):
         self.register_parameter("bias", None)
 
     def forward(self, x):
-        xf = x.float()
-        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps) * self.weight).to(x.dtype)
+        d = x.shape[-1]
+        if (_TORCH_NORM or d not in _LN_COLS or self.weight.dtype != torch.float32
+                or x.dtype not in (torch.float32, torch.bfloat16)):
+            xf = x.float()
+            return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps) * self.weight).to(x.dtype)
+        # HIP kernel (dna_rms_fwd/bwd). Out of autocast: x.dtype as above. Under CUDA bf16
+        # autocast the next op is the mixer's in_proj Linear, which casts this output to bf16:
+        # the kernel writes that rounding directly (x is the fp32 residual in every Block).
+        bf16_out = (torch.is_autocast_enabled("cuda")
+                    and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        y32, yb = DF.RMSNormFn.apply(x.reshape(-1, d), self.weight, self.eps,
+                                     not bf16_out, bf16_out)
+        y = yb if bf16_out else y32.to(x.dtype)
+        return y.view(*x.shape[:-1], d)
 
 
 class MambaBlock(nn.Module):
@@ -63,7 +80,7 @@ class CaduceusMixerModel(nn.Module):
         super().__init__()
         self.residual_in_fp32 = cfg["residual_in_fp32"]
         self.embeddings = CaduceusEmbeddings(cfg["vocab_size"], cfg["d_model"])
-        norm_cls = RMSNorm if cfg["rms_norm"] else nn.LayerNorm
+        norm_cls = RMSNorm if cfg["rms_norm"] else LayerNorm
         ssm = dict(cfg.get("ssm_cfg") or {})
         self.layers = nn.ModuleList([
             MambaBlock(cfg["d_model"],

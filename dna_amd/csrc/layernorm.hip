@@ -84,6 +84,7 @@ struct FwdArgs {
   const void* x; const float* bias; int act; float p; uint32_t th; float kscale;
   uint64_t seed, off; const float* res; const float* gamma; const float* beta;
   int rows, cols; float eps; float* y; bf16* yb; float* mean; float* rstd;
+  int rms;  // RMSNorm: no mean subtraction, no beta, mean[] not written
 };
 
 template <typename TX, int NV, bool VEC>
@@ -119,19 +120,26 @@ __global__ __launch_bounds__(256) void fwd_kernel(FwdArgs a) {
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) s += v[k];
-  const float mu = wave_sum(s) / a.cols;
+  const float mu = a.rms ? 0.f : wave_sum(s) / a.cols;
   float q = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) { float d = v[k] - mu; q += d * d; }
   const float rs = rsqrtf(wave_sum(q) / a.cols + a.eps);
   float g[NV], be[NV];
   load_row<float, NV, VEC>(a.gamma, lane, g);
-  load_row<float, NV, VEC>(a.beta, lane, be);
+  if (a.beta) load_row<float, NV, VEC>(a.beta, lane, be);
+  else {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) be[k] = 0.f;
+  }
 #pragma unroll
   for (int k = 0; k < NV; ++k) v[k] = (v[k] - mu) * rs * g[k] + be[k];
   if (a.y) store_row<float, NV, VEC>(a.y + ro, lane, v);
   if (a.yb) store_row<bf16, NV, VEC>(a.yb + ro, lane, v);
-  if (lane == 0) { a.mean[row] = mu; a.rstd[row] = rs; }
+  if (lane == 0) {
+    if (!a.rms) a.mean[row] = mu;
+    a.rstd[row] = rs;
+  }
 }
 
 struct BwdArgs {
@@ -139,6 +147,7 @@ struct BwdArgs {
   uint32_t th; float kscale; uint64_t seed, off; const float* res; const float* gamma;
   const float* mean; const float* rstd; int rows, cols; float* dres; void* dx;
   float* part;  // [gridDim.x][3][cols]: dgamma, dbeta, dbias
+  int rms;      // RMSNorm backward: mean taken as 0, no mean-gradient term
 };
 
 template <int NV, bool VEC>
@@ -190,7 +199,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[k] += r[k];
     }
-    const float mu = a.mean[row], rs = a.rstd[row];
+    const float mu = a.rms ? 0.f : a.mean[row], rs = a.rstd[row];
     float g[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) g[k] = 0.f;
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
       s1 += gy;
       s2 += gy * xh;
     }
-    const float c1 = wave_sum(s1) * inv_cols, c2 = wave_sum(s2) * inv_cols;
+    const float c1 = a.rms ? 0.f : wave_sum(s1) * inv_cols, c2 = wave_sum(s2) * inv_cols;
 #pragma unroll
     for (int k = 0; k < NV; ++k) g[k] = rs * (g[k] - c1 - v[k] * c2);  // d(pre-LN sum)
     if (a.dres) store_row<float, NV, VEC>(a.dres + ro, lane, g);
@@ -427,7 +436,7 @@ extern "C" int dna_ln_fwd(const void* x, int x_dtype, const float* bias, int act
   DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_ln_fwd: bad dtype");
   if (rows == 0) return DNA_OK;
   FwdArgs a{x, bias, act, p_drop, dropout_threshold(p_drop), 1.f / (1.f - p_drop), seed, offset,
-            residual, gamma, beta, rows, cols, eps, y, (bf16*)y_bf16, mean, rstd};
+            residual, gamma, beta, rows, cols, eps, y, (bf16*)y_bf16, mean, rstd, 0};
   hipStream_t s = as_stream(stream);
   dim3 grid((rows + WAVES - 1) / WAVES);
   int st = dispatch_cols(cols, [&](auto nv, auto vec) {
@@ -458,7 +467,7 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
   const int nb = bwd_blocks(rows);
   BwdArgs a{dy, (const bf16*)dy_bf16, x, bias, act, p_drop, dropout_threshold(p_drop),
             1.f / (1.f - p_drop), seed, offset, residual, gamma, mean, rstd, rows, cols,
-            dresidual, dx, (float*)workspace};
+            dresidual, dx, (float*)workspace, 0};
   hipStream_t s = as_stream(stream);
   const size_t lds = (size_t)WAVES * 3 * cols * sizeof(float);
   int st = dispatch_cols(cols, [&](auto nv, auto vec) {
@@ -553,4 +562,60 @@ extern "C" int dna_embed_ln_bwd_rows(const float* dy, const void* dy_bf16, const
   return embed_ln_bwd_impl(dy, dy_bf16, ids, word_emb, type_row, gamma, mean, rstd, rows, cols,
                            vocab, -1, p_drop, seed, offset, nullptr, drows, dtype_row, dgamma,
                            dbeta, workspace, workspace_bytes, stream);
+}
+
+// ------------------------------------------------------------------------------------ RMSNorm
+// y = x * rsqrt(mean(x^2) + eps) * gamma (mamba_ssm's RMSNorm as Caduceus' Blocks and norm_f use
+// it; fp32 statistics): the LayerNorm kernels above with the mean fixed at 0 and no beta.
+extern "C" int dna_rms_fwd(const void* x, int x_dtype, const float* gamma, int rows, int cols,
+                           float eps, float* y, void* y_bf16, float* rstd, void* stream) {
+  DNA_CHECK_ARG(x && gamma && rstd, "dna_rms_fwd: null pointer");
+  DNA_CHECK_ARG(y || y_bf16, "dna_rms_fwd: no output");
+  DNA_CHECK_ARG(rows >= 0, "dna_rms_fwd: bad rows");
+  DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_rms_fwd: bad dtype");
+  if (rows == 0) return DNA_OK;
+  FwdArgs a{x, nullptr, DNA_ACT_NONE, 0.f, 0u, 1.f, 0, 0, nullptr, gamma, nullptr, rows, cols, eps,
+            y, (bf16*)y_bf16, nullptr, rstd, 1};
+  hipStream_t s = as_stream(stream);
+  dim3 grid((rows + WAVES - 1) / WAVES);
+  int st = dispatch_cols(cols, [&](auto nv, auto vec) {
+    constexpr int NV = decltype(nv)::value;
+    constexpr bool VEC = decltype(vec)::value;
+    if (x_dtype == DNA_BF16)
+      hipLaunchKernelGGL((fwd_kernel<bf16, NV, VEC>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((fwd_kernel<float, NV, VEC>), grid, dim3(256), 0, s, a);
+  });
+  if (st) return st;
+  DNA_LAUNCH_CHECK("dna_rms_fwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_rms_bwd(const float* dy, const void* dy_bf16, const void* x, int x_dtype,
+                           const float* gamma, const float* rstd, int rows, int cols, void* dx,
+                           float* dgamma, void* workspace, size_t workspace_bytes, void* stream) {
+  DNA_CHECK_ARG(x && gamma && rstd && dx, "dna_rms_bwd: null pointer");
+  DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_rms_bwd: bad dtype");
+  if (rows == 0) return DNA_OK;
+  DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
+                "dna_rms_bwd: workspace too small (%zu < %zu)", workspace_bytes,
+                dna_ln_bwd_workspace(rows, cols));
+  const int nb = bwd_blocks(rows);
+  BwdArgs a{dy, (const bf16*)dy_bf16, x, nullptr, DNA_ACT_NONE, 0.f, 0u, 1.f, 0, 0, nullptr, gamma,
+            nullptr, rstd, rows, cols, nullptr, dx, (float*)workspace, 1};
+  hipStream_t s = as_stream(stream);
+  const size_t lds = (size_t)WAVES * 3 * cols * sizeof(float);
+  int st = dispatch_cols(cols, [&](auto nv, auto vec) {
+    constexpr int NV = decltype(nv)::value;
+    constexpr bool VEC = decltype(vec)::value;
+    if (x_dtype == DNA_BF16)
+      hipLaunchKernelGGL((bwd_kernel<bf16, NV, VEC>), dim3(nb), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((bwd_kernel<float, NV, VEC>), dim3(nb), dim3(256), lds, s, a);
+  });
+  if (st) return st;
+  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
+                     (const float*)workspace, nb, cols, dgamma, (float*)nullptr, (float*)nullptr);
+  DNA_LAUNCH_CHECK("dna_rms_bwd");
+  return DNA_OK;
 }

@@ -198,6 +198,45 @@ class FusedLayerNorm(torch.autograd.Function):
         return dx, dbias, dres, dg, db, None, None, None, None, None, None, None
 
 
+class RMSNormFn(torch.autograd.Function):
+    """x * rsqrt(mean(x^2) + eps) * gamma -> (y fp32|None, y_bf16|None): mamba_ssm's RMSNorm
+    as the Caduceus Blocks / norm_f apply it (modeling_caduceus.py:25-65, :214-216)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, eps, want_f32, want_bf16):
+        _gpu(x, gamma)
+        ctx.set_materialize_grads(False)
+        x = x.contiguous()
+        n, d = x.shape
+        y = torch.empty(n, d, device=x.device, dtype=torch.float32) if want_f32 else None
+        yb = torch.empty(n, d, device=x.device, dtype=torch.bfloat16) if want_bf16 else None
+        rstd = torch.empty(n, device=x.device, dtype=torch.float32)
+        nbytes = n * (d * (x.element_size() + (4 if want_f32 else 0) + (2 if want_bf16 else 0)) + 4)
+        with _timed("rms_fwd", nbytes, "byte"):
+            N.call("dna_rms_fwd", x.data_ptr(), _dt(x), gamma.data_ptr(), n, d, eps, _p(y), _p(yb),
+                   rstd.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(x, gamma, rstd)
+        return y, yb
+
+    @staticmethod
+    def backward(ctx, dy, dyb):
+        x, gamma, rstd = ctx.saved_tensors
+        n, d = x.shape
+        dx = torch.empty_like(x)
+        dg = torch.empty_like(gamma)
+        nws = N.lib().dna_ln_bwd_workspace(n, d)
+        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
+        dy = None if dy is None else dy.contiguous()
+        dyb = None if dyb is None else dyb.contiguous()
+        nbytes = n * (d * ((4 if dy is not None else 0) + (2 if dyb is not None else 0)
+                           + 2 * x.element_size()) + 4)
+        with _timed("rms_bwd", nbytes, "byte"):
+            N.call("dna_rms_bwd", _p(dy), _p(dyb), x.data_ptr(), _dt(x), gamma.data_ptr(),
+                   rstd.data_ptr(), n, d, dx.data_ptr(), dg.data_ptr(), ws.data_ptr(), nws,
+                   N.stream_ptr())
+        return dx, dg, None, None, None
+
+
 # ----------------------------------------------------------------------------------- attention
 class AlibiAttention(torch.autograd.Function):
     """softmax(q k^T * scale - slope_h |i-j| + pad_bias) v on packed qkv [T, 3*H*D]."""

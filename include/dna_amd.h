@@ -98,6 +98,19 @@ int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, int x_dtype,
                int rows, int cols, float* dresidual, void* dx, float* dgamma, float* dbeta,
                float* dbias, void* workspace, size_t workspace_bytes, void* stream);
 
+/* RMSNorm y = x * rsqrt(mean(x^2) + eps) * gamma with fp32 statistics -- replaces mamba_ssm's
+ * RMSNorm as the Caduceus Blocks and norm_f apply it (src/models/caduceus/modeling_caduceus.py
+ * :25-65 and :214-216 build them with rms_norm=True; the fused add is left to the caller).
+ * x [rows, cols] x_dtype; y fp32 and/or
+ * y_bf16; rstd [rows] fp32. Backward writes dx (x_dtype) and dgamma [cols] (written, not
+ * accumulated); the output gradient is dy (fp32) + dy_bf16, either may be NULL;
+ * workspace >= dna_ln_bwd_workspace(rows, cols). */
+int dna_rms_fwd(const void* x, int x_dtype, const float* gamma, int rows, int cols, float eps,
+                float* y, void* y_bf16, float* rstd, void* stream);
+int dna_rms_bwd(const float* dy, const void* dy_bf16, const void* x, int x_dtype,
+                const float* gamma, const float* rstd, int rows, int cols, void* dx,
+                float* dgamma, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------ embeddings
  * y = dropout( LN( word_emb[ids] + type_row ) )   (BertEmbeddings.forward, bert_layers.py:62-107;
  * token_type_ids are all zero so type_row = token_type_embeddings.weight[0]).

@@ -41,3 +41,35 @@ def test_caduceus_vs_oracle(rms, strategy):
     logits.backward(g.float().to(DEV))
     for n, p in m.named_parameters():
         assert _rel(p.grad, sd[n].grad) < 2e-3, n
+
+
+@pytest.mark.parametrize("d,dtype", [(256, torch.float32), (64, torch.float32), (256, torch.bfloat16)])
+def test_hip_rmsnorm_module(d, dtype):
+    """caduceus.RMSNorm on dna_rms_fwd/bwd vs a float64 restatement of mamba_ssm's RMSNorm:
+    fp32 / bf16 inputs out of autocast (output in the input dtype), and under bf16 autocast the
+    bf16 rounding of the fp32 result."""
+    from dna_amd.caduceus import RMSNorm
+    g = torch.Generator().manual_seed(d)
+    m = RMSNorm(d).to("cuda")
+    with torch.no_grad():
+        m.weight.copy_(1 + 0.1 * torch.randn(d, generator=g))
+    x = (torch.randn(5, 33, d, generator=g) * 2 + 0.3).to("cuda", dtype).requires_grad_(True)
+    dy = torch.randn(5, 33, d, generator=g).to("cuda")
+    xr = x.detach().double().requires_grad_(True)
+    wr = m.weight.detach().double().requires_grad_(True)
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    y = m(x)
+    assert y.dtype == dtype
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(y, yr) < tol
+    y.backward(dy.to(dtype))
+    yr.backward(dy.to(dtype).double())
+    assert _rel(x.grad, xr.grad) < tol * 5 and _rel(m.weight.grad, wr.grad) < tol * 5
+    if dtype == torch.float32:
+        x.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            yb = m(x)
+        assert yb.dtype == torch.bfloat16
+        assert (yb.float() - yr.float().bfloat16().float()).abs().max() <= 2 ** -7 * yr.abs().max()
+        yb.backward(dy.bfloat16())
+        assert _rel(x.grad, xr.grad) < 1e-2
