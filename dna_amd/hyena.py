@@ -9,13 +9,38 @@ kernels of dna_amd/csrc/fftconv.hip (four-step FFT of size 2L, fp32 internally);
 or torch.fft fallback -- without the native library or a GPU tensor this raises.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native as N
+from .functional import Linear as _LinearFn
 from .functional import _dt, _gpu, _p, _timed
+
+_TORCH_LINEAR = os.environ.get("DNA_HYENA_TORCH_LINEAR", "0") == "1"  # A/B switch: torch Linear
+
+
+class HipLinear(nn.Linear):
+    """nn.Linear (same parameters / state_dict) whose bf16-autocast forward and data gradient run
+    on the persistent MFMA GEMM (`dna_linear_fwd`, dgrad on a transposed bf16 weight copy) and
+    whose weight gradient is the fp32 split-K GEMM of functional.Linear -- the projections of the
+    Hyena operator (in_proj / out_proj, hyena.py:311-509) and of the HyenaDNA Block's Mlp
+    (fc1 / fc2). The reference runs them as autocast nn.Linear (bf16 GEMM of the bf16-cast input
+    and weight, bf16 output, fp32 weight / bias gradients): same operands, same output dtype.
+    Outside CUDA bf16 autocast, or for shapes the kernel does not take (K % 64, N % 256),
+    it is torch's Linear."""
+
+    def forward(self, x):
+        if (_TORCH_LINEAR or not x.is_cuda or self.in_features % 64 or self.out_features % 256
+                or not torch.is_autocast_enabled("cuda")
+                or torch.get_autocast_dtype("cuda") != torch.bfloat16):
+            return super().forward(x)
+        w_lp = self.weight.to(torch.bfloat16)
+        y = _LinearFn.apply(x.reshape(-1, self.in_features).to(torch.bfloat16), self.weight, w_lp,
+                            self.bias, w_lp.t().contiguous())
+        return y.view(*x.shape[:-1], self.out_features)
 
 
 def _bytes_per_elem(t):
@@ -365,8 +390,8 @@ class HyenaOperator(nn.Module):
         self.return_state, self.bidirectional = return_state, bidirectional
         self.activation = nn.Identity()
         self.dropout = nn.Dropout(dropout)
-        self.out_proj = nn.Linear(d_model * inner_factor, d_model)
-        self.in_proj = nn.Linear(d_model, (order + 1) * d_model)
+        self.out_proj = HipLinear(d_model * inner_factor, d_model)
+        self.in_proj = HipLinear(d_model, (order + 1) * d_model)
         total_width = d_model * inner_factor * (order + 1)
         self.short_filter = nn.Conv1d(total_width, total_width, kernel_size=short_filter_order,
                                       groups=total_width, padding=short_filter_order - 1)

@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .hyena import HyenaOperator
+from .hyena import HipLinear, HyenaOperator
 
 
 CausalLMOutput = namedtuple("CausalLMOutput", ["logits"])
@@ -82,9 +82,9 @@ class Mlp(nn.Module):
         super().__init__()
         fk = {"device": device, "dtype": dtype}
         hidden_features = hidden_features or in_features * 4
-        self.fc1 = nn.Linear(in_features, hidden_features, **fk)
+        self.fc1 = HipLinear(in_features, hidden_features, **fk)
         self.activation = activation
-        self.fc2 = nn.Linear(hidden_features, out_features or in_features, **fk)
+        self.fc2 = HipLinear(hidden_features, out_features or in_features, **fk)
 
     def forward(self, x):
         return self.fc2(self.activation(self.fc1(x)))

@@ -81,3 +81,28 @@ def test_hip_layernorm_module(d):
     assert (yb.float() - yr.float().bfloat16().float()).abs().max() <= 2 ** -7 * yr.abs().max()
     yb.backward(dy.bfloat16())
     assert _rel(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("k,n", [(256, 768), (1024, 256), (256, 1024), (64, 96)])
+def test_hip_linear_module_bf16(k, n):
+    """hyena.HipLinear under bf16 autocast (persistent MFMA GEMM fwd / dgrad, fp32 split-K wgrad)
+    vs an fp32 reference on the same bf16-rounded operands; (64, 96) is not a kernel shape and
+    stays on torch. Output bf16 like autocast nn.Linear; weight / bias gradients fp32."""
+    from dna_amd.hyena import HipLinear
+    g = torch.Generator().manual_seed(k + n)
+    lin = HipLinear(k, n).to(DEV)
+    x = torch.randn(2, 1000, k, generator=g).to(DEV).requires_grad_(True)
+    dy = torch.randn(2, 1000, n, generator=g).to(DEV).bfloat16()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lin(x)
+    assert y.dtype == torch.bfloat16
+    y.backward(dy)
+    xb = x.detach().bfloat16().float().requires_grad_(True)
+    wb = lin.weight.detach().bfloat16().float().requires_grad_(True)
+    br = lin.bias.detach().clone().requires_grad_(True)
+    yr = xb @ wb.t() + br
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xb.grad) < 1e-2
+    assert _rel(lin.weight.grad, wb.grad) < 2e-3
+    assert _rel(lin.bias.grad, br.grad) < 1e-4
