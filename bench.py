@@ -140,7 +140,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)   # 100 timed, 20 warm-up
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("DNA_BENCH_BATCH", 256)))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DNA_BENCH_BATCH", 512)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-b64", action="store_true", help="skip the extra per-GPU b=64 measurement")
