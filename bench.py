@@ -183,7 +183,8 @@ def main():
         # rank's host threads) -> DeviceBatch.from_host (row bookkeeping + pinned H2D copy)
         from dna_amd.hg38 import host_threads
         from scripts.data_pipeline_bench import measure, synthetic_root
-        root = synthetic_root(n_chroms=8, chrom_len=16_777_216)
+        # enough 4096-bp windows for warm-up + 60 timed batches of this size in one epoch
+        root = synthetic_root(n_chroms=8, chrom_len=16_777_216 * max(1, -(-args.batch // 256)))
         workers = 8
         data_pipeline = {"seq_per_s": round(measure(root, workers, args.batch, 60, device=device), 1),
                          "threads": host_threads(), "workers": workers,

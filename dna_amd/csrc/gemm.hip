@@ -1105,8 +1105,24 @@ extern "C" int dna_linear_fwd(const void* x, const void* w, const float* bias, i
   a.C = y; a.ldc = N; a.bias = bias;
   a.M = M; a.N = N; a.K = K; a.ksplit = K;
   if (persistent_enabled() && N <= BIAS_LDS / 4 && N % BN == 0 && K >= 2 * BK &&
-      (size_t)M * (K > N ? K : N) * 2 < (1ull << 31) && (size_t)N * K * 2 < (1ull << 31))
-    return launchp<EPI_BF16>(a, as_stream(stream), "dna_linear_fwd");
+      (size_t)N * K * 2 < (1ull << 31)) {
+    // the persistent kernel addresses an operand with 32-bit byte offsets: row blocks of at most
+    // mc rows (a multiple of the 256-row tile) per launch, so e.g. T = 262,144 tokens (b = 512)
+    // at N = 6144 runs as two launches of the b = 256 shape instead of the non-persistent kernel
+    const size_t wide = (size_t)(K > N ? K : N) * 2;
+    const int mc = (int)(((1ull << 31) - 1) / wide / BM * BM);
+    if (mc >= BM) {
+      for (int r0 = 0; r0 < M; r0 += mc) {
+        Args c = a;
+        c.A = a.A + (size_t)r0 * K;
+        c.C = (bf16*)a.C + (size_t)r0 * N;
+        c.M = M - r0 < mc ? M - r0 : mc;
+        const int st = launchp<EPI_BF16>(c, as_stream(stream), "dna_linear_fwd");
+        if (st != DNA_OK) return st;
+      }
+      return DNA_OK;
+    }
+  }
   return launch<true, true, EPI_BF16>(a, 1, as_stream(stream), "dna_linear_fwd");
 }
 

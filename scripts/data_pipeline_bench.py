@@ -42,7 +42,11 @@ def measure(root, workers, batch=256, batches=60, warmup=None, device=None):
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             t0 = time.perf_counter()
-        (masked, mask, labels), target = next(it)
+        try:
+            (masked, mask, labels), target = next(it)
+        except StopIteration:  # dataset smaller than warm-up + timed batches: next epoch
+            it = iter(loader)
+            (masked, mask, labels), target = next(it)
         DeviceBatch.from_host(masked, mask, labels, target, dev)
         if i >= warmup:
             n += masked.shape[0]

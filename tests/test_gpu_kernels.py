@@ -422,6 +422,26 @@ def test_gemm_linear_fwd_dgrad_wgrad(M, N, K):
         assert _rel(part.sum(0), dy.float().t() @ x.float()) < 1e-5
 
 
+def test_gemm_linear_fwd_row_blocks_past_32bit_offsets():
+    """An x operand of >= 2^31 bytes (M = 2^19 + 100 rows x K = 2048) runs the persistent kernel
+    in row blocks of 524,032 rows (a multiple of 256): rows on both sides of the block boundary,
+    and the ragged last rows, equal fp32 torch on the same bf16 operands; the output between
+    blocks is fully written."""
+    M, N, K = (1 << 19) + 100, 256, 2048
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.empty(M, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(DEV).bfloat16()
+    b = torch.randn(N, generator=g).to(DEV)
+    y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_linear_fwd", x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, y.data_ptr())
+    torch.cuda.synchronize()
+    assert not torch.isnan(y).any()
+    mc = ((1 << 31) - 1) // (K * 2) // 256 * 256
+    for r in (0, mc - 300, mc - 1, mc, mc + 1, M - 300):
+        rows = slice(r, min(r + 300, M))
+        assert _rel(y[rows], x[rows].float() @ w.float().t() + b) < 1e-2, r
+
+
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_gemm_geglu_fused_equals_unfused(p):
     """Fused gated_layers+GeGLU fwd and wo-dgrad+GeGLU bwd give bit-identical results to the
