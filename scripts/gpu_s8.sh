@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/s8
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "row_blocks or gemm_linear" tests/test_gpu_hyena_lm.py -x -q --timeout 120 --timeout-method thread > $O/new_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_hyena_lm.py -x -q --timeout 120 --timeout-method thread > $O/new_tests.log 2>&1 || exit 1
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1 || exit 1
 for b in 256 512; do
   timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-b64 --no-cpu-baseline --no-data-pipeline --batch $b >> $O/ab_batch.jsonl 2>> $O/ab_batch.err || exit 1
