@@ -13,7 +13,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python $ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-b64 --no-data-pipeline --batch $BATCH > $OUT/stats_bench.json 2> $OUT/stats_bench.err
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python $ROOT/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-b64 --no-data-pipeline --batch $BATCH > $OUT/fetch_bench.json 2> $OUT/fetch_bench.err
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python $ROOT/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-b64 --no-data-pipeline --batch $BATCH > $OUT/write_bench.json 2> $OUT/write_bench.err
-python $ROOT/scripts/traffic_from_pmc.py $OUT/fetch $OUT/write $OUT/traffic.json $BATCH > /dev/null
+python $ROOT/scripts/traffic_from_pmc.py $OUT/fetch $OUT/write $OUT/traffic.json $BATCH $OUT/fetch_bench.json > /dev/null
 cp $OUT/traffic.json $ROOT/profiles/$R/traffic.json
 python $ROOT/scripts/prof_summary.py $OUT/stats/run_kernel_stats.csv --steps 13 > $OUT/kernel_stats.md
 cd $ROOT

@@ -1,5 +1,6 @@
 #!/usr/bin/env python
 """HBM traffic per op launch from two rocprofv3 --pmc passes over the same bench command.
+Usage: traffic_from_pmc.py FETCH_DIR WRITE_DIR OUT.json [BATCH [PASS_BENCH.json]]
 
     python scripts/traffic_from_pmc.py FETCH_DIR WRITE_DIR OUT.json [BATCH]
 
@@ -60,6 +61,15 @@ def families(disp, scale):
 def main():
     fdir, wdir, out = sys.argv[1:4]
     batch = int(sys.argv[4]) if len(sys.argv) > 4 else None
+    # optional: the bench JSON line each pass printed -- op launches = launches_per_step x
+    # (steps + warmup), so a row-blocked GEMM call (two kernel launches, csrc/gemm.hip) counts once
+    ops = {}
+    if len(sys.argv) > 5 and os.path.exists(sys.argv[5]):
+        with open(sys.argv[5]) as f:
+            line = [l for l in f.read().splitlines() if l.startswith("{")][-1]
+        bj = json.loads(line)
+        for fam, k in bj.get("kernels", {}).items():
+            ops[fam] = k["launches_per_step"] * (bj["steps"] + bj["warmup"])
     fetch = per_dispatch(os.path.join(fdir, "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_dispatch(os.path.join(wdir, "run_counter_collection.csv"), "WRITE_SIZE")
     ft, fc = families(fetch, 2 * 1024.0)   # KiB, x2 gfx950 FETCH_SIZE correction
@@ -69,6 +79,8 @@ def main():
         n = fc.get(fam) or wc.get(fam)
         if not n:
             continue
+        if fam in ops:
+            fc[fam] = wc[fam] = n = ops[fam]
         res[fam] = {"bytes_per_launch": int((ft[fam] / fc[fam] if fc.get(fam) else 0)
                                             + (wt[fam] / wc[fam] if wc.get(fam) else 0)),
                     "read_bytes_per_launch": int(ft[fam] / fc[fam]) if fc.get(fam) else None,
