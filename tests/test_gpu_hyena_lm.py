@@ -106,4 +106,4 @@ def test_hip_linear_module_bf16(k, n):
     assert _rel(x.grad, xb.grad) < 1e-2
     # HIP: fp32 split-K weight gradient; torch's autocast Linear rounds dW to bf16 first
     assert _rel(lin.weight.grad, wb.grad) < (2e-3 if n % 256 == 0 else 1e-2)
-    assert _rel(lin.bias.grad, br.grad) < 1e-4
+    assert _rel(lin.bias.grad, br.grad) < (1e-4 if n % 256 == 0 else 1e-2)
