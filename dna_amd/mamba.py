@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from . import _native as N
 from .functional import _dt, _gpu, _p, _timed
+from .hyena import HipLinear
 
 
 class SelectiveScan(torch.autograd.Function):
@@ -173,7 +174,8 @@ class Mamba(nn.Module):
         self.A_log._no_weight_decay = True
         self.D = nn.Parameter(torch.ones(self.d_inner, device=device))
         self.D._no_weight_decay = True
-        self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **fk)
+        # bf16 autocast: the persistent MFMA GEMM (hyena.HipLinear; same parameters)
+        self.out_proj = HipLinear(self.d_inner, d_model, bias=bias, **fk)
 
     def forward(self, hidden_states, inference_params=None):
         if inference_params is not None:
