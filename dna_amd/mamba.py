@@ -21,7 +21,6 @@ import torch.nn.functional as F
 
 from . import _native as N
 from .functional import _dt, _gpu, _p, _timed
-from .hyena import HipLinear
 
 
 class SelectiveScan(torch.autograd.Function):
@@ -174,8 +173,10 @@ class Mamba(nn.Module):
         self.A_log._no_weight_decay = True
         self.D = nn.Parameter(torch.ones(self.d_inner, device=device))
         self.D._no_weight_decay = True
-        # bf16 autocast: the persistent MFMA GEMM (hyena.HipLinear; same parameters)
-        self.out_proj = HipLinear(self.d_inner, d_model, bias=bias, **fk)
+        # stays torch's Linear: on the persistent MFMA GEMM (hyena.HipLinear) the config-E step was
+        # slower, 92.0 vs 88.8 ms (its input is a transposed view that needs a copy first;
+        # profiles/r02/session4/cfge_*linear.txt)
+        self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **fk)
 
     def forward(self, hidden_states, inference_params=None):
         if inference_params is not None:
