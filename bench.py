@@ -2,7 +2,9 @@
 """MLM pretraining throughput of DNABERT-2-117M at seq_len 512 on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+    N > 1: either under a launcher (python -m torch.distributed.run --nproc-per-node N ...
+    bench.py --gpus N ...) or plain `bench.py --gpus N`, which starts the N rank processes itself
+    (rank r on cuda:r, RCCL; DNA_DIST_BACKEND=gloo rehearses it with every rank on one GPU).
 
 One step = forward (HIP kernels) + fused masked-CE + backward + RCCL gradient all-reduce + global
 clip + AdamW on a per-GPU batch of B synthetic hg38 windows (uniform ACGT, 4096 bp -> exactly 512
@@ -135,6 +137,69 @@ CONFIG_A = dict(vocab_size=4096, hidden_size=128, num_hidden_layers=2, num_atten
                 intermediate_size=512)
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N rank processes of this
+    script -- torchrun-style env (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT) --
+    before this process touches the GPU, wait for all of them, and exit with the first failing
+    rank's status. Rank r binds cuda:r; rank 0 prints the JSON line (stdout is inherited)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:  # one rank failed: the others would hang in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+def dist_skeleton(args, world, rank):
+    """--dist-dry-run: the multi-rank measurement protocol without the model (CPU, gloo): the
+    same barrier / timed region / max-over-ranks / one-JSON-line path, with a gradient-sized
+    all-reduce as the step. Used by the CPU test of the launcher; never a bench number."""
+    dist.init_process_group("gloo")
+    g = torch.ones(1 << 16)
+    for _ in range(args.warmup):
+        dist.all_reduce(g)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dist.all_reduce(g)
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "sequences/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                          "ms_per_step": round(float(el) / max(1, args.steps) * 1e3, 3),
+                          "config": {"parallelism": f"dp{world}", "global_batch": args.batch * world}}),
+              flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,11 +210,20 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-b64", action="store_true", help="skip the extra per-GPU b=64 measurement")
     ap.add_argument("--no-data-pipeline", action="store_true", help="skip the host data-path timing")
+    ap.add_argument("--dist-dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: become one (N rank processes), before any GPU call in this process
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} ranks",
+              file=sys.stderr)
+    if args.dist_dry_run:
+        return dist_skeleton(args, world, rank)
     # DNA_DIST_BACKEND=gloo (rehearsal only): every rank on the visible GPUs round-robin, gradient
     # all-reduce over gloo -- exercises the multi-rank bench path on a one-GPU box
     backend = os.environ.get("DNA_DIST_BACKEND", "nccl")
@@ -176,7 +250,8 @@ def main():
     batches = make_batches(4, args.batch, rank, device)
     t_data = time.perf_counter() - t_data
     data_pipeline = None
-    if rank == 0 and not args.no_data_pipeline:
+    # the host data path is measured once per node, on single-GPU runs (not part of value)
+    if rank == 0 and world == 1 and not args.no_data_pipeline:
         # train.py's own data path, timed before the GPU region (not part of value): registry
         # dataset bert_hg38 over a synthetic FASTA/BED -> torch DataLoader (batched __getitems__:
         # FASTA -> native multithreaded BPE -> native masking; 8 worker processes sharing this

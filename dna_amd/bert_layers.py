@@ -190,8 +190,11 @@ class BertForMaskedLM(nn.Module):
         self._lp_provider = None  # set by dna_amd.flat.FlatParams for a persistent bf16 copy
         self._lpt_provider = None  # ... and for the transposed bf16 projection weights
         self._init_weights()
-        for m in self.modules():  # projection weights: keep a W^T copy for the data gradient
-            if isinstance(m, nn.Linear):
+        # projection weights: keep a W^T copy for the data gradient dx = dy . W^T^T, where the
+        # MFMA kernel wants the reduction (out features) % 64 and the output (in features) % 8,
+        # as dna_transpose_bf16 does; other shapes keep the library dgrad
+        for m in self.modules():
+            if isinstance(m, nn.Linear) and m.out_features % 64 == 0 and m.in_features % 8 == 0:
                 m.weight._dna_transpose = True
 
     # -- reference-compatible utilities ------------------------------------------------------

@@ -200,10 +200,12 @@ class DNABERT2Pretrain(SequenceDataset):
                                  [self.max_length, self.max_length_val, self.max_length_test])]
 
     def _data_loader(self, dataset, batch_size, shuffle=False, sampler=None):
+        from .hg38 import worker_context
         return torch.utils.data.DataLoader(dataset, batch_size=batch_size,
                                            num_workers=self.num_workers, shuffle=shuffle,
                                            sampler=sampler, drop_last=self.drop_last,
-                                           pin_memory=self.pin_memory)
+                                           pin_memory=self.pin_memory,
+                                           multiprocessing_context=worker_context(self.num_workers))
 
     def train_dataloader(self, sampler=None, **kwargs):
         return self._data_loader(self.dataset_train, self.batch_size,

@@ -425,7 +425,8 @@ extern "C" int dna_bpe_encode(const dna_bpe* h, const char* text, int len, int32
   Scratch sc;
   std::vector<int32_t> ids;
   encode(*h, text, len, sc, ids);
-  if (out_ids) memcpy(out_ids, ids.data(), sizeof(int32_t) * std::min<size_t>(ids.size(), (size_t)std::max(cap, 0)));
+  const size_t n = std::min<size_t>(ids.size(), (size_t)std::max(cap, 0));
+  if (out_ids && n > 0) memcpy(out_ids, ids.data(), sizeof(int32_t) * n);  // memcpy(.., null, 0) is UB
   return (int)ids.size();
 }
 

@@ -537,8 +537,9 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   __syncthreads();
 
   // Operands through buffer resources over the whole matrices: per-lane offsets are fixed for the
-  // kernel's life (2 VGPRs per operand), tile / K position is the scalar soffset, and rows past M
-  // read as zeros (bounds check) -- no per-lane clamping, no 64-bit addresses.
+  // kernel's life (2 VGPRs per operand), the wave-uniform tile / K position is added to voffset
+  // (soffset is excluded from the range check), and rows past M read as zeros -- no per-lane
+  // clamping, no 64-bit addresses.
   const int NB = EPI == EPI_GEGLU ? 2 * a.F : a.N;  // rows of the weight operand
   const auto rA = out_rsrc(a.A, (uint32_t)((size_t)a.M * a.lda * 2));
   const auto rB = out_rsrc(a.B, (uint32_t)((size_t)NB * a.ldb * 2));
@@ -579,11 +580,13 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     else if constexpr (EPI == EPI_GEGLU) row0 = (h - 2) * a.F + c.n0;
     else row0 = c.n0 + (h - 2) * 128;
     const int ld = h < 2 ? a.lda : a.ldb;
-    const int soff = __builtin_amdgcn_readfirstlane((row0 * ld + k0) * 2);
+    // the tile offset goes into voffset, not soffset: the hardware range check covers
+    // voffset + inst_offset only, so rows past M must be visible there to read as zeros
+    const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane((row0 * ld + k0) * 2);
 #pragma unroll
     for (int p = 0; p < 2; ++p)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rA : rB, (lds_t*)(d + (p * 64 + wave * 8) * 128),
-                                               16, h < 2 ? voA[p] : voB[p], soff, 0, 0);
+                                               16, (h < 2 ? voA[p] : voB[p]) + toff, 0, 0, 0);
   };
 
   f32x4 acc[2][2][4][2];  // [mq][nq][i][j]
@@ -624,8 +627,8 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // epilogue stores: lane part of the offset fixed, tile row block in soffset, column block in
-  // the immediate; rows past M fall outside the resource and are dropped
+  // epilogue stores: lane part of the offset fixed, tile row / column block added to it; rows
+  // past M fall outside the resource and are dropped
   const int cq = 4 * (lane >> 4);
   const int ldo = EPI == EPI_GEGLU ? 2 * a.F : a.ldc;
   const auto rC = out_rsrc(a.C, (uint32_t)((size_t)a.M * ldo * 2));
@@ -649,13 +652,15 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       const auto sx = __builtin_amdgcn_permlane16_swap(h0[0], h1[0], false, false);
       const auto sy = __builtin_amdgcn_permlane16_swap(h0[1], h1[1], false, false);
       const u32x4 o = u32x4{sx[0], sy[0], sx[1], sy[1]};
-      const int soff = __builtin_amdgcn_readfirstlane(((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
+      // row block in voffset (range-checked: rows past M are dropped), never in soffset
+      const uint32_t off = voQ + (uint32_t)__builtin_amdgcn_readfirstlane(
+                                     ((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
       // DNA_GEMM_NT=1 streams the output tiles with the non-temporal policy (aux 2): +2-9 % on
       // isolated K = 768 GEMMs, but -1 % on the training step (the next kernel reads them), so off
       if (a.dbg == 0) {
-        if (a.nt) __builtin_amdgcn_raw_buffer_store_b128(o, rC, voQ, soff, 2);
-        else __builtin_amdgcn_raw_buffer_store_b128(o, rC, voQ, soff, 0);
-      } else if (a.dbg == 4) __builtin_amdgcn_raw_buffer_store_b128(o, rC, voQ, soff, 1);  // sc0
+        if (a.nt) __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 0);
+      } else if (a.dbg == 4) __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 1);  // sc0
       else if (a.dbg == 1) __builtin_amdgcn_raw_buffer_store_b128(o, rC, kOOB, 0, 0);
       else asm volatile("" :: "v"(o));
       acc[mq][nq][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -874,11 +879,11 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
     const bool isA = h < 2;
     const int col0 = isA ? c.m0 + h * 128 : c.n0 + (h - 2) * 128;
     const int ld = isA ? a.ldy : a.ldx;
-    const int soff = __builtin_amdgcn_readfirstlane((trow * ld + col0) * 2);
+    const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane((trow * ld + col0) * 2);
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 2; ++p)  // offset in voffset: token rows past T fail the range check
       __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, (lds_t*)(d + (p * 32 + wave * 4) * 256),
-                                               16, isA ? voA[p] : voB[p], soff, 0, 0);
+                                               16, (isA ? voA[p] : voB[p]) + toff, 0, 0, 0);
   };
 
   f32x4 acc[2][2][4][2];
@@ -922,12 +927,12 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
   auto store_quadrant = [&](const Cur& c, int mq, int nq) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int soff = __builtin_amdgcn_readfirstlane(
+      const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane(
           (int)((((size_t)c.c * a.Nw + c.m0 + mq * 128 + i * 16) * a.Kw + c.n0 + nq * 128) * 4));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mq][nq][i][j]), rC,
-                                               voC + j * 64, soff, 0);
+                                               voC + toff + j * 64, 0, 0);
         acc[mq][nq][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }

@@ -186,6 +186,9 @@ class BertHG38Dataset(torch.utils.data.Dataset):
     # same mask statistics as the reference's torch-RNG draws; __getitem__ keeps the
     # reference's exact torch draw order for the parity tests. bpe + stdmlm only; any other
     # configuration falls back to per-item __getitem__.
+    # Indices may arrive epoch-tagged (EpochSampler: epoch * len + i), so a window draws a fresh
+    # mask every epoch as the reference's per-__getitem__ torch draws do; mask_seed is set from
+    # train.seed by the data module's owner.
     mask_seed = 2222
     bpe_threads = 0  # 0: all cores (set per worker by BertHG38 when it starts several workers)
 
@@ -194,8 +197,9 @@ class BertHG38Dataset(torch.utils.data.Dataset):
                 and not self.replace_N_token and hasattr(self.tokenizer, "encode_windows")):
             return [self[i] for i in indices]
         wins = []
+        n = len(self.rows)
         for i in indices:
-            chr_name, start, end = self.rows[i]
+            chr_name, start, end = self.rows[int(i) % n]
             wins.append(self.fasta(chr_name, start, end, max_length=self.max_length,
                                    return_augs=self.return_augs))
         tok = self.tokenizer
@@ -210,7 +214,7 @@ class BertHG38Dataset(torch.utils.data.Dataset):
         return out
 
     def __getitem__(self, idx):
-        chr_name, start, end = self.rows[idx]
+        chr_name, start, end = self.rows[int(idx) % len(self.rows)]
         seq = self.fasta(chr_name, start, end, max_length=self.max_length,
                          return_augs=self.return_augs)
         seq = self._ids(seq)
@@ -229,6 +233,39 @@ class BertHG38Dataset(torch.utils.data.Dataset):
             return bert_mask(data, tok.mask_token_id, tok.pad_token_id, tok.vocab_size,
                              special_token_ids=tok.all_special_ids), target
         return random_mask(data, tok.mask_token_id), target
+
+
+class EpochSampler(torch.utils.data.Sampler):
+    """Wraps the loader's index sampler and tags every index with the epoch (epoch * len + i):
+    the indices travel to the (persistent) worker processes with each batch, so the dataset's
+    masking key changes per epoch without any state in the workers. set_epoch is forwarded to a
+    wrapped DistributedSampler (permutation = randperm(seed + epoch), as torch DDP)."""
+
+    def __init__(self, base, n):
+        self.base, self.n, self.epoch = base, int(n), 0
+
+    def set_epoch(self, epoch):
+        self.epoch = int(epoch)
+        if hasattr(self.base, "set_epoch"):
+            self.base.set_epoch(epoch)
+
+    def __iter__(self):
+        off = self.epoch * self.n
+        return (off + int(i) for i in self.base)
+
+    def __len__(self):
+        return len(self.base)
+
+
+def worker_context(num_workers):
+    """DataLoader workers are never forked from a process whose HIP runtime is up (train.py and
+    bench.py build their loaders after the model is on the GPU): a forked child inherits the
+    parent's HIP/HSA state -- queues, doorbells, and under rocprofv3 the profiler's interception
+    of them -- and can fault in it. Such a process gets spawned workers (the native FASTA and BPE
+    handles re-open on unpickle); before GPU init the default fork stays."""
+    if num_workers > 0 and torch.cuda.is_available() and torch.cuda.is_initialized():
+        return "spawn"
+    return None
 
 
 def host_threads():
@@ -318,11 +355,15 @@ class BertHG38(SequenceDataset):
         # each worker tokenises whole batches with the native multithreaded BPE: split the cores
         cores = host_threads()
         dataset.bpe_threads = max(1, cores // max(1, self.num_workers)) if self.num_workers else 0
+        if sampler is None:
+            sampler = (torch.utils.data.RandomSampler(dataset) if shuffle
+                       else torch.utils.data.SequentialSampler(dataset))
         return torch.utils.data.DataLoader(dataset, batch_size=batch_size,
-                                           num_workers=self.num_workers, shuffle=shuffle,
-                                           sampler=sampler, drop_last=self.drop_last,
-                                           pin_memory=self.pin_memory,
-                                           persistent_workers=self.num_workers > 0)
+                                           num_workers=self.num_workers,
+                                           sampler=EpochSampler(sampler, len(dataset)),
+                                           drop_last=self.drop_last, pin_memory=self.pin_memory,
+                                           persistent_workers=self.num_workers > 0,
+                                           multiprocessing_context=worker_context(self.num_workers))
 
     def train_dataloader(self, sampler=None, **kwargs):
         return self._data_loader(self.dataset_train, self.batch_size,

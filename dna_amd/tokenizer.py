@@ -110,9 +110,10 @@ class CharacterTokenizer:
     any other character (lowercase, space) -> [UNK]. With special tokens the sequence is
     `ids + [SEP]` (build_inputs_with_special_tokens, :88-96); truncation keeps room for it;
     padding with [PAD] on the LEFT (padding_side default 'left').
-    Parity: restated from the source -- the reference class does not construct under the
-    transformers 5.x installed here (it needs its vocab before PreTrainedTokenizer.__init__),
-    so no fixture could be generated by running it (unpinned)."""
+    Parity: tests/golden/char_golden.npz -- the reference class's constructor body and methods
+    run unmodified by tests/golden/make_char_golden.py (its base-class constructor, which fails
+    under the transformers 5.x here, replaced by a recorder); the 4.28 padding / truncation of
+    __call__ around them is restated (tests/test_char_tokenizer.py)."""
     special = {"[CLS]": 0, "[SEP]": 1, "[BOS]": 2, "[MASK]": 3, "[PAD]": 4, "[RESERVED]": 5,
                "[UNK]": 6}
 

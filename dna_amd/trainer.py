@@ -76,11 +76,14 @@ class MLMTrainer:
         self.model.dropout_rng.seed = int(st["seed"])
         self.model.dropout_rng.offset = int(st["offset"])
 
-    def step(self, batch) -> torch.Tensor:
+    def step(self, batch, accum=None) -> torch.Tensor:
         """One optimizer step over one micro-batch or a list of them (accumulate_grad_batches:
-        each micro-batch loss is divided by their number, like Lightning; gradients are
-        all-reduced only during the last micro-batch's backward, like DDP no_sync)."""
+        each micro-batch loss is divided by `accum` -- default their number -- like Lightning,
+        which divides by accumulate_grad_batches even in an epoch's short last window;
+        gradients are all-reduced only during the last micro-batch's backward, like DDP
+        no_sync)."""
         micro = batch if isinstance(batch, (list, tuple)) else [batch]
+        div = len(micro) if accum is None else int(accum)
         self.opt.zero_grad()
         total = None
         self.micro_losses = []
@@ -90,8 +93,8 @@ class MLMTrainer:
             loss, _ = self.model.mlm_loss(mb.masked_ids, mb.mask, mb.index, mb.n_mask,
                                           mb.n_unk_masked)
             self.micro_losses.append(loss.detach())
-            if len(micro) > 1:
-                loss = loss / len(micro)
+            if div > 1:
+                loss = loss / div
             loss.backward()
             total = loss.detach() if total is None else total + loss.detach()
         self.reducer.finish()

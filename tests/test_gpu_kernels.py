@@ -469,3 +469,36 @@ def test_gemm_geglu_fused_equals_unfused(p):
     dg2 = torch.empty_like(dg)
     _gemm_call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, M, F, p, 11, 5, dg2.data_ptr())
     assert torch.equal(dg, dg2)
+
+
+@pytest.mark.parametrize("M", [1, 255, 257, 300, 1000])
+@pytest.mark.parametrize("kind", ["fwd", "geglu"])
+def test_gemm_persistent_ragged_rows_write_nothing_past_m(M, kind):
+    """Canary for the persistent kernel's ragged last tile: the output is a view at the head of a
+    NaN-filled buffer and the operand rows past M are NaN; every row < M equals fp32 torch, and
+    not one element after the M output rows changes (rows past M fall out of the buffer
+    resource's range check -- loads read zero, stores are dropped)."""
+    g = torch.Generator(device="cpu").manual_seed(M)
+    K, N, F = 768, 768, 3072
+    xb = torch.full((M + 256, K), float("nan"), device=DEV, dtype=torch.bfloat16)
+    xb[:M] = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    x = xb[:M]
+    if kind == "fwd":
+        w = (torch.randn(N, K, generator=g) * 0.05).to(DEV).bfloat16()
+        b = torch.randn(N, generator=g).to(DEV)
+        buf = torch.full((M + 512, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        _gemm_call("dna_linear_fwd", x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, buf.data_ptr())
+        torch.cuda.synchronize()
+        assert _rel(buf[:M], x.float() @ w.float().t() + b) < 1e-2
+        assert torch.isnan(buf[M:]).all()
+    else:
+        wg = (torch.randn(2 * F, K, generator=g) * 0.05).to(DEV).bfloat16()
+        bg = (torch.randn(2 * F, generator=g) * 0.1).to(DEV)
+        gbuf = torch.full((M + 512, 2 * F), float("nan"), device=DEV, dtype=torch.bfloat16)
+        abuf = torch.full((M + 512, F), float("nan"), device=DEV, dtype=torch.bfloat16)
+        _gemm_call("dna_geglu_linear_fwd", x.data_ptr(), wg.data_ptr(), bg.data_ptr(), M, F, K, 0.0,
+                   1, 0, gbuf.data_ptr(), abuf.data_ptr())
+        torch.cuda.synchronize()
+        assert _rel(gbuf[:M], x.float() @ wg.float().t() + bg) < 1e-2
+        assert torch.isnan(gbuf[M:]).all() and torch.isnan(abuf[M:]).all()
+        assert not torch.isnan(abuf[:M]).any()

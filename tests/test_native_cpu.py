@@ -196,3 +196,43 @@ def test_bert_hg38_dataset_item(tmp_path):
     assert target.tolist() == ref_ids
     batch = next(iter(dm.train_dataloader()))
     assert batch[0][0].shape == (4, 128) and batch[1].shape == (4, 128)
+
+
+def test_bert_hg38_masks_change_per_epoch(tmp_path):
+    """Batched path (Philox masks): the same window gets a fresh mask every epoch (the
+    reference draws torch RNG per __getitem__, hg38_dataset.py:258-279) and the same mask when
+    an epoch is replayed (mid-epoch resume); the DistributedSampler permutation is
+    randperm(seed + epoch) on one rank too."""
+    from dna_amd.hg38 import BertHG38
+    from dna_amd.synthetic import write_hg38
+    write_hg38(str(tmp_path), n_chroms=1, chrom_len=60_000, max_length=1024)
+    dm = BertHG38(bed_file=str(tmp_path / "bert_hg38/human-sequences.bed"),
+                  fasta_file=str(tmp_path / "bert_hg38/hg38.ml.fa"), tokenizer_name="bpe",
+                  max_length=1024, pad_max_length=130, add_eos=False, batch_size=4,
+                  num_workers=0)
+    dm.setup()
+    ds = dm.dataset_train
+    smp = torch.utils.data.distributed.DistributedSampler(ds, num_replicas=1, rank=0, shuffle=True,
+                                                          seed=7)
+    loader = dm.train_dataloader(sampler=smp)
+
+    def epoch_masks(e):
+        loader.sampler.set_epoch(e)
+        order = list(smp)
+        out = {}
+        for (masked, mask, labels), target in loader:
+            for j in range(target.shape[0]):
+                out[len(out)] = (mask[j].clone(), target[j].clone())
+        # window id -> mask, via the epoch's permutation
+        return {order[k]: v for k, v in out.items()}
+
+    e0, e0b, e1 = epoch_masks(0), epoch_masks(0), epoch_masks(1)
+    assert set(e0) == set(e1) == set(range(len(ds)))
+    same = sum(torch.equal(e0[i][0], e1[i][0]) for i in e0)
+    assert same == 0, f"{same} windows kept their epoch-0 mask in epoch 1"
+    for i in e0:
+        assert torch.equal(e0[i][0], e0b[i][0]) and torch.equal(e0[i][1], e1[i][1])
+    loader.sampler.set_epoch(0)
+    p0 = list(smp)
+    loader.sampler.set_epoch(1)
+    assert p0 != list(smp)

@@ -161,11 +161,14 @@ def train(cfg, dry_run=False, out=sys.stdout):
         else:
             warnings.warn(f"resume checkpoint {resume} not found; training from scratch")
 
-    sampler = None
-    if world > 1:
-        sampler = torch.utils.data.distributed.DistributedSampler(
-            ds.dataset_train, num_replicas=world, rank=rank, shuffle=True,
-            seed=int(seed or 0))
+    # the permutation is randperm(seed + epoch) on every world size (DistributedSampler
+    # semantics), so a mid-epoch resume replays exactly the interrupted epoch's
+    # order, and the masks are keyed on (train.seed, epoch, window) (EpochSampler)
+    sampler = torch.utils.data.distributed.DistributedSampler(
+        ds.dataset_train, num_replicas=world, rank=rank,
+        shuffle=True if world > 1 else bool(getattr(ds, "shuffle", True)), seed=int(seed or 0))
+    if seed is not None and hasattr(ds.dataset_train, "mask_seed"):
+        ds.dataset_train.mask_seed = (int(seed) * 0x9E3779B1 + 2222) & (2 ** 63 - 1)
     loader = ds.train_dataloader(sampler=sampler)
     accum = int(tr.get("accumulate_grad_batches", 1) or 1)
     max_steps = cfg.train.get("max_steps") or tr.get("max_steps")
@@ -192,7 +195,9 @@ def train(cfg, dry_run=False, out=sys.stdout):
     epoch = start_epoch
 
     def optimizer_step(micro):
-        loss = trainer.step([m for m, _ in micro])
+        # Lightning 1.8 divides every micro-batch loss by accumulate_grad_batches, also in the
+        # epoch's last, shorter window
+        loss = trainer.step([m for m, _ in micro], accum=accum)
         for (_, numel), ml in zip(micro, trainer.micro_losses):
             ppl.update_count(ml, numel)  # numel = target.numel() of that micro-batch
             ntok.count = ntok.count + numel
@@ -219,7 +224,9 @@ def train(cfg, dry_run=False, out=sys.stdout):
                             {"num_tokens_local": int(ntok.count)})
 
     for epoch in range(start_epoch, max_epochs):
-        if sampler is not None:
+        if hasattr(loader.sampler, "set_epoch"):
+            loader.sampler.set_epoch(epoch)  # EpochSampler: forwarded to the DistributedSampler
+        else:
             sampler.set_epoch(epoch)
         ppl.reset()
         n_batches = len(loader)
