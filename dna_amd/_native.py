@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DNA_AMD_LIB", os.path.join(_HERE, "lib", "libdna_amd.so"))
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "dna_amd.h")
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 ACT_NONE, ACT_GELU = 0, 1
 
 _vp, _i, _u64, _f, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_float, ctypes.c_size_t
@@ -28,6 +28,10 @@ _SIGS = {
     "dna_attn_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp]),
     "dna_attn_bwd_ex": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp]),
     "dna_attn_dbias_part_rows": (_i, [_i, _i]),
+    "dna_flash_lse_rows": (_i, [_i]),
+    "dna_flash_fwd": (_i, [_vp, _i, _vp, _i, _i, _i64, _i64, _i64, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp]),
+    "dna_flash_bwd": (_i, [_vp, _i, _vp, _i, _i, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i,
+                           _f, _vp, _vp, _vp]),
     "dna_colsum_f32": (_i, [_vp, _i, _i, _vp, _i, _vp]),
     "dna_causal_conv1d_fwd": (_i, [_vp, _sz, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "dna_causal_conv1d_part_rows": (_sz, [_i, _i]),

@@ -125,6 +125,8 @@ struct Args {
   int dbg;                    // diagnostics (DNA_GEMM_DBG): 1 = stores dropped (OOB), 2 = no stores,
                               // 4 = output stores with the sc0 cache policy (A/B)
   int nt;                     // persistent kernel: non-temporal output stores (DNA_GEMM_NT, default 0)
+  int order;                  // persistent kernel unit order: 0 = round-robin over the grid (XCD-
+                              // remapped), 1 = XCD-major (each XCD sweeps one contiguous unit range)
 };
 
 __device__ __forceinline__ void tile_of(const Args& a, int& mt, int& nt) {
@@ -523,10 +525,25 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int G = gridDim.x, b = blockIdx.x;
-  const int L = xcd_remap(b, G);  // blocks of one XCD: consecutive units
   const int U = a.tilesM * a.tilesN;
-  const int nb = L < U ? (U - L + G - 1) / G : 0;
+  // this block's units: ubase + i * ustride, i < nb
+  int ubase, ustride, nb;
+  if (a.order == 1 && (G & 7) == 0) {
+    // XCD-major: the blocks sharing an L2 (b % 8) sweep one contiguous eighth of the unit order,
+    // so an A row panel is fetched into one L2 and used there for every column tile
+    const int X = b & 7, j = b >> 3, GX = G >> 3;
+    const int lo = (int)(((long long)U * X) >> 3), hi = (int)(((long long)U * (X + 1)) >> 3);
+    ubase = lo + j;
+    ustride = GX;
+    nb = j < hi - lo ? (hi - lo - j + GX - 1) / GX : 0;
+  } else {
+    const int L = xcd_remap(b, G);  // blocks of one XCD: consecutive units
+    ubase = L;
+    ustride = G;
+    nb = L < U ? (U - L + G - 1) / G : 0;
+  }
   if (nb == 0) return;
+  const int L = ubase;
   const int KT = a.K / BK;
   const int V = nb * KT;
   float* bias_lds = reinterpret_cast<float*>(smem + LDS_BYTES);
@@ -558,7 +575,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     Cur c;
     c.i = i;
     c.kt = 0;
-    unit_tile<EPI>(a, min(i, nb - 1) * G + L, c.m0, c.n0);
+    unit_tile<EPI>(a, ubase + min(i, nb - 1) * ustride, c.m0, c.n0);
     return c;
   };
   auto advance = [&](Cur& c) {
@@ -1065,6 +1082,8 @@ int launchp(Args& a, hipStream_t s, const char* name) {
   if (const char* e = getenv("DNA_GEMM_DBG")) a.dbg = atoi(e);
   a.nt = 0;
   if (const char* e = getenv("DNA_GEMM_NT")) a.nt = atoi(e);
+  a.order = 0;
+  if (const char* e = getenv("DNA_GEMM_ORDER")) a.order = atoi(e);
   hipLaunchKernelGGL((gemmp_kernel<EPI>), dim3(G), dim3(NTHR), 0, s, a);
   DNA_LAUNCH_CHECK(name);
   return DNA_OK;

@@ -13,16 +13,22 @@ asserts (flash_attn_triton.py:849-855) -- instead of letting a kernel read out o
     torch.ops.dna_amd.geglu_bwd(da, g, p, seed, offset, dg)
     torch.ops.dna_amd.xent_fwd(logits, target, loss, lse)         per-row CE
     torch.ops.dna_amd.transpose_bf16(src, dst)
-and the functional slot of the reference's FlashAttention call site (bert_layers.py:167-178 ->
-flash_attn_qkvpacked_func, flash_attn_triton.py:1077-1130), autograd included:
+and the reference's FlashAttention kernel slot with its own signature (flash_attn_triton.py:
+1077-1130, called at bert_layers.py:188/192 as flash_attn_qkvpacked_func(qkv, bias)), autograd
+included:
 
-    out, lse = torch.ops.dna_amd.flash_attn_qkvpacked(qkv[b,S,3,H,D], slopes[H],
-                                                      key_valid[b,S] | None, softmax_scale)
-    out = dna_amd.ops.flash_attn_qkvpacked_func(qkv, slopes, key_valid, softmax_scale)
-The ALiBi + key-pad bias enters as (slopes, key_valid) instead of a materialised [b,H,S,S] bias
-tensor: bias[h,i,j] = -slopes[h]*|i-j| + (key j pad ? -10000 : 0), exactly what
-bert_layers.py:421-448 builds. The model's own autograd Functions (dna_amd.functional) call the
-same C ABI directly (no per-call dispatcher overhead on the ~300 launches of a step).
+    out = dna_amd.ops.flash_attn_qkvpacked_func(qkv[b,S,3,H,D], bias=None, causal=False,
+                                                softmax_scale=None)
+    out, lse = torch.ops.dna_amd.flash_attn_qkvpacked(qkv, bias, causal, softmax_scale)
+with the reference's bias forms ("vector" [., ., 1, S] / "matrix" [., ., S, S], batch / head
+broadcast, fp32 or the qkv dtype), fp16 and bf16, any S, head_dim <= 128 (csrc/flash_slot.hip).
+The model itself runs the fast path, where the ALiBi + key-pad bias enters as (slopes,
+key_valid) instead of a materialised [b,H,S,S] tensor: bias[h,i,j] = -slopes[h]*|i-j| +
+(key j pad ? -10000 : 0), exactly what bert_layers.py:421-448 builds:
+
+    out = dna_amd.ops.alibi_attn_qkvpacked_func(qkv, slopes, key_valid, softmax_scale)
+The model's own autograd Functions (dna_amd.functional) call the C ABI directly (no per-call
+dispatcher overhead on the ~300 launches of a step).
 """
 import math
 
@@ -84,10 +90,11 @@ def attn_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torc
            delta.data_ptr(), N.stream_ptr())
 
 
-@torch.library.custom_op("dna_amd::flash_attn_qkvpacked", mutates_args=())
-def flash_attn_qkvpacked(qkv: torch.Tensor, slopes: torch.Tensor, key_valid: torch.Tensor | None,
+@torch.library.custom_op("dna_amd::alibi_attn_qkvpacked", mutates_args=())
+def alibi_attn_qkvpacked(qkv: torch.Tensor, slopes: torch.Tensor, key_valid: torch.Tensor | None,
                          softmax_scale: float | None = None) -> tuple[torch.Tensor, torch.Tensor]:
-    """-> (out [b, S, H, D], lse [b, H, S] fp32 natural-log softmax normaliser)."""
+    """The model's fast path: the ALiBi + key-pad bias of bert_layers.py:421-448 from (slopes,
+    key_valid), never materialised. -> (out [b, S, H, D], lse [b, H, S] fp32 natural log)."""
     _check(qkv.dim() == 5 and qkv.shape[2] == 3, f"qkv must be [b, S, 3, H, D], got {tuple(qkv.shape)}")
     b, S, _, H, D = qkv.shape
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
@@ -99,13 +106,13 @@ def flash_attn_qkvpacked(qkv: torch.Tensor, slopes: torch.Tensor, key_valid: tor
     return out.view(b, S, H, D), lse
 
 
-@flash_attn_qkvpacked.register_fake
+@alibi_attn_qkvpacked.register_fake
 def _(qkv, slopes, key_valid, softmax_scale=None):
     b, S, _, H, D = qkv.shape
     return qkv.new_empty(b, S, H, D), qkv.new_empty(b, H, S, dtype=torch.float32)
 
 
-def _fa_setup(ctx, inputs, output):
+def _alibi_setup(ctx, inputs, output):
     qkv, slopes, key_valid, softmax_scale = inputs
     out, lse = output
     ctx.save_for_backward(qkv, slopes, key_valid if key_valid is not None else torch.empty(0),
@@ -114,7 +121,7 @@ def _fa_setup(ctx, inputs, output):
     ctx.scale = softmax_scale
 
 
-def _fa_backward(ctx, dout, dlse):
+def _alibi_backward(ctx, dout, dlse):
     qkv, slopes, key_valid, out, lse = ctx.saved_tensors
     b, S, _, H, D = qkv.shape
     scale = ctx.scale if ctx.scale is not None else 1.0 / math.sqrt(D)
@@ -126,13 +133,118 @@ def _fa_backward(ctx, dout, dlse):
     return dqkv.view(qkv.shape), None, None, None
 
 
-flash_attn_qkvpacked.register_autograd(_fa_backward, setup_context=_fa_setup)
+alibi_attn_qkvpacked.register_autograd(_alibi_backward, setup_context=_alibi_setup)
 
 
-def flash_attn_qkvpacked_func(qkv, slopes, key_valid=None, softmax_scale=None):
-    """Drop-in for flash_attn_qkvpacked_func at bert_layers.py:167-178 (returns out only); the
-    bias argument is replaced by the ALiBi slopes and the key-valid mask it is built from."""
-    return torch.ops.dna_amd.flash_attn_qkvpacked(qkv, slopes, key_valid, softmax_scale)[0]
+def alibi_attn_qkvpacked_func(qkv, slopes, key_valid=None, softmax_scale=None):
+    """The fast path: out of alibi_attn_qkvpacked (bias = -slopes[h]*|i-j| + pad*-10000)."""
+    return torch.ops.dna_amd.alibi_attn_qkvpacked(qkv, slopes, key_valid, softmax_scale)[0]
+
+
+# ------------------------------------------------------------------- generic FlashAttention slot
+_FDT = {torch.bfloat16: N.BF16, torch.float16: N.F16, torch.float32: N.F32}
+
+
+def _bias_args(bias, b, H, S, qkv_dtype):
+    """The reference's bias handling (flash_attn_triton.py:780-807): 4-D, fp32 or the qkv dtype,
+    last dims (1, S) "vector" or (S, S) "matrix", first dims broadcastable to (b, H) -- broadcast
+    as stride 0 here instead of repeat copies. -> (bias, dtype code, type, sb, sh, sq)."""
+    if bias is None:
+        return None, N.F32, 0, 0, 0, 0
+    _check(bias.dtype in (qkv_dtype, torch.float32), f"bias dtype {bias.dtype} must be fp32 or {qkv_dtype}")
+    _check(bias.is_cuda, "bias must be on the GPU")
+    _check(bias.dim() == 4, f"bias must be 4-D, got {bias.dim()}-D")
+    if bias.stride(-1) != 1:
+        bias = bias.contiguous()
+    if tuple(bias.shape[2:]) == (1, S):
+        btype = 1
+    elif tuple(bias.shape[2:]) == (S, S):
+        btype = 2
+    else:
+        raise RuntimeError("Last 2 dimensions of bias must be (1, seqlen_k) or (seqlen_q, seqlen_k)")
+    _check(bias.shape[0] in (1, b) and bias.shape[1] in (1, H),
+           f"First 2 dimensions of bias must be broadcastible to (batch, nheads) = ({b}, {H}). "
+           f"Bias has shape: {tuple(bias.shape)}")
+    sb = bias.stride(0) if bias.shape[0] == b and b > 1 else 0
+    sh = bias.stride(1) if bias.shape[1] == H and H > 1 else 0
+    sq = bias.stride(2) if btype == 2 else 0
+    return bias, _FDT[bias.dtype], btype, sb, sh, sq
+
+
+def _pad_head(t, Dp):
+    D = t.shape[-1]
+    return t if D == Dp else torch.nn.functional.pad(t, (0, Dp - D))
+
+
+def _kernel_dim(D):
+    _check(D <= 128, "FlashAttention only support head dimensions up to 128")
+    return 32 if D <= 32 else (64 if D <= 64 else 128)
+
+
+@torch.library.custom_op("dna_amd::flash_attn_qkvpacked", mutates_args=())
+def flash_attn_qkvpacked(qkv: torch.Tensor, bias: torch.Tensor | None = None, causal: bool = False,
+                         softmax_scale: float | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """_flash_attn_forward over packed qkv [b, S, 3, H, D] (flash_attn_triton.py:767-860)
+    -> (out [b, S, H, D], lse [b, H, ceil(S/128)*128] fp32 natural log)."""
+    _check(qkv.dim() == 5 and qkv.shape[2] == 3, f"qkv must be [b, S, 3, H, D], got {tuple(qkv.shape)}")
+    _check(qkv.dtype in (torch.float16, torch.bfloat16), "Only support fp16 and bf16")
+    _check(qkv.is_cuda, "qkv must be on the GPU (no CPU fallback)")
+    b, S, _, H, D = qkv.shape
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    Dp = _kernel_dim(D)
+    x = _pad_head(qkv, Dp).contiguous()
+    bias, bdt, btype, sb, sh, sq = _bias_args(bias, b, H, S, qkv.dtype)
+    out = torch.empty(b, S, H, Dp, device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty(b, H, N.lib().dna_flash_lse_rows(S), device=qkv.device, dtype=torch.float32)
+    N.call("dna_flash_fwd", x.data_ptr(), _FDT[qkv.dtype], _p(bias), bdt, btype, sb, sh, sq, b, S, H,
+           Dp, int(bool(causal)), scale, out.data_ptr(), lse.data_ptr(), N.stream_ptr())
+    return (out if Dp == D else out[..., :D].contiguous()), lse
+
+
+@flash_attn_qkvpacked.register_fake
+def _(qkv, bias=None, causal=False, softmax_scale=None):
+    b, S, _, H, D = qkv.shape
+    return qkv.new_empty(b, S, H, D), qkv.new_empty(b, H, (S + 127) // 128 * 128, dtype=torch.float32)
+
+
+def _flash_setup(ctx, inputs, output):
+    qkv, bias, causal, softmax_scale = inputs
+    out, lse = output
+    ctx.save_for_backward(qkv, bias if bias is not None else torch.empty(0), out, lse)
+    ctx.has_bias = bias is not None
+    ctx.causal = bool(causal)
+    ctx.scale = softmax_scale
+
+
+def _flash_backward(ctx, dout, dlse):
+    qkv, bias, out, lse = ctx.saved_tensors
+    # flash_attn_triton.py:1109-1110
+    _check(not ctx.needs_input_grad[1], "FlashAttention does not support bias gradient yet")
+    b, S, _, H, D = qkv.shape
+    scale = ctx.scale if ctx.scale is not None else 1.0 / math.sqrt(D)
+    Dp = _kernel_dim(D)
+    x = _pad_head(qkv, Dp).contiguous()
+    o = _pad_head(out, Dp).contiguous()
+    g = _pad_head(dout, Dp).contiguous()
+    bias, bdt, btype, sb, sh, sq = _bias_args(bias if ctx.has_bias else None, b, H, S, qkv.dtype)
+    delta = torch.empty_like(lse)
+    dqkv = torch.empty_like(x)
+    N.call("dna_flash_bwd", x.data_ptr(), _FDT[qkv.dtype], _p(bias), bdt, btype, sb, sh, sq,
+           o.data_ptr(), g.data_ptr(), lse.data_ptr(), b, S, H, Dp, int(ctx.causal), scale,
+           delta.data_ptr(), dqkv.data_ptr(), N.stream_ptr())
+    return (dqkv if Dp == D else dqkv[..., :D].contiguous()), None, None, None
+
+
+flash_attn_qkvpacked.register_autograd(_flash_backward, setup_context=_flash_setup)
+
+
+def flash_attn_qkvpacked_func(qkv, bias=None, causal=False, softmax_scale=None):
+    """Drop-in for flash_attn_qkvpacked_func (flash_attn_triton.py:1077-1130, the reference's
+    _FlashAttnQKVPackedFunc.apply): same positional signature and semantics -- qkv [b, S, 3, H, D]
+    fp16 / bf16, bias broadcastible to (b, H, S, S) as "vector" [., ., 1, S] or "matrix"
+    [., ., S, S] (fp32 or qkv dtype), causal, softmax_scale (default 1/sqrt(D)); returns
+    out [b, S, H, D]; the backward gives dqkv (no bias gradient, as the reference)."""
+    return torch.ops.dna_amd.flash_attn_qkvpacked(qkv, bias, bool(causal), softmax_scale)[0]
 
 
 # ------------------------------------------------------------------------------- GEMM
@@ -195,5 +307,6 @@ def xent_fwd(logits: torch.Tensor, target: torch.Tensor, loss: torch.Tensor,
            loss.data_ptr(), lse.data_ptr(), N.stream_ptr())
 
 
-OPS = ("attn_fwd", "attn_bwd", "flash_attn_qkvpacked", "linear_fwd", "transpose_bf16",
+OPS = ("attn_fwd", "attn_bwd", "alibi_attn_qkvpacked", "flash_attn_qkvpacked", "linear_fwd",
+       "transpose_bf16",
        "geglu_fwd", "geglu_bwd", "xent_fwd")

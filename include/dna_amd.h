@@ -33,7 +33,7 @@ enum dna_status {
   DNA_ERR_NOMEM = 5        /* host allocation failed or caller buffer too small */
 };
 
-enum dna_dtype { DNA_F32 = 0, DNA_BF16 = 1 };
+enum dna_dtype { DNA_F32 = 0, DNA_BF16 = 1, DNA_F16 = 2 };
 enum dna_act { DNA_ACT_NONE = 0, DNA_ACT_GELU = 1 };
 
 int dna_abi_version(void);
@@ -55,6 +55,30 @@ const char* dna_last_error(void);
 int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const float* slopes, int batch,
                  int seqlen, int heads, int head_dim, int dtype, float softmax_scale, void* out,
                  float* lse, void* stream);
+
+/* ------------------------------------------------------------------ generic FlashAttention slot
+ * flash_attn_qkvpacked_func(qkv, bias=None, causal=False, softmax_scale=None) with the reference's
+ * signature (src/models/sequence/flash_attn_triton.py:1077-1130; _flash_attn_forward :767-860,
+ * _flash_attn_backward :863-1074; call site src/models/DNABERT2/bert_layers.py:188,192):
+ *   qkv  [batch, seqlen, 3, heads, head_dim] contiguous, dtype DNA_BF16 or DNA_F16, head_dim
+ *        32 / 64 / 128, any seqlen;
+ *   bias bias_type 0 none, 1 "vector" [., ., 1, seqlen], 2 "matrix" [., ., seqlen, seqlen];
+ *        element (b, h, q, k) at bias[b*bias_sb + h*bias_sh + q*bias_sq + k] (a stride of 0
+ *        broadcasts that dim, as the reference's repeat does); bias_dtype DNA_F32 or the qkv dtype;
+ *   out  [batch, seqlen, heads, head_dim] (qkv dtype); lse [batch, heads, dna_flash_lse_rows]
+ *        fp32 natural-log LSE (the reference's seqlen_q_rounded layout).
+ * softmax(q k^T * softmax_scale + bias), causal masks key > query. The backward writes dqkv
+ * [batch, seqlen, 3, heads, head_dim]; delta is caller workspace [batch, heads, lse rows]. */
+int dna_flash_lse_rows(int seqlen);
+int dna_flash_fwd(const void* qkv, int dtype, const void* bias, int bias_dtype, int bias_type,
+                  long long bias_sb, long long bias_sh, long long bias_sq, int batch, int seqlen,
+                  int heads, int head_dim, int causal, float softmax_scale, void* out, float* lse,
+                  void* stream);
+int dna_flash_bwd(const void* qkv, int dtype, const void* bias, int bias_dtype, int bias_type,
+                  long long bias_sb, long long bias_sh, long long bias_sq, const void* out,
+                  const void* dout, const float* lse, int batch, int seqlen, int heads,
+                  int head_dim, int causal, float softmax_scale, float* delta, void* dqkv,
+                  void* stream);
 
 /* Backward of dna_attn_fwd (replaces autograd through bert_layers.py:167-178 and
  * _flash_attn_backward, flash_attn_triton.py:941-1074). Writes dqkv [T, 3*H*D] (dtype).

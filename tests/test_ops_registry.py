@@ -22,8 +22,8 @@ def test_ops_registered_and_reject_cpu():
 
 
 @pytest.mark.gpu
-def test_flash_attn_slot_matches_product_attention():
-    """The functional FlashAttention slot (fwd + autograd bwd) == dna_amd.functional.alibi_attention
+def test_alibi_attn_op_matches_product_attention():
+    """The ALiBi fast-path operator (fwd + autograd bwd) == dna_amd.functional.alibi_attention
     on the same packed inputs, bit for bit (same kernels), with pad keys."""
     from dna_amd import functional as DF
     from dna_amd import ops
@@ -35,7 +35,7 @@ def test_flash_attn_slot_matches_product_attention():
     valid[1, 200:] = False
     valid = valid.cuda()
     slopes = torch.tensor(alibi_slopes(H), dtype=torch.float32).cuda()
-    out = ops.flash_attn_qkvpacked_func(qkv, slopes, valid)
+    out = ops.alibi_attn_qkvpacked_func(qkv, slopes, valid)
     dout = torch.randn(out.shape, generator=g).cuda().bfloat16()
     out.backward(dout)
     q2 = qkv.detach().clone().view(b * S, 3 * H * D).requires_grad_(True)
