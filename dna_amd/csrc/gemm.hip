@@ -859,8 +859,6 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
   const int nb = L < U ? (U - L + G - 1) / G : 0;
   if (nb == 0) return;
 
-  const auto rA = out_rsrc(a.dy, (uint32_t)((size_t)a.T * a.ldy * 2));
-  const auto rB = out_rsrc(a.x, (uint32_t)((size_t)a.T * a.ldx * 2));
   uint32_t voA[2], voB[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -889,18 +887,23 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
     if (++c.kt == c.len) c = cur_at(c.i + 1);
   };
   auto img = [&](int v, int h) { return smem + ((v & 1) * 4 + h) * HALF; };
+  // one buffer resource per (chunk, operand): base at the chunk's first token row, records up to
+  // its last row (or T), so offsets stay 32-bit for any T and rows past T read as zeros
   auto stage = [&](const Cur& c, int v, int h) {
-    const int step = c.t0 + (c.i < nb ? c.kt : c.len - 1);
-    const int trow = step * BK;
+    const int kt = c.i < nb ? c.kt : c.len - 1;
     char* d = img(v, h);
     const bool isA = h < 2;
     const int col0 = isA ? c.m0 + h * 128 : c.n0 + (h - 2) * 128;
     const int ld = isA ? a.ldy : a.ldx;
-    const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane((trow * ld + col0) * 2);
+    const long long r0 = (long long)c.t0 * BK;
+    const int rows = min((long long)a.T, (long long)(c.t0 + c.len) * BK) - r0;
+    const bf16* base = (isA ? a.dy : a.x) + r0 * ld;
+    const auto rs = out_rsrc(base, (uint32_t)((size_t)rows * ld * 2));
+    const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane((kt * BK * ld + col0) * 2);
 #pragma unroll
-    for (int p = 0; p < 2; ++p)  // offset in voffset: token rows past T fail the range check
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, (lds_t*)(d + (p * 32 + wave * 4) * 256),
-                                               16, (isA ? voA[p] : voB[p]) + toff, 0, 0, 0);
+    for (int p = 0; p < 2; ++p)  // offset in voffset: token rows past the chunk fail the range check
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(d + (p * 32 + wave * 4) * 256), 16,
+                                               (isA ? voA[p] : voB[p]) + toff, 0, 0, 0);
   };
 
   f32x4 acc[2][2][4][2];
@@ -1229,8 +1232,9 @@ extern "C" int dna_linear_wgrad_p(const void* dy, const void* x, int M, int N, i
                 "dna_linear_wgrad_p: N, K %% 256 required (N=%d K=%d)", N, K);
   const int KTtot = (M + BK - 1) / BK;
   DNA_CHECK_ARG(splits >= 1 && KTtot / splits >= 2, "dna_linear_wgrad_p: bad splits %d", splits);
-  DNA_CHECK_ARG((size_t)M * (N > K ? N : K) * 2 < (1ull << 31) && (size_t)splits * N * K * 4 < (1ull << 32),
-                "dna_linear_wgrad_p: operands too large for 32-bit buffer offsets");
+  DNA_CHECK_ARG((size_t)((KTtot + splits - 1) / splits) * BK * (N > K ? N : K) * 2 < (1ull << 31) &&
+                    (size_t)splits * N * K * 4 < (1ull << 32),
+                "dna_linear_wgrad_p: chunks / partials too large for 32-bit buffer offsets");
   WArgs a{};
   a.dy = (const bf16*)dy; a.ldy = N;
   a.x = (const bf16*)x; a.ldx = K;

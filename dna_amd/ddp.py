@@ -19,9 +19,19 @@ import torch.distributed as dist
 
 
 class GradBucketReducer:
-    def __init__(self, flat, bucket_mb: float = 25.0, group=None):
+    """wire_dtype "fp32" (default) all-reduces the fp32 gradient buckets in place; "bf16" halves
+    the bytes on the wire (234 MB instead of 468 MB for DNABERT-2): each bucket is
+    cast to a persistent bf16 staging slice when it fires, all-reduced (SUM) there, and cast back
+    into the fp32 flat gradient in finish(), after its collective. The 1/world average stays in
+    the AdamW kernel either way (grad_scale)."""
+
+    def __init__(self, flat, bucket_mb: float = 25.0, group=None, wire_dtype="fp32"):
         self.flat = flat
         self.group = group
+        if wire_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"wire_dtype {wire_dtype!r}: fp32 or bf16")
+        self.wire_dtype = wire_dtype
+        self._wire = None  # bf16 staging buffer (allocated on first use)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         cap = int(bucket_mb * 1024 * 1024 / 4)
         # contiguous buckets of whole parameters, in flat (= backward) order
@@ -66,8 +76,17 @@ class GradBucketReducer:
         from .functional import join_side_stream
         if self.flat.grad.is_cuda:
             join_side_stream()
-        self._works.append(dist.all_reduce(self.flat.grad[s:e], op=dist.ReduceOp.SUM,
-                                           group=self.group, async_op=True))
+        if self.wire_dtype == "bf16":
+            if self._wire is None:
+                self._wire = torch.empty(self.flat.grad.numel(), dtype=torch.bfloat16,
+                                         device=self.flat.grad.device)
+            w = self._wire[s:e]
+            w.copy_(self.flat.grad[s:e])
+            self._works.append((dist.all_reduce(w, op=dist.ReduceOp.SUM, group=self.group,
+                                                async_op=True), s, e))
+        else:
+            self._works.append((dist.all_reduce(self.flat.grad[s:e], op=dist.ReduceOp.SUM,
+                                                group=self.group, async_op=True), s, e))
 
     def prepare(self, sync=True):
         """Call before each backward; sync=False for accumulation micro-batches (no collective,
@@ -96,8 +115,10 @@ class GradBucketReducer:
         for bi in range(len(self.buckets)):
             if not self._fired[bi]:
                 self._launch(bi)
-        for w in self._works:
+        for w, s, e in self._works:
             w.wait()
+            if self.wire_dtype == "bf16":
+                self.flat.grad[s:e].copy_(self._wire[s:e])
         self._works = []
 
     @property

@@ -42,7 +42,9 @@ class SelectiveScan(torch.autograd.Function):
         states = torch.empty(N.lib().dna_selective_scan_states(b, d, l, n), device=u.device,
                              dtype=torch.float32)
         last = torch.empty(b, d, n, device=u.device, dtype=torch.float32) if return_last_state else None
-        with _timed("selective_scan_fwd", b * d * l * 3 * u.element_size(), "byte"):
+        # algorithmic HBM bytes: u, delta (+ z), B, C in, out
+        nbytes = (b * d * l * (4 if z is not None else 3) + 2 * b * n * l) * u.element_size()
+        with _timed("selective_scan_fwd", nbytes, "byte"):
             N.call("dna_selective_scan_fwd", u.data_ptr(), delta.data_ptr(), A32.data_ptr(),
                    B.data_ptr(), C.data_ptr(), _p(D32), _p(z), _p(db32), int(bool(delta_softplus)),
                    _dt(u), b, d, l, n, out.data_ptr(), states.data_ptr(), _p(last), N.stream_ptr())
@@ -68,7 +70,10 @@ class SelectiveScan(torch.autograd.Function):
         dC = torch.zeros_like(dB)
         dD = torch.zeros(d, device=u.device, dtype=torch.float32) if has_D else None
         dbias = torch.zeros(d, device=u.device, dtype=torch.float32) if has_bias else None
-        with _timed("selective_scan_bwd", b * d * l * 5 * u.element_size(), "byte"):
+        # u, delta, dout (+ z), B, C in; du, ddelta (+ dz) out; dB, dC fp32 out
+        nz = 2 if z is not None else 0
+        nbytes = (b * d * l * (5 + nz) + 2 * b * n * l) * u.element_size() + 2 * b * n * l * 4
+        with _timed("selective_scan_bwd", nbytes, "byte"):
             N.call("dna_selective_scan_bwd", u.data_ptr(), delta.data_ptr(), A32.data_ptr(),
                    B.data_ptr(), C.data_ptr(), _p(D32), _p(z), _p(db32), int(softplus), _dt(u),
                    b, d, l, n, states.data_ptr(), dout.data_ptr(), du.data_ptr(), ddelta.data_ptr(),

@@ -219,7 +219,8 @@ def _flash_setup(ctx, inputs, output):
 def _flash_backward(ctx, dout, dlse):
     qkv, bias, out, lse = ctx.saved_tensors
     # flash_attn_triton.py:1109-1110
-    _check(not ctx.needs_input_grad[1], "FlashAttention does not support bias gradient yet")
+    _check(not (ctx.has_bias and ctx.needs_input_grad[1]),
+           "FlashAttention does not support bias gradient yet")
     b, S, _, H, D = qkv.shape
     scale = ctx.scale if ctx.scale is not None else 1.0 / math.sqrt(D)
     Dp = _kernel_dim(D)

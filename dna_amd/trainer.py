@@ -42,10 +42,49 @@ class DeviceBatch:
                                                        idx.flat_masked))), n_mask, n_unk)
 
 
+class ModuleTrainer:
+    """The same data-parallel step for any model (BASELINE configs D / E: HyenaDNA, Caduceus):
+    parameters and gradients in one flat buffer (FlatParams), gradient buckets all-reduced over
+    RCCL as they complete in the backward (GradBucketReducer, fp32 or bf16 wire), global-norm clip
+    + AdamW in one fused launch (FusedAdamW), the 1/world average folded into it. `loss_fn(model,
+    batch)` returns the scalar loss; with `autocast` set it runs under torch.autocast (the configs'
+    bf16 mixed precision: fp32 master weights, bf16 compute)."""
+
+    def __init__(self, model, device, loss_fn, lr=1e-3, weight_decay=0.0, betas=(0.9, 0.999),
+                 eps=1e-8, max_grad_norm=1.0, bucket_mb=25.0, wire_dtype="fp32",
+                 autocast=torch.bfloat16):
+        self.model = model.to(device).train()
+        self.device = torch.device(device)
+        self.loss_fn = loss_fn
+        self.autocast = autocast
+        self.flat = FlatParams(self.model, device, shadow_dtype=None)
+        self.opt = FusedAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                              max_grad_norm=max_grad_norm)
+        self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
+        self.world = self.reducer.world
+        if self.world > 1:  # DDP construction broadcast
+            dist.broadcast(self.flat.flat, src=0)
+        self.global_step = 0
+
+    def step(self, batch) -> torch.Tensor:
+        self.opt.zero_grad()
+        self.reducer.prepare(sync=True)
+        if self.autocast is not None:
+            with torch.autocast(self.device.type, dtype=self.autocast):
+                loss = self.loss_fn(self.model, batch)
+        else:
+            loss = self.loss_fn(self.model, batch)
+        loss.backward()
+        self.reducer.finish()
+        self.opt.step(grad_scale=self.reducer.grad_scale)
+        self.global_step += 1
+        return loss.detach()
+
+
 class MLMTrainer:
     def __init__(self, model: BertForMaskedLM, device, lr=5e-4, weight_decay=1e-5,
                  betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0, scheduler=None,
-                 bucket_mb=25.0, seed=None):
+                 bucket_mb=25.0, seed=None, wire_dtype="fp32"):
         self.model = model.to(device).train()
         self.device = device
         self.flat = FlatParams(self.model, device)
@@ -55,7 +94,7 @@ class MLMTrainer:
         self.sched = None
         if scheduler is not None:
             self.sched = LinearLRSchedulerWarmup(self.opt, **scheduler)
-        self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb)
+        self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
         self.world = self.reducer.world
         if self.world > 1:  # DDP construction broadcast (C2 in SURVEY §2.2)
             dist.broadcast(self.flat.flat, src=0)

@@ -49,9 +49,10 @@ def _check(b, S, H, D, dtype, bias, causal, tol_o=2.5e-2, tol_g=3e-2, seed=0):
     ref.backward(dout.float())
     rel = float((qkv.grad.float() - x32.grad).norm() / x32.grad.norm())
     assert rel < tol_g, rel
-    for t in range(3):  # q, k and v gradients each
-        r_t = float((qkv.grad[:, :, t].float() - x32.grad[:, :, t]).norm() / x32.grad[:, :, t].norm())
-        assert r_t < tol_g, (t, r_t)
+    for t in range(3):  # q, k and v gradients each (S = 1: softmax == 1, dq == dk == 0 exactly)
+        ref_n = float(x32.grad[:, :, t].norm())
+        diff = float((qkv.grad[:, :, t].float() - x32.grad[:, :, t]).norm())
+        assert diff <= tol_g * ref_n + 1e-6, (t, diff, ref_n)
 
 
 def test_reference_call_site_dnabert2_bias_with_pads():

@@ -77,7 +77,7 @@ def _free_port():
     return p
 
 
-def _ddp_worker(rank, world, port, q):
+def _ddp_worker(rank, world, port, q, wire="fp32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -92,7 +92,7 @@ def _ddp_worker(rank, world, port, q):
         head.weight = emb.weight  # tied: two gradient contributions per step
         m["head"] = head
         flat = FlatParams(m, "cpu", shadow_dtype=None)
-        red = GradBucketReducer(flat, bucket_mb=0.002)  # tiny buckets -> many collectives
+        red = GradBucketReducer(flat, bucket_mb=0.002, wire_dtype=wire)  # tiny buckets
         assert len(red.buckets) > 3
         results = []
         for step in range(3):
@@ -138,11 +138,14 @@ def _single_grads():
     return out
 
 
-def test_grad_bucket_reducer_gloo_two_ranks():
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_grad_bucket_reducer_gloo_two_ranks(wire):
+    """fp32 wire: exact average; bf16 wire (SURVEY §8(e) 234 MB format): within bf16 rounding of
+    the summands (one cast per rank, the sum itself rounded once more)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q, wire)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
@@ -152,8 +155,13 @@ def test_grad_bucket_reducer_gloo_two_ranks():
     ref = _single_grads()
     for step in range(3):
         a, b = torch.tensor(res[0][step]), torch.tensor(res[1][step])
-        assert torch.allclose(a, b)  # every rank holds the same averaged gradient
-        assert torch.allclose(a, ref[step], atol=1e-6), (a - ref[step]).abs().max()
+        assert torch.equal(a, b)  # every rank holds the same averaged gradient
+        if wire == "fp32":
+            assert torch.allclose(a, ref[step], atol=1e-6), (a - ref[step]).abs().max()
+        else:
+            rel = float((a - ref[step]).norm() / ref[step].norm())
+            assert rel < 1e-2, rel
+            assert not torch.equal(a, ref[step])  # the bf16 wire really was used
 
 
 def _metrics_worker(rank, world, port, q):
