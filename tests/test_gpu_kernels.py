@@ -502,3 +502,54 @@ def test_gemm_persistent_ragged_rows_write_nothing_past_m(M, kind):
         assert _rel(gbuf[:M], x.float() @ wg.float().t() + bg) < 1e-2
         assert torch.isnan(gbuf[M:]).all() and torch.isnan(abuf[M:]).all()
         assert not torch.isnan(abuf[:M]).any()
+
+
+# ------------------------------------------------------------------ bench-shape GEMM parity
+BENCH_T = 512 * 512  # per-GPU batch 512 x S 512 tokens (bench.py default)
+
+
+def _sample_rows(M, n=384, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    rows = torch.randint(0, M, (n,), generator=g)
+    return torch.cat([rows, torch.tensor([0, 1, 255, 256, M // 2 - 1, M // 2, M - 2, M - 1])]).to(DEV)
+
+
+def test_gemm_bench_shape_gated_fwd_and_k6144_dgrad():
+    """The two row-blocked calls of the step at T = 262,144 (operands past 2^31 bytes): the
+    gated_layers forward (N = 6144, K = 768) and its data gradient (K = 6144 on the transposed
+    weight), on sampled rows (incl. both sides of the row-block boundary) vs fp32 torch."""
+    T, F2, H = BENCH_T, 6144, 768
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(T, H, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(F2, H, device=DEV, generator=g) * 0.05).bfloat16()
+    y = torch.empty(T, F2, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_linear_fwd", x.data_ptr(), w.data_ptr(), None, T, F2, H, y.data_ptr())
+    mc = ((1 << 31) - 1) // (F2 * 2) // 256 * 256
+    rows = torch.cat([_sample_rows(T), torch.tensor([mc - 1, mc, mc + 1], device=DEV)])
+    assert _rel(y[rows], x[rows].float() @ w.float().t()) < 1e-2
+    del y
+    dy = torch.randn(T, F2, device=DEV, generator=g).bfloat16()
+    wt = w.t().contiguous()  # [768, 6144]: the transposed bf16 copy FlatParams keeps
+    dx = torch.empty(T, H, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, T, H, F2, dx.data_ptr())
+    assert _rel(dx[rows], dy[rows].float() @ w.float()) < 1e-2
+
+
+@pytest.mark.parametrize("n,k", [(2304, 768), (768, 768), (6144, 768), (768, 3072)])
+def test_wgrad_p_bench_shapes(n, k):
+    """dna_linear_wgrad_p (the hand-written token-major weight gradient, fp32 chunk partials +
+    dna_sum_slices_accum) at the step's four projection shapes and T = 262,144 vs fp32 torch,
+    and accumulating into an existing gradient; plus a ragged T."""
+    from dna_amd import functional as DF
+    for T in (BENCH_T, 100_003):
+        g = torch.Generator(device=DEV).manual_seed(n + k + T)
+        dy = torch.randn(T, n, device=DEV, generator=g).bfloat16()
+        x = torch.randn(T, k, device=DEV, generator=g).bfloat16()
+        ref = dy.float().t() @ x.float()
+        prev = torch.randn(n, k, device=DEV, generator=g)
+        grad = prev.clone()
+        parts, s = DF._hip_wgrad_parts(dy, x)
+        assert s >= 1 and parts.shape == (s, n, k)
+        from dna_amd import _native as N
+        N.call("dna_sum_slices_accum", parts.data_ptr(), s, n * k, grad.data_ptr(), N.stream_ptr())
+        assert _rel(grad - prev, ref) < 1e-5, (T, s)
