@@ -1418,7 +1418,7 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
   bf16* Kimg = reinterpret_cast<bf16*>(smem);          // [S][64] swz
   bf16* Qimg = Kimg + S * D;                            // [2][32][64] swz
   bf16* Oimg = Qimg + 2 * 32 * D;                       // [2][32][64] dO, swz
-  bf16* dST = Oimg + 2 * 32 * D;                        // [S][32] dS^T, 8-B chunks XOR (row>>2)
+  bf16* dST = Oimg + 2 * 32 * D;                        // [S][32] dS^T, 8-B chunks XOR (row>>1)&7
   float* rc = reinterpret_cast<float*>(dST + S * 32);  // [2][4][32] row constants (as dkdv2)
   float* red = reinterpret_cast<float*>(smem + bwd3_red_off<KB>());  // [2][1024] dQ^T partials
                                                                       // of key half 1
@@ -1497,7 +1497,8 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
   // sig[kb] = sum over the queries this lane holds of dS[q][key]: the dQ column sums of the bias
   // gradient are sum_key K[key][d] * sum_q dS[q][key] (per-key sums, contracted with K in the
   // epilogue), so the loop carries KB floats instead of per-slice cross-lane reductions
-  // (kept in LDS, sigl[key][hh], read early in each block and written back by the owner lane:
+  // (kept in LDS, sigl[hh][key] -- consecutive keys on consecutive lanes, conflict-free -- read
+  // early in each block and written back by the owner lane:
   // four loop-carried registers more push the loop over the register file)
   float* sigl = red + 2 * 1024;
   if (DBL)
@@ -1593,7 +1594,7 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
       bf16x8 pb[2], sb[2];
       bf16x8 ao, aq;
       float ssum = 0.f;
-      const float sold = (DBL && kb < KB) ? sigl[2 * (kbase + kl_t) + hh] : 0.f;
+      const float sold = (DBL && kb < KB) ? sigl[hh * S + kbase + kl_t] : 0.f;
       if (kb > 0) { ao = tr_pair(O, 0); aq = tr_pair(Q, 0); }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -1620,16 +1621,19 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
       }
       if (kb > 0) {
         // dS^T image of block kb-1: register group g holds q = 8g + 4hh + 0..3 of key kl (the
-        // chunk swizzle ((key >> 2) & 7) depends on kl only, blocks being 32-aligned)
+        // chunk swizzle ((key >> 1) & 7) depends on kl only, blocks being 32-aligned). A 16-lane
+        // ds_write_b64 group (kl 0..15) then covers all 32 banks of its (a/4) mod 32 map: the
+        // odd / even kl split the two 64-B halves, (kl >> 1) & 7 the 8-B slots (the former
+        // (kl >> 2) & 7 key put kl and kl + 2 on one bank: a 2-way conflict on every write)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const bf16x8& src = sbp[g >> 1];
           const bf16x4 v = {src[4 * (g & 1)], src[4 * (g & 1) + 1], src[4 * (g & 1) + 2], src[4 * (g & 1) + 3]};
-          *reinterpret_cast<bf16x4*>(dSTw + (kb - 1) * 32 * 32 + kl * 32 + 4 * ((2 * g + hh) ^ ((kl >> 2) & 7))) = v;
+          *reinterpret_cast<bf16x4*>(dSTw + (kb - 1) * 32 * 32 + kl * 32 + 4 * ((2 * g + hh) ^ ((kl >> 1) & 7))) = v;
         }
       }
       if (kb < KB) {
-        if (DBL) sigl[2 * (kbase + kl_t) + hh] = sold + ssum;
+        if (DBL) sigl[hh * S + kbase + kl_t] = sold + ssum;
         pbp[0] = pb[0]; pbp[1] = pb[1];
         sbp[0] = sb[0]; sbp[1] = sb[1];
       }
@@ -1645,22 +1649,17 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
       const int dcol = 32 * dth + 16 * (g16 & 1) + 4 * (i16 & 3);
       const int qc = 4 * (g16 & 1) + (i16 & 3);  // 8-B chunk of q = 16(g16&1) + 4(i16&3)
       // rows 16ks + r (r = 4hh + (i16>>2), and + 8): swz(16ks + r, c) = 16ks*D + swz(r, c); the
-      // dS^T chunk swizzle ((row >> 2) & 7) = (4ks + (r >> 2)) & 7 alternates with ks & 1
+      // dS^T chunk swizzle ((row >> 1) & 7) = (r >> 1) & 7 does not depend on ks
       const int rr = 4 * (g16 >> 1) + (i16 >> 2);
       const int ka0 = swz(rr, dcol), ka1 = swz(rr + 8, dcol);
-      int sa0[2], sa1[2];
-#pragma unroll
-      for (int par = 0; par < 2; ++par) {
-        sa0[par] = rr * 32 + 4 * (qc ^ ((4 * par + (rr >> 2)) & 7));
-        sa1[par] = (rr + 8) * 32 + 4 * (qc ^ ((4 * par + ((rr + 8) >> 2)) & 7));
-      }
+      const int sa0 = rr * 32 + 4 * (qc ^ ((rr >> 1) & 7));
+      const int sa1 = (rr + 8) * 32 + 4 * (qc ^ (((rr + 8) >> 1) & 7));
       // operands of step ks + PF are read while step ks multiplies (LDS latency off the chain)
       constexpr int PF = KS2 < 4 ? KS2 : 4;
       bf16x8 ra[PF], rb[PF];
       auto rd = [&](int ks, bf16x8& a, bf16x8& bb) {
-        const int par = ks & 1;
         a = cat(tr_read(Kh + 16 * ks * D + ka0), tr_read(Kh + 16 * ks * D + ka1));
-        bb = cat(tr_read(dSTh + 16 * ks * 32 + sa0[par]), tr_read(dSTh + 16 * ks * 32 + sa1[par]));
+        bb = cat(tr_read(dSTh + 16 * ks * 32 + sa0), tr_read(dSTh + 16 * ks * 32 + sa1));
       };
 #pragma unroll
       for (int ks = 0; ks < PF; ++ks) rd(ks, ra[ks], rb[ks]);
@@ -1751,7 +1750,7 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
         const int key = wave * KPW + 32 * kb + kl_e;
-        sgm[kb] = sigl[2 * key] + sigl[2 * key + 1];
+        sgm[kb] = sigl[key] + sigl[S + key];
       }
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {

@@ -102,6 +102,33 @@ __device__ __forceinline__ bf16x4 tr_read(const char* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
+// tr_read with the row offset as an instruction immediate: the address VGPR is per-lane and
+// per-fragment (computed once per read group), the k-block / row-half steps are immediates
+template <int OFF>
+__device__ __forceinline__ bf16x4 tr_read_imm(uint32_t addr) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return __builtin_bit_cast(bf16x4, v);
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+// lane part of read_n's address for k-block 0, row half 0 of the fragment whose columns start
+// at c0: rows k and k + 4 (the other row half) and k + 32 (k-block 1) share the chunk swizzle
+__device__ __forceinline__ uint32_t read_n_lane_off(int c0, int lane) {
+  const int i = lane & 15, kq = lane >> 4;
+  const int r = kq * 8 + (i >> 2);
+  const int col = c0 + 4 * (i & 3);
+  return (uint32_t)(r * 256 + ((((col >> 3) ^ nswz(r)) << 4) + (col & 7) * 2));
+}
+// both k-blocks of one fragment: {kk = 0, kk = 1}
+__device__ __forceinline__ void read_n2(uint32_t addr, bf16x8& k0, bf16x8& k1) {
+  const bf16x4 a = tr_read_imm<0>(addr), b = tr_read_imm<1024>(addr);
+  const bf16x4 c = tr_read_imm<8192>(addr), d = tr_read_imm<9216>(addr);
+  k0 = bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  k1 = bf16x8{c[0], c[1], c[2], c[3], d[0], d[1], d[2], d[3]};
+}
+
 // MFMA operand (8 consecutive k of one column) from a [64 k][128] image: two transposed reads.
 // lane l: image column c0 + (l&15), k = kbase + 8*(l>>4) + j
 __device__ __forceinline__ bf16x8 read_n(const char* img, int kbase, int c0, int lane) {
@@ -1127,19 +1154,20 @@ __global__ __launch_bounds__(NTHR) void wgradr_kernel(WArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[q][r][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  uint32_t loA[4], loB[2];  // per-lane parts of the fragment addresses (k-block / row half: immediates)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) loA[i] = read_n_lane_off(wr * 64 + i * 16, lane);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) loB[j] = read_n_lane_off(wc * 32 + j * 16, lane);
   auto readA = [&](int v, int mq) {
-    const char* im = slot(v, mq);
+    const uint32_t im = lds_addr(slot(v, mq));
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_n(im, kk * 32, wr * 64 + i * 16, lane);
+    for (int i = 0; i < 4; ++i) read_n2(im + loA[i], af[i][0], af[i][1]);
   };
   auto readB = [&](int v, int nq, bf16x8 (&bf)[2][2]) {
-    const char* im = slot(v, 2 + nq);
+    const uint32_t im = lds_addr(slot(v, 2 + nq));
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = read_n(im, kk * 32, wc * 32 + j * 16, lane);
+    for (int j = 0; j < 2; ++j) read_n2(im + loB[j], bf[j][0], bf[j][1]);
   };
   auto mma = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
     __builtin_amdgcn_s_setprio(1);

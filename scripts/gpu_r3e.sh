@@ -10,4 +10,8 @@ cat $O/wgrad.jsonl
 timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 200 --timeout-method thread -k "bench_shape or wgrad or ragged" > $O/tests.txt 2>&1
 rc=$?
 grep -E "PASS|FAIL|Error|assert" $O/tests.txt | tail -30
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 200 --timeout-method thread -k "attention" > $O/attn.txt 2>&1
+rc=$?
+tail -3 $O/attn.txt
 exit $rc
