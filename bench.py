@@ -82,6 +82,27 @@ def make_batches(n_batches, batch, rank, device):
     return out
 
 
+def measure_data_pipeline(batch, device):
+    """train.py's data path: registry dataset bert_hg38 over a synthetic FASTA/BED -> torch
+    DataLoader (batched __getitems__: FASTA -> native multithreaded BPE -> native masking; 8
+    worker processes sharing this rank's host threads) -> DeviceBatch.from_host (row bookkeeping
+    + pinned H2D copy), steady state over 60 batches."""
+    import shutil
+    from dna_amd.hg38 import host_threads
+    from scripts.data_pipeline_bench import measure, synthetic_root
+    # enough 4096-bp windows for warm-up + 60 timed batches of this size in one epoch
+    root = synthetic_root(n_chroms=8, chrom_len=16_777_216 * max(1, -(-batch // 256)))
+    workers = 8
+    try:
+        rate = measure(root, workers, batch, 60, device=device)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return {"seq_per_s": round(rate, 1), "threads": host_threads(), "workers": workers,
+            "what": "train.py data path: BertHG38 DataLoader (FASTA -> native BPE -> masking, "
+                    "8 workers) + DeviceBatch.from_host (pinned H2D) over 4096-bp synthetic hg38 "
+                    "windows, steady state over 60 batches; not part of value"}
+
+
 def cpu_baseline(seconds_budget=10.0, threads=None, cfg=None, seq=None, batch=2, max_seq=100000,
                  label="DNABERT-2-117M S=512"):
     """Oracle restatement (PyTorch CPU fp32, oracle/bert_ref.py, pinned to the reference) timing
@@ -224,6 +245,12 @@ def main():
               file=sys.stderr)
     if args.dist_dry_run:
         return dist_skeleton(args, world, rank)
+
+    data_pipeline = None
+    if rank == 0 and world == 1 and not args.no_data_pipeline:
+        # train.py's own data path, timed before this process touches the GPU (its DataLoader
+        # workers fork from a clean process; the H2D leg then brings HIP up) -- not part of value
+        data_pipeline = measure_data_pipeline(args.batch, torch.device("cuda", local))
     # DNA_DIST_BACKEND=gloo (rehearsal only): every rank on the visible GPUs round-robin, gradient
     # all-reduce over gloo -- exercises the multi-rank bench path on a one-GPU box
     backend = os.environ.get("DNA_DIST_BACKEND", "nccl")
@@ -249,27 +276,8 @@ def main():
     t_data = time.perf_counter()
     batches = make_batches(4, args.batch, rank, device)
     t_data = time.perf_counter() - t_data
-    data_pipeline = None
-    # the host data path is measured once per node, on single-GPU runs (not part of value)
-    if rank == 0 and world == 1 and not args.no_data_pipeline:
-        # train.py's own data path, timed before the GPU region (not part of value): registry
-        # dataset bert_hg38 over a synthetic FASTA/BED -> torch DataLoader (batched __getitems__:
-        # FASTA -> native multithreaded BPE -> native masking; 8 worker processes sharing this
-        # rank's host threads) -> DeviceBatch.from_host (row bookkeeping + pinned H2D copy)
-        from dna_amd.hg38 import host_threads
-        from scripts.data_pipeline_bench import measure, synthetic_root
-        # enough 4096-bp windows for warm-up + 60 timed batches of this size in one epoch
-        root = synthetic_root(n_chroms=8, chrom_len=16_777_216 * max(1, -(-args.batch // 256)))
-        workers = 8
-        data_pipeline = {"seq_per_s": round(measure(root, workers, args.batch, 60, device=device), 1),
-                         "threads": host_threads(), "workers": workers,
-                         "bench_batch_prep_seq_per_s": round(4 * args.batch / t_data, 1),
-                         "what": "train.py data path: BertHG38 DataLoader (FASTA -> native BPE -> "
-                                 "masking, 8 workers) + DeviceBatch.from_host (pinned H2D) over "
-                                 "4096-bp synthetic hg38 windows, steady state over 60 batches; "
-                                 "not part of value"}
-        import shutil
-        shutil.rmtree(root, ignore_errors=True)
+    if data_pipeline is not None:
+        data_pipeline["bench_batch_prep_seq_per_s"] = round(4 * args.batch / t_data, 1)
 
     for i in range(args.warmup):
         trainer.step(batches[i % len(batches)])

@@ -257,13 +257,22 @@ class EpochSampler(torch.utils.data.Sampler):
         return len(self.base)
 
 
+def _profiler_attached():
+    """rocprofv3 preloads its tool library, which brings the HSA runtime up before main()."""
+    pre = os.environ.get("LD_PRELOAD", "")
+    return "rocprof" in pre or any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+
+
 def worker_context(num_workers):
-    """DataLoader workers are never forked from a process whose HIP runtime is up (train.py and
-    bench.py build their loaders after the model is on the GPU): a forked child inherits the
-    parent's HIP/HSA state -- queues, doorbells, and under rocprofv3 the profiler's interception
-    of them -- and can fault in it. Such a process gets spawned workers (the native FASTA and BPE
-    handles re-open on unpickle); before GPU init the default fork stays."""
-    if num_workers > 0 and torch.cuda.is_available() and torch.cuda.is_initialized():
+    """DataLoader workers are never forked from a process whose HIP runtime is up (train.py builds
+    its loader after the model is on the GPU; under rocprofv3 the tool library has brought HSA up
+    before main): a forked child inherits the parent's HIP/HSA state -- queues, doorbells, the
+    profiler's interception of them -- and can fault in it (round 2's "workers crash under the
+    profiler"). Such a process gets spawned workers (the native FASTA and BPE handles re-open on
+    unpickle); before any GPU init the default fork stays (bench.py measures its data path
+    there)."""
+    if num_workers > 0 and (_profiler_attached() or
+                            (torch.cuda.is_available() and torch.cuda.is_initialized())):
         return "spawn"
     return None
 
