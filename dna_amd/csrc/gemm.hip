@@ -882,6 +882,7 @@ struct WArgs {
   int T, Nw, Kw, tilesM, tilesN, s, KTtot;
 };
 
+template <bool IMM>
 __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
   constexpr int QS = 8;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -952,19 +953,36 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[q][r][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  // IMM: per-lane fragment addresses computed once; k-block / row-half steps are instruction
+  // immediates (4 address VALU per read group instead of 16)
+  uint32_t loA[4], loB[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) loA[i] = read_n_lane_off(wr * 64 + i * 16, lane);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) loB[j] = read_n_lane_off(wc * 32 + j * 16, lane);
   auto readA = [&](int v, int mq) {
     const char* im = img(v, mq);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (IMM) {
+        read_n2(lds_addr(im) + loA[i], af[i][0], af[i][1]);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_n(im, kk * 32, wr * 64 + i * 16, lane);
+        for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_n(im, kk * 32, wr * 64 + i * 16, lane);
+      }
+    }
   };
   auto readB = [&](int v, int nq, bf16x8 (&bf)[2][2]) {
     const char* im = img(v, 2 + nq);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (IMM) {
+        read_n2(lds_addr(im) + loB[j], bf[j][0], bf[j][1]);
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = read_n(im, kk * 32, wc * 32 + j * 16, lane);
+        for (int kk = 0; kk < 2; ++kk) bf[j][kk] = read_n(im, kk * 32, wc * 32 + j * 16, lane);
+      }
+    }
   };
   auto mma = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
@@ -1063,213 +1081,6 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
       kstep(v, role);
       advance(c1);
       advance(c2);
-    }
-    c0 = cur_at(i + 1);
-  }
-  if (wr == 0) DNA_BARRIER();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// The same weight gradient with a 10-slot LDS ring (all 160 KB: the kernel has no bias) so that
-// six half-tiles of LDS-DMA stay in flight instead of four -- both operands stream from HBM here,
-// unlike the forward whose weight operand is L2-resident. Phase p of K-step v stages stream
-// element e = 4v + p, which is half-tile (A0, B0, B1, A1)[p] of K-step v + 2, into slot
-// (e + 2) mod 10; phase 0 reads A0(v), B0(v), phase 1 B1(v), phase 2 A1(v) (lookahead 8, 7, 7, 7
-// phases); a slot is restaged two phases after its last read. The wait of phase p retires stream
-// element 4v + p - 6 (read in phase p + 1): vmcnt(12) plus the partial-sum stores issued after it
-// (QS per quadrant in a unit's last K-step, which are younger than that element for the phases
-// counted in wait_vm below).
-__global__ __launch_bounds__(NTHR) void wgradr_kernel(WArgs a) {
-  constexpr int QS = 8;
-  constexpr int RING = 10;
-  __shared__ __attribute__((aligned(1024))) char smem[RING * HALF];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int G = gridDim.x, b = blockIdx.x;
-  const int L = xcd_remap(b, G);
-  const int tiles = a.tilesM * a.tilesN;
-  const int U = tiles * a.s;
-  const int nb = L < U ? (U - L + G - 1) / G : 0;
-  if (nb == 0) return;
-
-  uint32_t voA[2], voB[2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int r = p * 32 + wave * 4 + (lane >> 4);
-    const int ch = ((lane & 15) ^ nswz(r)) * 16;
-    voA[p] = (uint32_t)(r * a.ldy * 2 + ch);
-    voB[p] = (uint32_t)(r * a.ldx * 2 + ch);
-  }
-  struct Cur { int i, kt, len, t0, m0, n0, c; };
-  auto cur_at = [&](int i) {
-    Cur c;
-    c.i = i;
-    c.kt = 0;
-    const int u = min(i, nb - 1) * G + L;
-    c.c = u / tiles;
-    const int tl = u - c.c * tiles;
-    c.m0 = (tl / a.tilesN) * BM;
-    c.n0 = (tl % a.tilesN) * BN;
-    const int s0 = (int)((long long)c.c * a.KTtot / a.s), s1 = (int)((long long)(c.c + 1) * a.KTtot / a.s);
-    c.t0 = s0;
-    c.len = s1 - s0;
-    return c;
-  };
-  auto advance = [&](Cur& c) {
-    if (++c.kt == c.len) c = cur_at(c.i + 1);
-  };
-  // stream element e -> slot (e + 2) mod 10; half-tile h (A0 A1 B0 B1 = 0 1 2 3) of K-step w is
-  // element 4w - 8 + o, o = (A0, B0, B1, A1) order = {0, 3, 1, 2}[h]
-  auto slot = [&](int w, int h) {
-    const int o = h == 0 ? 0 : (h == 1 ? 3 : h - 1);
-    int e = 4 * w + o + 2;  // (4w - 8 + o + 10)
-    e -= (e / RING) * RING;
-    return smem + e * HALF;
-  };
-  auto stage = [&](const Cur& c, int w, int h) {
-    const int kt = c.i < nb ? c.kt : c.len - 1;
-    char* d = slot(w, h);
-    const bool isA = h < 2;
-    const int col0 = isA ? c.m0 + h * 128 : c.n0 + (h - 2) * 128;
-    const int ld = isA ? a.ldy : a.ldx;
-    const long long r0 = (long long)c.t0 * BK;
-    const int rows = min((long long)a.T, (long long)(c.t0 + c.len) * BK) - r0;
-    const bf16* base = (isA ? a.dy : a.x) + r0 * ld;
-    const auto rs = out_rsrc(base, (uint32_t)((size_t)rows * ld * 2));
-    const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane((kt * BK * ld + col0) * 2);
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(d + (p * 32 + wave * 4) * 256), 16,
-                                               (isA ? voA[p] : voB[p]) + toff, 0, 0, 0);
-  };
-
-  f32x4 acc[2][2][4][2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[q][r][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
-  uint32_t loA[4], loB[2];  // per-lane parts of the fragment addresses (k-block / row half: immediates)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) loA[i] = read_n_lane_off(wr * 64 + i * 16, lane);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) loB[j] = read_n_lane_off(wc * 32 + j * 16, lane);
-  auto readA = [&](int v, int mq) {
-    const uint32_t im = lds_addr(slot(v, mq));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) read_n2(im + loA[i], af[i][0], af[i][1]);
-  };
-  auto readB = [&](int v, int nq, bf16x8 (&bf)[2][2]) {
-    const uint32_t im = lds_addr(slot(v, 2 + nq));
-#pragma unroll
-    for (int j = 0; j < 2; ++j) read_n2(im + loB[j], bf[j][0], bf[j][1]);
-  };
-  auto mma = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = mfma(bf[j][kk], af[i][kk], acc[mq][nq][i][j]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  const int cq = 4 * (lane >> 4);
-  const auto rC = out_rsrc(a.part, (uint32_t)min((size_t)a.s * a.Nw * a.Kw * 4, (size_t)0xFFFFFFF0u));
-  const uint32_t voC = (uint32_t)(((wr * 64 + (lane & 15)) * a.Kw + wc * 32 + cq) * 4);
-  auto store_quadrant = [&](const Cur& c, int mq, int nq) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)((((size_t)c.c * a.Nw + c.m0 + mq * 128 + i * 16) * a.Kw + c.n0 + nq * 128) * 4));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mq][nq][i][j]), rC,
-                                               voC + toff + j * 64, 0, 0);
-        acc[mq][nq][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  };
-
-  // prologue: K-steps 0 and 1 (stream elements -8..-1), in stream order
-  Cur c0 = cur_at(0), cs = c0;
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    stage(cs, w, 0);
-    stage(cs, w, 2);
-    stage(cs, w, 3);
-    stage(cs, w, 1);
-    advance(cs);
-  }
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(12));
-  DNA_BARRIER();
-  if (wr == 1) DNA_BARRIER();
-
-  // role: 0 plain, 1 a unit's last K-step (stores after each quadrant), 2 / 3 the first / second
-  // K-step after one (its stores are still younger than the element being retired)
-  auto wait_vm = [&](auto phase, int role) {
-    constexpr int p = decltype(phase)::value;
-    constexpr int w1 = 12 + p * QS;
-    constexpr int w2 = 12 + (p == 3 ? 3 : 4) * QS;
-    constexpr int w3 = 12 + (p == 0 ? 2 : (p == 1 ? 1 : 0)) * QS;
-    if (role == 0) __builtin_amdgcn_s_waitcnt(waitcnt_imm(12));
-    else if (role == 1) __builtin_amdgcn_s_waitcnt(waitcnt_imm(w1));
-    else if (role == 2) __builtin_amdgcn_s_waitcnt(waitcnt_imm(w2));
-    else __builtin_amdgcn_s_waitcnt(waitcnt_imm(w3));
-  };
-  using P0 = std::integral_constant<int, 0>;
-  using P1 = std::integral_constant<int, 1>;
-  using P2 = std::integral_constant<int, 2>;
-  using P3 = std::integral_constant<int, 3>;
-  auto kstep = [&](int v, int role) {
-    const bool st = role == 1;
-    stage(cs, v + 2, 0);  // A0(v + 2)
-    wait_vm(P0{}, role);
-    readA(v, 0);
-    readB(v, 0, bf0);
-    DNA_BARRIER();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mma(0, 0, bf0);
-    if (st) store_quadrant(c0, 0, 0);
-    DNA_BARRIER();
-    stage(cs, v + 2, 2);  // B0(v + 2)
-    wait_vm(P1{}, role);
-    readB(v, 1, bf1);
-    DNA_BARRIER();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mma(0, 1, bf1);
-    if (st) store_quadrant(c0, 0, 1);
-    DNA_BARRIER();
-    stage(cs, v + 2, 3);  // B1(v + 2)
-    wait_vm(P2{}, role);
-    readA(v, 1);
-    DNA_BARRIER();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mma(1, 1, bf1);
-    if (st) store_quadrant(c0, 1, 1);
-    DNA_BARRIER();
-    stage(cs, v + 2, 1);  // A1(v + 2)
-    wait_vm(P3{}, role);
-    DNA_BARRIER();
-    mma(1, 0, bf0);
-    if (st) store_quadrant(c0, 1, 0);
-    DNA_BARRIER();
-  };
-
-  int v = 0;
-  for (int i = 0; i < nb; ++i) {
-    for (int kt = 0; kt < c0.len; ++kt, ++v) {
-      const int role = kt == c0.len - 1 ? 1 : (i > 0 && kt == 0) ? 2 : (i > 0 && kt == 1) ? 3 : 0;
-      kstep(v, role);
-      advance(cs);
     }
     c0 = cur_at(i + 1);
   }
@@ -1487,12 +1298,11 @@ extern "C" int dna_linear_wgrad_p(const void* dy, const void* x, int M, int N, i
   const int U = a.tilesM * a.tilesN * splits;
   int G = num_cus() & ~7;
   G = U < G ? U : G;
-  const char* re = getenv("DNA_WGRAD_RING");  // A/B: 8 = the two-buffer kernel
-  const int ring = re ? atoi(re) : 10;
-  if (ring == 10)
-    hipLaunchKernelGGL(wgradr_kernel, dim3(G), dim3(NTHR), 0, as_stream(stream), a);
+  const char* ie = getenv("DNA_WGRAD_IMM");  // A/B: 0 = per-read address VALU
+  if (!ie || atoi(ie) != 0)
+    hipLaunchKernelGGL(wgradp_kernel<true>, dim3(G), dim3(NTHR), 0, as_stream(stream), a);
   else
-    hipLaunchKernelGGL(wgradp_kernel, dim3(G), dim3(NTHR), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(wgradp_kernel<false>, dim3(G), dim3(NTHR), 0, as_stream(stream), a);
   DNA_LAUNCH_CHECK("dna_linear_wgrad_p");
   return DNA_OK;
 }

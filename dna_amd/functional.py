@@ -1,8 +1,8 @@
 """Autograd Functions over the dna_amd C ABI (HIP kernels on the current torch stream).
 
-Each Function is one fused HIP op with a hand-written backward; the forward and data-gradient
-GEMMs run the MFMA kernels of csrc/gemm.hip, the fp32 weight gradients (split-K) are the only
-work left to the vendor library (hipBLASLt through torch.bmm).
+Each Function is one fused HIP op with a hand-written backward; the forward, data-gradient and
+weight-gradient GEMMs run the MFMA kernels of csrc/gemm.hip (hipBLASLt through torch only for
+shapes those kernels do not take, or as the DNA_GEMM_IMPL / DNA_WGRAD_IMPL=torch A/B arm).
 No CPU fallback: every op raises if the native library is missing or a tensor is not on a GPU.
 """
 import math
@@ -375,8 +375,9 @@ def _hip_linear(x, w_nk, bias):
 class Linear(torch.autograd.Function):
     """y = x @ w_lp^T (+ b): forward and dgrad on the compute dtype copy `w_lp` of the fp32
     master weight `w` -- bf16: the hand-written MFMA kernel (csrc/gemm.hip), the data gradient
-    on the transposed copy `w_lpt` (dx = dy . w = dy . (w^T)^T, both operands K-major); wgrad
-    produced directly in fp32 (hipBLASLt split-K, out_dtype=float32)."""
+    on the transposed copy `w_lpt` (dx = dy . w = dy . (w^T)^T, both operands K-major); the
+    weight gradient in fp32 from the token-major MFMA kernel (dna_linear_wgrad_p chunk partials
+    folded into the flat gradient by dna_sum_slices_accum)."""
 
     @staticmethod
     def forward(ctx, x, w, w_lp, b, w_lpt):
@@ -501,15 +502,15 @@ def wgrad_splits(rows, m, n, target_tiles=512, max_splits=None):
 
 
 def _hip_wgrad_ok(dy, x):
-    """The persistent token-major wgrad kernel is opt-in (DNA_WGRAD_IMPL=hip): at the bench shapes
-    it reaches ~0.5 PF/s against hipBLASLt's 0.8-1.0 (its waves wait on HBM 77 % of the time:
-    one K-step of LDS-DMA lookahead is too short for first-touch token panels), so the default
-    stays hipBLASLt's split-K batched GEMM."""
+    """The persistent token-major weight-gradient kernel (dna_linear_wgrad_p) for every bf16
+    projection with 256-multiple sides -- all of DNABERT-2's. At the bench shapes (T = 262,144)
+    it is 1-22 % faster than hipBLASLt's split-K batched GEMM (0.40-0.43 of the bf16 peak vs
+    0.34-0.42; profiles/r03/wgrad_ab*.jsonl). DNA_WGRAD_IMPL=torch is the A/B arm."""
     rows, m = dy.shape
     n = x.shape[1]
     return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.is_cuda
             and m % 256 == 0 and n % 256 == 0 and _gemm_impl() == "hip"
-            and os.environ.get("DNA_WGRAD_IMPL", "torch") == "hip")
+            and os.environ.get("DNA_WGRAD_IMPL", "hip") == "hip")
 
 
 def _hip_wgrad_parts(dy, x):
