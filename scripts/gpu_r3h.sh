@@ -17,7 +17,11 @@ lines=open("gpurun_out/r3h/ab_bench.txt").read().splitlines()
 for tag, l in zip(lines[0::2], lines[1::2]):
     d=json.loads(l); print(tag, d["value"], d["ms_per_step"], {k: (v["avg_ms"], v.get("frac")) for k, v in d["kernels"].items() if "gemm" in k})
 PY
-timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_trainer.py -x -v --timeout 300 --timeout-method thread > $O/tests.txt 2>&1
+for v in 0 2 0 2; do
+  echo "attn_fwd=$v $(DNA_ATTN_FWD=$v timeout -k 10 120 python scripts/attn_bench.py --b 512 --which fwd 2>/dev/null | tail -1)" >> $O/ab_attn.txt || exit 1
+done
+cat $O/ab_attn.txt
+timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_trainer.py tests/test_gpu_kernels.py -x -v --timeout 300 --timeout-method thread -k "not bench_shape" > $O/tests.txt 2>&1
 rc=$?
 grep -E "PASS|FAIL|Error|assert" $O/tests.txt | tail -40
 exit $rc
