@@ -335,11 +335,8 @@ __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballo
 // key offset (within a 32-key half, lane half hh excluded) of accumulator register r
 __device__ __forceinline__ constexpr int aoff(int r) { return (r & 3) + 8 * (r >> 2); }
 
-// NW = 8 (S % 512 == 0): one workgroup of 8 waves holds all 512 queries of a (batch, head) at
-// S = 512, so each K/V tile is read from HBM once and shared in LDS by twice the queries (with
-// 4-wave / 256-query workgroups two blocks streamed the same K/V: 1.42x the algorithmic bytes)
-template <int NQB, int NW = 4>
-__global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (NQB == 1 ? 3 : (NQB == 2 ? 2 : 1))) void fwd2_bf16_kernel(const bf16* __restrict__ qkv,
+template <int NQB>
+__global__ __launch_bounds__(256, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_bf16_kernel(const bf16* __restrict__ qkv,
                                                            const uint8_t* __restrict__ key_valid,
                                                            const float* __restrict__ slopes,
                                                            int S, int H, float c,
@@ -351,8 +348,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (NQB == 1 ? 3 : (NQB == 2 ? 
   float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);  // [2][64] pad bias (log2 units)
 
   int qblk, h, b;
-  constexpr int QPB = NW * 32 * NQB;  // queries per workgroup
-  constexpr int CPT = 512 / (NW * 64);  // K (and V) 16-B chunks per thread of a 64-key tile
+  constexpr int QPB = 4 * 32 * NQB;  // queries per workgroup
   decode_block((S + QPB - 1) / QPB, H, qblk, h, b);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches stay uniform
@@ -380,10 +376,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (NQB == 1 ? 3 : (NQB == 2 ? 
   }
 
   // per-lane LDS element offsets (tile buffer, kh and s add immediates)
-  int so[CPT];
+  int so[2];
 #pragma unroll
-  for (int i = 0; i < CPT; ++i) {
-    const int cidx = tid + i * NW * 64;
+  for (int i = 0; i < 2; ++i) {
+    const int cidx = tid + i * 256;
     so[i] = swz(cidx >> 3, (cidx & 7) * 8);
   }
   int kro[4];
@@ -401,8 +397,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (NQB == 1 ? 3 : (NQB == 2 ? 
 
   auto load_tile = [&](int kt, TileRegs& t, float& bias) {
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int cidx = tid + i * NW * 64;
+    for (int i = 0; i < 2; ++i) {
+      const int cidx = tid + i * 256;
       const bf16* src = base + (size_t)(kt * BK + (cidx >> 3)) * ld + h * D + (cidx & 7) * 8;
       t.k[i] = *reinterpret_cast<const bf16x8*>(src + H * D);
       t.v[i] = *reinterpret_cast<const bf16x8*>(src + 2 * H * D);
@@ -412,7 +408,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (NQB == 1 ? 3 : (NQB == 2 ? 
   };
   auto store_tile = [&](int buf, const TileRegs& t, float bias) {
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
+    for (int i = 0; i < 2; ++i) {
       *reinterpret_cast<bf16x8*>(Ks + buf * BK * D + so[i]) = t.k[i];
       *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + so[i]) = t.v[i];
     }
@@ -1978,7 +1974,7 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
   hipStream_t s = as_stream(stream);
   if (dtype == DNA_BF16) {
     // A/B switch for benchmarks: DNA_ATTN_FWD=1 runs the v1 forward
-    const int forced = getenv("DNA_ATTN_FWD") ? atoi(getenv("DNA_ATTN_FWD")) : 0;
+    static const int forced = getenv("DNA_ATTN_FWD") ? atoi(getenv("DNA_ATTN_FWD")) : 0;
     if (forced == 1) {
       dim3 grid(((seqlen + BQ - 1) / BQ) * heads * batch);
       hipLaunchKernelGGL(fwd_bf16_kernel, grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
@@ -1992,11 +1988,7 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
         dim3 grid(((seqlen + 127) / 128) * heads * batch);
         hipLaunchKernelGGL((fwd2_bf16_kernel<1>), grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
                            key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
-      } else if (seqlen % 512 == 0 && forced != 2) {  // 8 waves x 64 queries per workgroup
-        dim3 grid((seqlen / 512) * heads * batch);
-        hipLaunchKernelGGL((fwd2_bf16_kernel<2, 8>), grid, dim3(512), FWD_LDS, s, (const bf16*)qkv,
-                           key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
-      } else {  // DNA_ATTN_FWD=2: the 4-wave / 256-query workgroups (A/B)
+      } else {
         dim3 grid(((seqlen + BQ2 - 1) / BQ2) * heads * batch);
         hipLaunchKernelGGL((fwd2_bf16_kernel<2>), grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
                            key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
