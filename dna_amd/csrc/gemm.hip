@@ -553,7 +553,10 @@ __device__ __forceinline__ void unit_tile(const Args& a, int u, int& m0, int& n0
   n0 = (w / gsz) * (EPI == EPI_GEGLU ? BN / 2 : BN);
 }
 
-template <int EPI>
+// ABL (diagnostic ablations of the main loop, DNA_GEMM_ABL; results are garbage, timing only):
+// 1 = no LDS-DMA staging, 2 = no LDS reads (MFMAs on stale fragments), 4 = no barriers,
+// 8 = no B staging and no B reads, 16 = no B reads, 32 = no B staging
+template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU, "persistent kernel: bf16 / GeGLU epilogues");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
@@ -806,48 +809,58 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   using P2 = std::integral_constant<int, 2>;
   using P3 = std::integral_constant<int, 3>;
   auto kstep = [&](int v, int role) {
+    auto stg = [&](const Cur& c, int vv, int h) {
+      if constexpr (!(ABL & 1)) {
+        if (!(ABL & 40) || h < 2) stage(c, vv, h);
+      }
+    };
+    auto rdA = [&](int vv, int mq) { if constexpr (!(ABL & 2)) readA(vv, mq); };
+    auto rdB = [&](int vv, int nq, bf16x8 (&bf)[2][2]) {
+      if constexpr (!(ABL & 2) && !(ABL & 24)) readB(vv, nq, bf);
+    };
+    auto bar = [&]() { if constexpr (!(ABL & 4)) { DNA_BARRIER(); } else { __builtin_amdgcn_sched_barrier(0); } };
     const bool st = EPI == EPI_BF16 && role == 1;
     const bool sg = EPI == EPI_GEGLU && role == 1;
     // phase 0: quadrant (0,0)
-    stage(c1, v + 1, 3);
+    stg(c1, v + 1, 3);
     wait_vm(P0{}, role);
-    readA(v, 0);
-    readB(v, 0, bf0);
-    DNA_BARRIER();
+    rdA(v, 0);
+    rdB(v, 0, bf0);
+    bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     mma(0, 0, bf0);
     if (st) store_quadrant(c0, 0, 0);
-    DNA_BARRIER();
+    bar();
     // phase 1: quadrant (0,1)
-    stage(c1, v + 1, 1);
+    stg(c1, v + 1, 1);
     wait_vm(P1{}, role);
-    readB(v, 1, bf1);
-    DNA_BARRIER();
+    rdB(v, 1, bf1);
+    bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     mma(0, 1, bf1);
     if (st) store_quadrant(c0, 0, 1);
     if (sg) store_geglu_half(c0, 0);
-    DNA_BARRIER();
+    bar();
     // phase 2: quadrant (1,1)
-    stage(c2, v + 2, 0);
+    stg(c2, v + 2, 0);
     wait_vm(P2{}, role);
-    readA(v, 1);
-    DNA_BARRIER();
+    rdA(v, 1);
+    bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     mma(1, 1, bf1);
     if (st) store_quadrant(c0, 1, 1);
-    DNA_BARRIER();
+    bar();
     // phase 3: quadrant (1,0)
-    stage(c2, v + 2, 2);
+    stg(c2, v + 2, 2);
     wait_vm(P3{}, role);
-    DNA_BARRIER();
+    bar();
     mma(1, 0, bf0);
     if (st) store_quadrant(c0, 1, 0);
     if (sg) store_geglu_half(c0, 1);
-    DNA_BARRIER();
+    bar();
   };
 
   int v = 0;
@@ -1141,7 +1154,16 @@ int launchp(Args& a, hipStream_t s, const char* name) {
   if (const char* e = getenv("DNA_GEMM_NT")) a.nt = atoi(e);
   a.order = 0;
   if (const char* e = getenv("DNA_GEMM_ORDER")) a.order = atoi(e);
-  hipLaunchKernelGGL((gemmp_kernel<EPI>), dim3(G), dim3(NTHR), 0, s, a);
+  const char* ab = getenv("DNA_GEMM_ABL");
+  const int abl = ab ? atoi(ab) : 0;
+  if (abl == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 1>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (abl == 2) hipLaunchKernelGGL((gemmp_kernel<EPI, 2>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (abl == 3) hipLaunchKernelGGL((gemmp_kernel<EPI, 3>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (abl == 7) hipLaunchKernelGGL((gemmp_kernel<EPI, 7>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (abl == 8) hipLaunchKernelGGL((gemmp_kernel<EPI, 8>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (abl == 16) hipLaunchKernelGGL((gemmp_kernel<EPI, 16>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (abl == 32) hipLaunchKernelGGL((gemmp_kernel<EPI, 32>), dim3(G), dim3(NTHR), 0, s, a);
+  else hipLaunchKernelGGL((gemmp_kernel<EPI>), dim3(G), dim3(NTHR), 0, s, a);
   DNA_LAUNCH_CHECK(name);
   return DNA_OK;
 }
