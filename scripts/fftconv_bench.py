@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dna_amd import _native as N  # noqa: E402
 from dna_amd.hyena import fftconv  # noqa: E402
 
-PEAK_HBM = 8000.0
+PEAK_HBM = 8000.0  # GB/s
+PEAK_FP32 = 157.3  # TFLOP/s, MI355X fp32 vector (MI355X_MICROARCH.md)
 
 
 def timeit(fn, iters):
@@ -80,9 +81,19 @@ def main():
         t_torch = timeit(lambda: torch_fftconv(u, k, bias, bi), a.iters)
         fwd_bytes = 2 * B * D * L * s + D * L * 4
         bwd_bytes = 3 * B * D * L * s + 2 * D * L * 4
+        # roofline: max(algorithmic bytes / HBM peak, FFT flops / fp32 VALU peak); flops of an
+        # N-point complex transform = 5 N log2 N, per row pair a forward and an inverse transform
+        # (the backward: dy forward, du inverse, plus one inverse per channel for dk)
+        n = 2 * L
+        lg = n.bit_length() - 1
+        P = (B + 1) // 2 * D
+        fwd_flop = P * 10 * n * lg
+        bwd_flop = P * 10 * n * lg + D * 5 * n * lg
+        b_fwd = max(fwd_bytes / (PEAK_HBM * 1e3), fwd_flop / (PEAK_FP32 * 1e6))
+        b_bwd = max(bwd_bytes / (PEAK_HBM * 1e3), bwd_flop / (PEAK_FP32 * 1e6))
         print(f"{dn} B={B} D={D} L={L} bi={int(bi)}: fwd {t_fwd:8.1f} us ({fwd_bytes / t_fwd / 1e3:7.1f} GB/s alg, "
-              f"{fwd_bytes / t_fwd / 1e3 / PEAK_HBM:.3f} of HBM) | bwd {t_bwd:8.1f} us "
-              f"({bwd_bytes / t_bwd / 1e3:7.1f} GB/s alg) | torch.fft fwd {t_torch:8.1f} us "
+              f"{fwd_bytes / t_fwd / 1e3 / PEAK_HBM:.3f} of HBM, roofline frac {b_fwd / t_fwd:.3f}) | bwd {t_bwd:8.1f} us "
+              f"({bwd_bytes / t_bwd / 1e3:7.1f} GB/s alg, roofline frac {b_bwd / t_bwd:.3f}) | torch.fft fwd {t_torch:8.1f} us "
               f"-> speedup {t_torch / t_fwd:.2f}x", flush=True)
 
 
