@@ -161,7 +161,7 @@ __device__ __forceinline__ void stockham_pass(cf* buf, int G, int logM, int S, i
 }
 
 template <bool INV>
-__device__ void fft_lds(cf* buf, int G, int logM, int S, const cf* twM) {
+__device__ __forceinline__ void fft_lds(cf* buf, int G, int logM, int S, const cf* twM) {
   int logNs = 0, left = logM;
   while (left >= 3) {
     stockham_pass<8, 3, INV>(buf, G, logM, S, logNs, twM);
@@ -215,6 +215,19 @@ struct Pairing {
 struct Geo {
   int L, logN, logM1, logM2;  // N = 2L = M1 * M2
 };
+// Kernels are instantiated for fixed transform sizes (LN = log2 N > 0) next to a generic one
+// (LN = 0): with the geometry a compile-time constant every LDS address of the Stockham passes
+// (sequence, stride, pad slot, twiddle index) folds into immediate offsets instead of per-point
+// shift / mask arithmetic with run-time amounts.
+template <int LN>
+__device__ __forceinline__ Geo fixed(Geo g) {
+  if constexpr (LN > 0) {
+    g.logN = LN;
+    g.logM2 = LN - 1 < 9 ? LN - 1 : 9;
+    g.logM1 = LN - g.logM2;
+  }
+  return g;
+}
 
 // Column passes: G = PTS / M1 columns per block (16 at M1 = 512), column stride M1 + 1 (the
 // transposing global<->LDS copies then spread over the banks). Row pass: G = PTS / M2 rows.
@@ -227,9 +240,10 @@ __host__ __device__ __forceinline__ int log_row_group(const Geo& g) {
 
 // ---------------------------------------------------------------- A: column FFT over n1
 // src rows [.][L] (dtype T); z[n] = x_a[n - off] + i x_b[n - off] (zero outside [0, L)).
-template <typename T>
-__global__ FFT_BOUNDS void col_fwd_kernel(const T* __restrict__ x, Pairing pr, Geo g,
+template <typename T, int LN>
+__global__ FFT_BOUNDS void col_fwd_kernel(const T* __restrict__ x, Pairing pr, Geo g_,
                                                       int off, cf* __restrict__ ws) {
+  const Geo g = fixed<LN>(g_);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M1 = 1 << g.logM1, M2 = 1 << g.logM2;
   const int lcw = log_col_group(g), cw = 1 << lcw;
@@ -282,9 +296,10 @@ enum RowMode { ROW_SPEC = 0, ROW_MUL = 1, ROW_MULCONJ = 2, ROW_INV = 3, ROW_INV_
 // ROW_SPEC: FFT, store the spectrum (natural k2). ROW_MUL(CONJ): FFT, times (conj) kspec[d],
 // inverse FFT, store. ROW_INV: input is a spectrum (natural k2): inverse FFT, store.
 // ROW_INV_MULCONJ: input is a spectrum: times conj kspec[d], inverse FFT, store.
-template <int MODE>
+template <int MODE, int LN>
 __global__ FFT_BOUNDS void row_kernel(cf* __restrict__ ws, const cf* __restrict__ kspec,
-                                      Pairing pr, Geo g, cf* __restrict__ zsave) {
+                                      Pairing pr, Geo g_, cf* __restrict__ zsave) {
+  const Geo g = fixed<LN>(g_);
   constexpr bool FWD = MODE == ROW_SPEC || MODE == ROW_MUL || MODE == ROW_MULCONJ;
   constexpr bool MUL = MODE == ROW_MUL || MODE == ROW_MULCONJ || MODE == ROW_INV_MULCONJ;
   constexpr bool CONJK = MODE == ROW_MULCONJ || MODE == ROW_INV_MULCONJ;
@@ -353,9 +368,10 @@ __global__ FFT_BOUNDS void row_kernel(cf* __restrict__ ws, const cf* __restrict_
 enum OutMode { OUT_PAIR = 0, OUT_REAL = 1 };
 // OUT_PAIR: rows ra/rb of y get Re/Im at i = n - off for i in [0, L).
 // OUT_REAL: row p (= channel) of outf gets Re * scale at i = n for i < L.
-template <typename T, int MODE>
-__global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr, Geo g, int off,
+template <typename T, int MODE, int LN>
+__global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr, Geo g_, int off,
                                           T* __restrict__ y, float* __restrict__ outf, float scale) {
+  const Geo g = fixed<LN>(g_);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M1 = 1 << g.logM1, M2 = 1 << g.logM2;
   const int lcw = log_col_group(g), cw = 1 << lcw;
@@ -536,28 +552,57 @@ inline void allow_lds(Kern k, size_t bytes) {
   if (bytes > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// instantiated sizes: N = 2^16 .. 2^18 (L = 32,768 .. 131,072: HyenaDNA's long configs, config D
+// at 2^17); every other size runs the generic kernels. DNA_FFT_GENERIC=1 forces those (A/B).
+inline int fixed_ln(const Geo& g) {
+  static const bool generic = getenv("DNA_FFT_GENERIC") && atoi(getenv("DNA_FFT_GENERIC")) == 1;
+  return (!generic && g.logN >= 16 && g.logN <= 18) ? g.logN : 0;
+}
+#define DNA_FFT_DISPATCH(LAUNCH)      \
+  switch (fixed_ln(g)) {              \
+    case 16: LAUNCH(16); break;       \
+    case 17: LAUNCH(17); break;       \
+    case 18: LAUNCH(18); break;       \
+    default: LAUNCH(0); break;        \
+  }
+
 template <typename T>
 int launch_col_fwd(const void* x, Pairing pr, const Geo& g, int off, cf* ws, int P, hipStream_t s) {
-  auto k = col_fwd_kernel<T>;
-  allow_lds(k, col_lds(g));
-  hipLaunchKernelGGL(k, col_grid(g, P), dim3(NTH), col_lds(g), s, (const T*)x, pr, g, off, ws);
+#define L_(LN)                                                                                    \
+  {                                                                                               \
+    auto k = col_fwd_kernel<T, LN>;                                                               \
+    allow_lds(k, col_lds(g));                                                                     \
+    hipLaunchKernelGGL(k, col_grid(g, P), dim3(NTH), col_lds(g), s, (const T*)x, pr, g, off, ws); \
+  }
+  DNA_FFT_DISPATCH(L_)
+#undef L_
   return DNA_OK;
 }
 
 template <int MODE>
 void launch_row(cf* ws, const cf* kspec, Pairing pr, const Geo& g, int P, hipStream_t s,
                 cf* zsave = nullptr) {
-  auto k = row_kernel<MODE>;
-  allow_lds(k, row_lds(g));
-  hipLaunchKernelGGL(k, row_grid(g, P), dim3(NTH), row_lds(g), s, ws, kspec, pr, g, zsave);
+#define L_(LN)                                                                                  \
+  {                                                                                             \
+    auto k = row_kernel<MODE, LN>;                                                              \
+    allow_lds(k, row_lds(g));                                                                   \
+    hipLaunchKernelGGL(k, row_grid(g, P), dim3(NTH), row_lds(g), s, ws, kspec, pr, g, zsave); \
+  }
+  DNA_FFT_DISPATCH(L_)
+#undef L_
 }
 
 template <typename T, int MODE>
 void launch_col_inv(const cf* ws, Pairing pr, const Geo& g, int off, void* y, float* outf, float scale,
                     int P, hipStream_t s) {
-  auto k = col_inv_kernel<T, MODE>;
-  allow_lds(k, col_lds(g));
-  hipLaunchKernelGGL(k, col_grid(g, P), dim3(NTH), col_lds(g), s, ws, pr, g, off, (T*)y, outf, scale);
+#define L_(LN)                                                                                                  \
+  {                                                                                                             \
+    auto k = col_inv_kernel<T, MODE, LN>;                                                                       \
+    allow_lds(k, col_lds(g));                                                                                   \
+    hipLaunchKernelGGL(k, col_grid(g, P), dim3(NTH), col_lds(g), s, ws, pr, g, off, (T*)y, outf, scale);        \
+  }
+  DNA_FFT_DISPATCH(L_)
+#undef L_
 }
 
 inline int pad_before(int L, int bidirectional) {
