@@ -16,6 +16,6 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d $OUT/col_fwd_$i -o run --output-format csv -- $CMD > $OUT/pmc$i.log 2>&1 || echo "pmc $i failed" >> $OUT/errors.txt
 done
-python $ROOT/scripts/pmc_table.py $OUT --kernel "col_fwd_kernel" > $OUT/pmc_colfwd.txt 2>&1 || true
-python $ROOT/scripts/pmc_table.py $OUT --kernel "row_kernel<1>" > $OUT/pmc_row.txt 2>&1 || true
-python $ROOT/scripts/pmc_table.py $OUT --kernel "col_inv_kernel<float, 0>" > $OUT/pmc_colinv.txt 2>&1 || true
+python $ROOT/scripts/pmc_table.py $OUT --kernel "col_fwd_kernel<float, 17>" > $OUT/pmc_colfwd.txt 2>&1 || true
+python $ROOT/scripts/pmc_table.py $OUT --kernel "row_kernel<1, 17>" > $OUT/pmc_row.txt 2>&1 || true
+python $ROOT/scripts/pmc_table.py $OUT --kernel "col_inv_kernel<float, 0, 17>" > $OUT/pmc_colinv.txt 2>&1 || true
