@@ -23,6 +23,7 @@ constexpr int TP = 64;   // positions per tile
 constexpr int TC = 32;   // channels per tile
 constexpr int CPW = TC / 4;  // channels per wave in the conv phases
 constexpr int PAD = 1;   // LDS row padding (floats)
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 
 template <typename T>
 __device__ __forceinline__ T cvt(float v) { return from_f32<T>(v); }
@@ -149,90 +150,117 @@ struct Bwd {
 // duc (d of the conv outputs) at positions [t0, t0 + TP + K - 1), then
 //   du[t, ch]  = sum_k w[ch][k] duc[t + K - 1 - k]
 //   dw[ch][k] += sum_{t in tile} duc[t] u[t - (K - 1 - k)],  dbias[ch] += sum_{t in tile} duc[t]
+// Work split (all 256 threads busy in every phase): the duc rows of a wave's 8 channels are one
+// flat (channel, row) range over the lanes, so the K - 1 halo rows do not cost a second full pass;
+// du is written as channel pairs (4-B bf16 / 8-B fp32 stores, 16 pairs x 4 rows per wave pass);
+// the dw / dbias tile sums are split into 4 row quarters per (group, channel) and combined in LDS
+// in a fixed order before the per-tile partial is written (deterministic).
 template <typename T, int K>
 __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   extern __shared__ float smem[];
   const int G = a.order + 1, C = G * a.d;
   const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
-  const int RU = TP + 2 * (K - 1);  // u rows: [t0 - (K-1), t0 + TP + K - 1)
-  const int RD = TP + K - 1;        // duc rows: [t0, t0 + TP + K - 1)
-  float* us = smem;                              // [G][RU][TC + PAD]
-  float* ds = smem + G * RU * (TC + PAD);        // [G][RD][TC + PAD]
+  constexpr int RU = TP + 2 * (K - 1);  // u rows: [t0 - (K-1), t0 + TP + K - 1)
+  constexpr int RD = TP + K - 1;        // duc rows: [t0, t0 + TP + K - 1)
+  constexpr int LW = TC + PAD;
+  float* us = smem;                  // [G][RU][LW]
+  float* ds = smem + G * RU * LW;    // [G][RD][LW]
+  float* red = ds + G * RD * LW;     // [4][G * TC][K + 1] row-quarter sums
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
   for (int g = 0; g < G; ++g)
-    load_tok_tile(us + g * RU * (TC + PAD), u, a.L, C, t0, K - 1, K - 1, g * a.d + c0);
+    load_tok_tile(us + g * RU * LW, u, a.L, C, t0, K - 1, K - 1, g * a.d + c0);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // duc for this tile's positions plus the K-1 after it (0 at t >= L: cropped conv outputs)
-  for (int j = wv * CPW; j < wv * CPW + CPW; ++j) {
-    const int c = c0 + j;
-    for (int rr = lane; rr < RD; rr += 64) {
-      const int t = t0 + rr;
-      float conv_last = 0.f, conv_v = 0.f;
-      if (t < a.L) {
-        // recompute the conv outputs of groups order-1 and order at t (u rows rr .. rr + K - 1)
-        for (int g = a.order - 1; g <= a.order; ++g) {
-          const int ch = g * a.d + c;
-          const float* tl = us + g * RU * (TC + PAD);
-          float acc = a.bias[ch];
+  for (int q = lane; q < CPW * RD; q += 64) {
+    const int jj = q / RD, rr = q - jj * RD;
+    const int j = wv * CPW + jj, c = c0 + j;
+    const int t = t0 + rr;
+    float conv_last = 0.f, conv_v = 0.f;
+    if (t < a.L) {
+      // recompute the conv outputs of groups order-1 and order at t (u rows rr .. rr + K - 1)
 #pragma unroll
-          for (int k = 0; k < K; ++k) acc = fmaf(a.w[ch * K + k], tl[(rr + k) * (TC + PAD) + j], acc);
-          if (g == a.order - 1) conv_last = acc; else conv_v = acc;
+      for (int e = 0; e < 2; ++e) {
+        const int g = a.order - 1 + e;
+        const int ch = g * a.d + c;
+        const float* tl = us + g * RU * LW;
+        float acc = a.bias[ch];
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = fmaf(a.w[ch * K + k], tl[(rr + k) * LW + j], acc);
+        if (e == 0) conv_last = acc; else conv_v = acc;
+      }
+    }
+    for (int g = 0; g < G; ++g) {
+      float v = 0.f;
+      if (t < a.L) {
+        if (g < a.order - 1) {
+          v = to_f32(((const T*)a.dxs)[((size_t)b * (a.order - 1) * a.d + g * a.d + c) * a.L + t]);
+        } else {
+          const float dvx = to_f32(((const T*)a.dvx)[((size_t)b * a.d + c) * a.L + t]);
+          v = g == a.order - 1 ? dvx * conv_v : dvx * conv_last;
         }
       }
-      for (int g = 0; g < G; ++g) {
-        float v = 0.f;
-        if (t < a.L) {
-          if (g < a.order - 1) {
-            v = to_f32(((const T*)a.dxs)[((size_t)b * (a.order - 1) * a.d + g * a.d + c) * a.L + t]);
-          } else {
-            const float dvx = to_f32(((const T*)a.dvx)[((size_t)b * a.d + c) * a.L + t]);
-            v = g == a.order - 1 ? dvx * conv_v : dvx * conv_last;
-          }
-        }
-        ds[(g * RD + rr) * (TC + PAD) + j] = v;
-      }
+      ds[(g * RD + rr) * LW + j] = v;
     }
   }
   __syncthreads();
-  // du (token-major): lane = (row parity, channel); 4 waves x 2 rows per pass
+  // du (token-major): lane = (row in 4, channel pair in 16); 4 waves x 4 rows per pass
   T* du = (T*)a.du + (size_t)b * a.L * C;
-  constexpr int RPW = 64 / TC;
-  const int cl = lane % TC, rsub = lane / TC;
+  const int cp = 2 * (lane & 15), rsub = lane >> 4;
   for (int g = 0; g < G; ++g) {
-    const int ch = g * a.d + c0 + cl;
-    float wk[K];
+    const int ch = g * a.d + c0 + cp;
+    float w0[K], w1[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) wk[k] = a.w[ch * K + k];
-    const float* dl = ds + g * RD * (TC + PAD);
-    for (int r = wv * RPW + rsub; r < TP; r += 4 * RPW) {
+    for (int k = 0; k < K; ++k) { w0[k] = a.w[ch * K + k]; w1[k] = a.w[(ch + 1) * K + k]; }
+    const float* dl = ds + g * RD * LW;
+    for (int r = wv * 4 + rsub; r < TP; r += 16) {
       const int t = t0 + r;
       if (t >= a.L) break;
-      float acc = 0.f;
+      float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc = fmaf(wk[k], dl[(r + K - 1 - k) * (TC + PAD) + cl], acc);
-      du[(size_t)t * C + ch] = cvt<T>(acc);
+      for (int k = 0; k < K; ++k) {
+        const float* src = dl + (r + K - 1 - k) * LW + cp;
+        a0 = fmaf(w0[k], src[0], a0);
+        a1 = fmaf(w1[k], src[1], a1);
+      }
+      T* o = du + (size_t)t * C + ch;
+      if constexpr (sizeof(T) == 2) {
+        const bf16x2 v = {cvt<T>(a0), cvt<T>(a1)};
+        *reinterpret_cast<bf16x2*>(o) = v;
+      } else {
+        *reinterpret_cast<float2*>(o) = make_float2(a0, a1);
+      }
     }
   }
-  // dw / dbias partials: a (group, channel) per thread; sum over the tile's TP positions
-  const int nL = gridDim.x;
-  float* prow = a.part + ((size_t)b * nL + blockIdx.x) * C * (K + 1);
-  for (int gc = threadIdx.x; gc < G * TC; gc += blockDim.x) {
+  // dw / dbias: (row quarter, group, channel) per thread, 16 rows each
+  const int items = 4 * G * TC;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int qr = it / (G * TC), gc = it - qr * (G * TC);
     const int g = gc / TC, j = gc - g * TC;
-    const int ch = g * a.d + c0 + j;
-    const float* dl = ds + g * RD * (TC + PAD);
-    const float* ul = us + g * RU * (TC + PAD);
+    const float* dl = ds + g * RD * LW;
+    const float* ul = us + g * RU * LW;
     float sw[K + 1];
 #pragma unroll
     for (int k = 0; k <= K; ++k) sw[k] = 0.f;
-    for (int r = 0; r < TP; ++r) {
-      const float dv = dl[r * (TC + PAD) + j];  // duc at t0 + r (0 past L)
+#pragma unroll 4
+    for (int r = 16 * qr; r < 16 * qr + 16; ++r) {
+      const float dv = dl[r * LW + j];  // duc at t0 + r (0 past L)
 #pragma unroll
-      for (int k = 0; k < K; ++k) sw[k] = fmaf(dv, ul[(r + k) * (TC + PAD) + j], sw[k]);  // u[t - (K-1-k)]
+      for (int k = 0; k < K; ++k) sw[k] = fmaf(dv, ul[(r + k) * LW + j], sw[k]);  // u[t - (K-1-k)]
       sw[K] += dv;
     }
 #pragma unroll
-    for (int k = 0; k <= K; ++k) prow[(size_t)ch * (K + 1) + k] = sw[k];
+    for (int k = 0; k <= K; ++k) red[(qr * G * TC + gc) * (K + 1) + k] = sw[k];
+  }
+  __syncthreads();
+  const int nL = gridDim.x;
+  float* prow = a.part + ((size_t)b * nL + blockIdx.x) * C * (K + 1);
+  for (int e = threadIdx.x; e < G * TC * (K + 1); e += blockDim.x) {
+    const int gc = e / (K + 1), k = e - gc * (K + 1);
+    const int g = gc / TC, j = gc - g * TC;
+    const float v = ((red[e] + red[G * TC * (K + 1) + e]) + red[2 * G * TC * (K + 1) + e]) +
+                    red[3 * G * TC * (K + 1) + e];
+    prow[(size_t)(g * a.d + c0 + j) * (K + 1) + k] = v;
   }
 }
 
@@ -296,7 +324,8 @@ extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w,
   DNA_CHECK_ARG(((uintptr_t)u & 15) == 0, "dna_hyena_shortconv_bwd: u must be 16-byte aligned");
   Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part};
   const dim3 grid((L + TP - 1) / TP, d / TC, B);
-  const size_t lds = (size_t)(order + 1) * ((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) * sizeof(float);
+  const size_t lds = (size_t)(order + 1) * (((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) + 4 * TC * (K + 1)) *
+                     sizeof(float);
   DNA_CHECK_ARG(lds <= 160 * 1024, "dna_hyena_shortconv_bwd: order %d needs %zu B of LDS", order, lds);
   hipStream_t s = as_stream(stream);
   dispatch_k(K, [&](auto kk) {
