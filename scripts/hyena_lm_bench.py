@@ -75,6 +75,20 @@ def main():
             kernels[k].update(bound="mfma", achieved_tflops=round(rate / 1e12, 1), frac=round(rate / 2.5e15, 4))
         else:
             kernels[k].update(bound="hbm", achieved_gbs=round(rate / 1e9, 1), frac=round(rate / 8e12, 4))
+    # FFT long conv: roofline = max(algorithmic bytes / HBM peak, FFT flops / fp32 VALU peak)
+    # (5 N log2 N per N-point complex transform; forward: the filter's D/2 channel pairs + a
+    # forward and an inverse transform per row pair; backward: dy forward + du inverse per pair,
+    # one inverse per channel for dk)
+    D, N = 256, 2 * a.L
+    lg, P = N.bit_length() - 1, (a.B + 1) // 2 * D
+    tr = {"fftconv_fwd": (D // 2 + 2 * P), "fftconv_bwd": (2 * P + D)}
+    for k, ntr in tr.items():
+        if k in summ:
+            n, t, u, kind = summ[k]
+            flop = ntr * 5 * N * lg
+            bound_ms = max(u / 8e12, flop / 157.3e12) * 1e3
+            kernels[k].update(flop_per_launch=flop, roofline_bound_ms=round(bound_ms, 4),
+                              roofline_frac=round(bound_ms / t, 4))
     dom = max(summ, key=lambda k: summ[k][0] * summ[k][1]) if summ else None
     roof = None
     if dom:
@@ -84,6 +98,9 @@ def main():
                 "achieved": kernels[dom].get("achieved_gbs", kernels[dom].get("achieved_tflops")),
                 "peak": 8000.0 if kind != "flop" else 2500.0,
                 "unit": "GB/s" if kind != "flop" else "TFLOP/s"}
+        if "roofline_frac" in kernels[dom]:
+            roof.update(fft_roofline_bound_ms=kernels[dom]["roofline_bound_ms"],
+                        fft_roofline_frac=kernels[dom]["roofline_frac"])
     import json
     print(json.dumps({"metric": "HyenaDNA-small MLM train step (BASELINE config D)", "value": round(a.B / dt, 3),
                       "unit": "sequences/s", "tokens_per_s": round(a.B * a.L / dt), "ms_per_step": round(dt * 1e3, 2),
