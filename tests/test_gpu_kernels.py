@@ -252,9 +252,12 @@ def test_geglu_row_unrolled_bf16(n):
     for dt, code in ((torch.bfloat16, 1), (torch.float32, 0)):
         a = torch.empty(n, F, device=DEV, dtype=dt)
         dg = torch.empty(n, 2 * F, device=DEV, dtype=dt)
-        N.call("dna_geglu_fwd", g.to(dt).data_ptr(), code, n, F, 0.1, 7, 3, a.data_ptr(),
-               N.stream_ptr())
-        N.call("dna_geglu_bwd", da.to(dt).data_ptr(), g.to(dt).data_ptr(), code, n, F, 0.1, 7, 3,
+        # converted inputs held in variables: a temporary passed as `.to(dt).data_ptr()` is freed
+        # before the kernel runs, and the next conversion may reuse its block (seen in the full
+        # suite: the fp32 reference read a dO overwritten by g's conversion)
+        gi, di = g.to(dt), da.to(dt)
+        N.call("dna_geglu_fwd", gi.data_ptr(), code, n, F, 0.1, 7, 3, a.data_ptr(), N.stream_ptr())
+        N.call("dna_geglu_bwd", di.data_ptr(), gi.data_ptr(), code, n, F, 0.1, 7, 3,
                dg.data_ptr(), N.stream_ptr())
         outs[code] = (a.float(), dg.float())
     (a1, dg1), (a0, dg0) = outs[1], outs[0]
