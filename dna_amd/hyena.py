@@ -307,6 +307,26 @@ class ExponentialModulation(_OptimModule):
         return x * (torch.exp(-t * self.deltas.abs()) + self.shift)
 
 
+def _split_k_linear(x, lin, rows_per_chunk=512):
+    """nn.Linear over the L positions of the implicit filter MLP ([1, L, K] -> [1, L, N], K and N
+    64-256). As one GEMM its weight gradient is a 64 x 64 (or 256 x 64) output reduced over all
+    L = 65,536 positions, which hipBLASLt ran as one or four workgroups (≈210 us per call, 12 % of
+    the config-D step). Written as a batched product against the weight expanded over L / 512
+    chunks, autograd computes that gradient as a batched GEMM over the chunks plus the expand's sum:
+    split-K with every CU busy. Same math; the forward is the same GEMM batched. Short or odd
+    lengths and CPU tensors keep the plain linear."""
+    L = x.shape[-2]
+    if not x.is_cuda or os.environ.get("DNA_HYENA_FILTER_SPLITK", "1") == "0" or L < 8 * rows_per_chunk \
+            or L % rows_per_chunk or x.dim() != 3 or x.shape[0] != 1:
+        return lin(x)
+    c = L // rows_per_chunk
+    K, N = lin.in_features, lin.out_features
+    y = torch.bmm(x.reshape(c, rows_per_chunk, K), lin.weight.t().unsqueeze(0).expand(c, K, N))
+    if lin.bias is not None:
+        y = y + lin.bias
+    return y.reshape(1, L, N)
+
+
 class HyenaFilter(_OptimModule):
     """Implicit long filter + the long convolution (hyena.py:166-280). `forward` runs the HIP
     FFT convolution (the reference's `fftconv_ref` path, fused_fft_conv=False)."""
@@ -342,7 +362,9 @@ class HyenaFilter(_OptimModule):
 
     def filter(self, L, *args, **kwargs):
         z, t = self.pos_emb(L)
-        h = self.implicit_filter(z)
+        h = z
+        for layer in self.implicit_filter:
+            h = _split_k_linear(h, layer) if isinstance(layer, nn.Linear) else layer(h)
         if self.modulate:
             h = self.modulation(t, h)
         if self.normalized:

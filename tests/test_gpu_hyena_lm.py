@@ -172,3 +172,21 @@ def test_config_d_full_step_65536_bf16_trains():
     assert all(torch.isfinite(torch.tensor(losses)))
     assert torch.isfinite(tr.flat.flat).all()
     assert losses[-1] < losses[0], losses
+
+
+def test_implicit_filter_split_k_linear_matches_linear():
+    """The implicit filter MLP's split-K linear (batched product over 512-position chunks) == one
+    nn.Linear: output and every gradient, fp32 at L = 65,536."""
+    from dna_amd.hyena import _split_k_linear
+    torch.manual_seed(0)
+    for k_in, n_out, bias in ((5, 64, True), (64, 64, True), (64, 256, False)):
+        lin = torch.nn.Linear(k_in, n_out, bias=bias).cuda()
+        x = torch.randn(1, 65536, k_in, device="cuda", requires_grad=True)
+        dy = torch.randn(1, 65536, n_out, device="cuda")
+        y0 = lin(x)
+        g0 = torch.autograd.grad(y0, [x, lin.weight] + ([lin.bias] if bias else []), dy)
+        y1 = _split_k_linear(x, lin)
+        g1 = torch.autograd.grad(y1, [x, lin.weight] + ([lin.bias] if bias else []), dy)
+        assert (y1 - y0).abs().max().item() <= 1e-5 * y0.abs().max().item() + 1e-6
+        for a, b in zip(g1, g0):
+            assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item()
