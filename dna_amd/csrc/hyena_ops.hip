@@ -28,28 +28,43 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 template <typename T>
 __device__ __forceinline__ T cvt(float v) { return from_f32<T>(v); }
 
-// Load rows [t0 - lo, t0 + TP + hi) x channels [col0, col0 + TC) of a token-major [L, ldc] matrix
-// into lds[row][TC + PAD] (zero outside [0, L)), 16-byte vectors along the channels.
-template <typename T>
-__device__ __forceinline__ void load_tok_tile(float* lds, const T* src, int L, int ldc, int t0,
-                                              int lo, int hi, int col0) {
+// Load rows [t0 - LO, t0 + TP + HI) x channels [g*d + col0, + TC) of the G channel groups of a
+// token-major [L, ldc] matrix into lds[g][row][TC + PAD] (zero outside [0, L)), 16-byte vectors
+// along the channels. Every load of a thread (all groups) is issued before the first LDS store:
+// these kernels are memory-latency bound (PMC: 78-92 % of wave cycles in s_waitcnt), and a
+// load -> convert -> store loop kept one 16-B load per thread in flight.
+constexpr int GMAX = 5;  // order + 1 <= 5
+template <typename T, int LO, int HI>
+__device__ __forceinline__ void load_tok_tiles(float* lds, const T* src, int L, int ldc, int t0,
+                                               int G, int d, int col0) {
   constexpr int VE = 16 / sizeof(T);      // elements per vector
   constexpr int VPR = TC / VE;            // vectors per row
-  const int rows = TP + lo + hi;
-  for (int i = threadIdx.x; i < rows * VPR; i += blockDim.x) {
-    const int r = i / VPR, cv = (i - r * VPR) * VE;
-    const int t = t0 - lo + r;
-    float* dst = lds + r * (TC + PAD) + cv;
-    if (t >= 0 && t < L) {
-      const uint4 raw = *reinterpret_cast<const uint4*>(src + (size_t)t * ldc + col0 + cv);
-      const T* e = reinterpret_cast<const T*>(&raw);
+  constexpr int ROWS = TP + LO + HI;
+  constexpr int NIT = (ROWS * VPR + 255) / 256;  // per group and thread (256-thread blocks)
+  uint4 raw[GMAX][NIT];
+#pragma unroll
+  for (int g = 0; g < GMAX; ++g)
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = threadIdx.x + it * 256;
+      const int r = i / VPR, cv = (i - r * VPR) * VE;
+      const int t = t0 - LO + r;
+      raw[g][it] = make_uint4(0u, 0u, 0u, 0u);
+      if (g < G && i < ROWS * VPR && t >= 0 && t < L)
+        raw[g][it] = *reinterpret_cast<const uint4*>(src + (size_t)t * ldc + g * d + col0 + cv);
+    }
+#pragma unroll
+  for (int g = 0; g < GMAX; ++g)
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = threadIdx.x + it * 256;
+      if (g >= G || i >= ROWS * VPR) continue;
+      const int r = i / VPR, cv = (i - r * VPR) * VE;
+      float* dst = lds + (g * ROWS + r) * (TC + PAD) + cv;
+      const T* e = reinterpret_cast<const T*>(&raw[g][it]);
 #pragma unroll
       for (int q = 0; q < VE; ++q) dst[q] = to_f32(e[q]);
-    } else {
-#pragma unroll
-      for (int q = 0; q < VE; ++q) dst[q] = 0.f;
     }
-  }
 }
 
 struct Fwd {
@@ -64,8 +79,7 @@ __global__ __launch_bounds__(256) void shortconv_fwd_kernel(Fwd a) {
   const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
   const int R = TP + K - 1;  // rows incl. halo
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
-  for (int g = 0; g < G; ++g)
-    load_tok_tile(smem + g * R * (TC + PAD), u, a.L, C, t0, K - 1, 0, g * a.d + c0);
+  load_tok_tiles<T, K - 1, 0>(smem, u, a.L, C, t0, G, a.d, c0);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int t = t0 + lane;
@@ -97,14 +111,19 @@ __global__ __launch_bounds__(256) void gate_out_fwd_kernel(const T* yc, const T*
   __shared__ float tile[TC][TP + PAD];
   const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int j = wv; j < TC; j += 4) {
+  {  // the 8 channel rows of this wave: all 16 loads issued before the products
+    constexpr int NJ = TC / 4;
+    T ly[NJ], lx[NJ];
     const int t = t0 + lane;
-    float v = 0.f;
-    if (t < L) {
+#pragma unroll
+    for (int n = 0; n < NJ; ++n) {
+      const int j = wv + 4 * n;
       const size_t o = ((size_t)b * d + c0 + j) * L + t;
-      v = to_f32(yc[o]) * to_f32(x0[(size_t)b * x0_bstride + (size_t)(c0 + j) * L + t]);
+      ly[n] = t < L ? yc[o] : T(0.f);
+      lx[n] = t < L ? x0[(size_t)b * x0_bstride + (size_t)(c0 + j) * L + t] : T(0.f);
     }
-    tile[j][lane] = v;
+#pragma unroll
+    for (int n = 0; n < NJ; ++n) tile[wv + 4 * n][lane] = to_f32(ly[n]) * to_f32(lx[n]);
   }
   __syncthreads();
   // token-major rows of TC channels: a wave covers 64 / TC rows per pass
@@ -131,14 +150,29 @@ __global__ __launch_bounds__(256) void gate_out_bwd_kernel(const T* dy, const T*
     tile[r][cl] = t < L ? to_f32(dy[((size_t)b * L + t) * d + c0 + cl]) : 0.f;
   }
   __syncthreads();
-  for (int j = wv; j < TC; j += 4) {
+  {  // the 8 channel rows of this wave: all 16 loads issued before the products and stores
+    constexpr int NJ = TC / 4;
+    T lx[NJ], ly[NJ];
     const int t = t0 + lane;
-    if (t >= L) continue;
-    const float g = tile[lane][j];
-    const size_t o = ((size_t)b * d + c0 + j) * L + t;
-    const size_t ox = (size_t)b * x_bstride + (size_t)(c0 + j) * L + t;
-    dyc[o] = cvt<T>(g * to_f32(x0[ox]));
-    dx0[ox] = cvt<T>(g * to_f32(yc[o]));
+#pragma unroll
+    for (int n = 0; n < NJ; ++n) {
+      const int j = wv + 4 * n;
+      const size_t o = ((size_t)b * d + c0 + j) * L + t;
+      const size_t ox = (size_t)b * x_bstride + (size_t)(c0 + j) * L + t;
+      lx[n] = t < L ? x0[ox] : T(0.f);
+      ly[n] = t < L ? yc[o] : T(0.f);
+    }
+    if (t < L) {
+#pragma unroll
+      for (int n = 0; n < NJ; ++n) {
+        const int j = wv + 4 * n;
+        const float g = tile[lane][j];
+        const size_t o = ((size_t)b * d + c0 + j) * L + t;
+        const size_t ox = (size_t)b * x_bstride + (size_t)(c0 + j) * L + t;
+        dyc[o] = cvt<T>(g * to_f32(lx[n]));
+        dx0[ox] = cvt<T>(g * to_f32(ly[n]));
+      }
+    }
   }
 }
 
@@ -167,12 +201,30 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   float* ds = smem + G * RU * LW;    // [G][RD][LW]
   float* red = ds + G * RD * LW;     // [4][G * TC][K + 1] row-quarter sums
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
-  for (int g = 0; g < G; ++g)
-    load_tok_tile(us + g * RU * LW, u, a.L, C, t0, K - 1, K - 1, g * a.d + c0);
+  load_tok_tiles<T, K - 1, K - 1>(us, u, a.L, C, t0, G, a.d, c0);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // duc for this tile's positions plus the K-1 after it (0 at t >= L: cropped conv outputs)
-  for (int q = lane; q < CPW * RD; q += 64) {
+  // duc for this tile's positions plus the K-1 after it (0 at t >= L: cropped conv outputs).
+  // All the lane's d(x_g) / d(v x) loads (NQ (channel, row) items, order <= 4) are issued first.
+  constexpr int NQ = (CPW * RD + 63) / 64;
+  T lx[NQ][GMAX - 2], lv[NQ];
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) {
+    const int q = lane + 64 * n;
+    const int jj = q / RD, rr = q - jj * RD;
+    const int c = c0 + wv * CPW + jj, t = t0 + rr;
+    const bool ok = q < CPW * RD && t < a.L;
+    lv[n] = ok ? ((const T*)a.dvx)[((size_t)b * a.d + c) * a.L + t] : T(0.f);
+#pragma unroll
+    for (int g = 0; g < GMAX - 2; ++g)
+      lx[n][g] = (ok && g < a.order - 1)
+                     ? ((const T*)a.dxs)[((size_t)b * (a.order - 1) * a.d + g * a.d + c) * a.L + t]
+                     : T(0.f);
+  }
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) {
+    const int q = lane + 64 * n;
+    if (q >= CPW * RD) break;
     const int jj = q / RD, rr = q - jj * RD;
     const int j = wv * CPW + jj, c = c0 + j;
     const int t = t0 + rr;
@@ -190,16 +242,11 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
         if (e == 0) conv_last = acc; else conv_v = acc;
       }
     }
+    const float dvx = to_f32(lv[n]);
     for (int g = 0; g < G; ++g) {
-      float v = 0.f;
-      if (t < a.L) {
-        if (g < a.order - 1) {
-          v = to_f32(((const T*)a.dxs)[((size_t)b * (a.order - 1) * a.d + g * a.d + c) * a.L + t]);
-        } else {
-          const float dvx = to_f32(((const T*)a.dvx)[((size_t)b * a.d + c) * a.L + t]);
-          v = g == a.order - 1 ? dvx * conv_v : dvx * conv_last;
-        }
-      }
+      float v;
+      if (g < a.order - 1) v = to_f32(lx[n][g < GMAX - 2 ? g : 0]);
+      else v = g == a.order - 1 ? dvx * conv_v : dvx * conv_last;
       ds[(g * RD + rr) * LW + j] = v;
     }
   }
