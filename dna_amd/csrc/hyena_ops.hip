@@ -33,32 +33,31 @@ __device__ __forceinline__ T cvt(float v) { return from_f32<T>(v); }
 // along the channels. Every load of a thread (all groups) is issued before the first LDS store:
 // these kernels are memory-latency bound (PMC: 78-92 % of wave cycles in s_waitcnt), and a
 // load -> convert -> store loop kept one 16-B load per thread in flight.
-constexpr int GMAX = 5;  // order + 1 <= 5
-template <typename T, int LO, int HI>
+template <typename T, int LO, int HI, int G>
 __device__ __forceinline__ void load_tok_tiles(float* lds, const T* src, int L, int ldc, int t0,
-                                               int G, int d, int col0) {
+                                               int d, int col0) {
   constexpr int VE = 16 / sizeof(T);      // elements per vector
   constexpr int VPR = TC / VE;            // vectors per row
   constexpr int ROWS = TP + LO + HI;
   constexpr int NIT = (ROWS * VPR + 255) / 256;  // per group and thread (256-thread blocks)
-  uint4 raw[GMAX][NIT];
+  uint4 raw[G][NIT];
 #pragma unroll
-  for (int g = 0; g < GMAX; ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int i = threadIdx.x + it * 256;
       const int r = i / VPR, cv = (i - r * VPR) * VE;
       const int t = t0 - LO + r;
       raw[g][it] = make_uint4(0u, 0u, 0u, 0u);
-      if (g < G && i < ROWS * VPR && t >= 0 && t < L)
+      if (i < ROWS * VPR && t >= 0 && t < L)
         raw[g][it] = *reinterpret_cast<const uint4*>(src + (size_t)t * ldc + g * d + col0 + cv);
     }
 #pragma unroll
-  for (int g = 0; g < GMAX; ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int i = threadIdx.x + it * 256;
-      if (g >= G || i >= ROWS * VPR) continue;
+      if (i >= ROWS * VPR) continue;
       const int r = i / VPR, cv = (i - r * VPR) * VE;
       float* dst = lds + (g * ROWS + r) * (TC + PAD) + cv;
       const T* e = reinterpret_cast<const T*>(&raw[g][it]);
@@ -72,14 +71,15 @@ struct Fwd {
   void* xs; void* vx;
 };
 
-template <typename T, int K>
+template <typename T, int K, int ORD>
 __global__ __launch_bounds__(256) void shortconv_fwd_kernel(Fwd a) {
   extern __shared__ float smem[];
-  const int G = a.order + 1, C = G * a.d;
+  constexpr int G = ORD + 1;  // channel groups x_0 .. x_{order-1}, v (compile-time: exact unrolls)
+  const int C = G * a.d;
   const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
   const int R = TP + K - 1;  // rows incl. halo
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
-  load_tok_tiles<T, K - 1, 0>(smem, u, a.L, C, t0, G, a.d, c0);
+  load_tok_tiles<T, K - 1, 0, G>(smem, u, a.L, C, t0, a.d, c0);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int t = t0 + lane;
@@ -93,9 +93,9 @@ __global__ __launch_bounds__(256) void shortconv_fwd_kernel(Fwd a) {
 #pragma unroll
       for (int k = 0; k < K; ++k) acc = fmaf(a.w[ch * K + k], tl[(lane + k) * (TC + PAD) + j], acc);
       if (t < a.L) {
-        if (g < a.order - 1)
-          ((T*)a.xs)[((size_t)b * (a.order - 1) * a.d + g * a.d + c) * a.L + t] = cvt<T>(acc);
-        else if (g == a.order - 1)
+        if (g < ORD - 1)
+          ((T*)a.xs)[((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t] = cvt<T>(acc);
+        else if (g == ORD - 1)
           last = acc;
         else
           ((T*)a.vx)[((size_t)b * a.d + c) * a.L + t] = cvt<T>(acc * last);
@@ -189,10 +189,11 @@ struct Bwd {
 // du is written as channel pairs (4-B bf16 / 8-B fp32 stores, 16 pairs x 4 rows per wave pass);
 // the dw / dbias tile sums are split into 4 row quarters per (group, channel) and combined in LDS
 // in a fixed order before the per-tile partial is written (deterministic).
-template <typename T, int K>
+template <typename T, int K, int ORD>
 __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   extern __shared__ float smem[];
-  const int G = a.order + 1, C = G * a.d;
+  constexpr int G = ORD + 1;
+  const int C = G * a.d;
   const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
   constexpr int RU = TP + 2 * (K - 1);  // u rows: [t0 - (K-1), t0 + TP + K - 1)
   constexpr int RD = TP + K - 1;        // duc rows: [t0, t0 + TP + K - 1)
@@ -201,13 +202,13 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   float* ds = smem + G * RU * LW;    // [G][RD][LW]
   float* red = ds + G * RD * LW;     // [4][G * TC][K + 1] row-quarter sums
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
-  load_tok_tiles<T, K - 1, K - 1>(us, u, a.L, C, t0, G, a.d, c0);
+  load_tok_tiles<T, K - 1, K - 1, G>(us, u, a.L, C, t0, a.d, c0);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // duc for this tile's positions plus the K-1 after it (0 at t >= L: cropped conv outputs).
   // All the lane's d(x_g) / d(v x) loads (NQ (channel, row) items, order <= 4) are issued first.
   constexpr int NQ = (CPW * RD + 63) / 64;
-  T lx[NQ][GMAX - 2], lv[NQ];
+  T lx[NQ][ORD - 1 > 0 ? ORD - 1 : 1], lv[NQ];
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
     const int q = lane + 64 * n;
@@ -216,10 +217,8 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
     const bool ok = q < CPW * RD && t < a.L;
     lv[n] = ok ? ((const T*)a.dvx)[((size_t)b * a.d + c) * a.L + t] : T(0.f);
 #pragma unroll
-    for (int g = 0; g < GMAX - 2; ++g)
-      lx[n][g] = (ok && g < a.order - 1)
-                     ? ((const T*)a.dxs)[((size_t)b * (a.order - 1) * a.d + g * a.d + c) * a.L + t]
-                     : T(0.f);
+    for (int g = 0; g < ORD - 1; ++g)
+      lx[n][g] = ok ? ((const T*)a.dxs)[((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t] : T(0.f);
   }
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
@@ -233,7 +232,7 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
       // recompute the conv outputs of groups order-1 and order at t (u rows rr .. rr + K - 1)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const int g = a.order - 1 + e;
+        const int g = ORD - 1 + e;
         const int ch = g * a.d + c;
         const float* tl = us + g * RU * LW;
         float acc = a.bias[ch];
@@ -245,8 +244,8 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
     const float dvx = to_f32(lv[n]);
     for (int g = 0; g < G; ++g) {
       float v;
-      if (g < a.order - 1) v = to_f32(lx[n][g < GMAX - 2 ? g : 0]);
-      else v = g == a.order - 1 ? dvx * conv_v : dvx * conv_last;
+      if (g < ORD - 1) v = to_f32(lx[n][g < ORD - 1 ? g : 0]);
+      else v = g == ORD - 1 ? dvx * conv_v : dvx * conv_last;
       ds[(g * RD + rr) * LW + j] = v;
     }
   }
@@ -320,6 +319,17 @@ int dispatch_k(int K, F&& f) {
     default: return -1;
   }
 }
+// (K, order) -> f(K, ORD) for K in 2..4, order in 2..4 (hy_check validated both)
+template <typename F>
+int dispatch_k_ord(int K, int order, F&& f) {
+  return dispatch_k(K, [&](auto kk) {
+    switch (order) {
+      case 2: f(kk, std::integral_constant<int, 2>()); break;
+      case 3: f(kk, std::integral_constant<int, 3>()); break;
+      default: f(kk, std::integral_constant<int, 4>()); break;
+    }
+  });
+}
 
 }  // namespace hyop
 }  // namespace dna
@@ -346,12 +356,12 @@ extern "C" int dna_hyena_shortconv_fwd(const void* u, int dtype, const float* w,
   const dim3 grid((L + TP - 1) / TP, d / TC, B);
   const size_t lds = (size_t)(order + 1) * (TP + K - 1) * (TC + PAD) * sizeof(float);
   hipStream_t s = as_stream(stream);
-  dispatch_k(K, [&](auto kk) {
-    constexpr int KK = decltype(kk)::value;
+  dispatch_k_ord(K, order, [&](auto kk, auto oo) {
+    constexpr int KK = decltype(kk)::value, OO = decltype(oo)::value;
     if (dtype == DNA_F32)
-      hipLaunchKernelGGL((shortconv_fwd_kernel<float, KK>), grid, dim3(256), lds, s, a);
+      hipLaunchKernelGGL((shortconv_fwd_kernel<float, KK, OO>), grid, dim3(256), lds, s, a);
     else
-      hipLaunchKernelGGL((shortconv_fwd_kernel<bf16, KK>), grid, dim3(256), lds, s, a);
+      hipLaunchKernelGGL((shortconv_fwd_kernel<bf16, KK, OO>), grid, dim3(256), lds, s, a);
   });
   DNA_LAUNCH_CHECK("dna_hyena_shortconv_fwd");
   return DNA_OK;
@@ -375,14 +385,14 @@ extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w,
                      sizeof(float);
   DNA_CHECK_ARG(lds <= 160 * 1024, "dna_hyena_shortconv_bwd: order %d needs %zu B of LDS", order, lds);
   hipStream_t s = as_stream(stream);
-  dispatch_k(K, [&](auto kk) {
-    constexpr int KK = decltype(kk)::value;
+  dispatch_k_ord(K, order, [&](auto kk, auto oo) {
+    constexpr int KK = decltype(kk)::value, OO = decltype(oo)::value;
     if (dtype == DNA_F32) {
-      auto k = shortconv_bwd_kernel<float, KK>;
+      auto k = shortconv_bwd_kernel<float, KK, OO>;
       if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
     } else {
-      auto k = shortconv_bwd_kernel<bf16, KK>;
+      auto k = shortconv_bwd_kernel<bf16, KK, OO>;
       if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
     }
