@@ -102,8 +102,12 @@ template <int R, bool INV> __device__ __forceinline__ void dft(cf* x) {
 // (Govindaraju et al. 2008): natural order in and out, in place (each pass reads its 16
 // points into registers, barrier, writes them, barrier). Twiddles from the LDS table
 // twM[m] = W_M^m (m < M). Unscaled; INV conjugates all twiddles.
-constexpr int NTH = 512;
-constexpr int PTS = 8192;
+#ifndef FFT_LOG_PTS
+#define FFT_LOG_PTS 13
+#endif
+constexpr int LOG_PTS = FFT_LOG_PTS;  // points per block: 8192 (512 threads) or 4096 (256)
+constexpr int PTS = 1 << LOG_PTS;
+constexpr int NTH = PTS / 16;
 constexpr int PPT = PTS / NTH;  // points per thread per pass
 // 8 waves per block, 2 blocks per CU (LDS ~78 KB each): 4 waves per SIMD, <= 128 VGPRs.
 #define FFT_BOUNDS __launch_bounds__(NTH, 4)  // HIP: 2nd argument = min waves per SIMD
@@ -232,10 +236,10 @@ __device__ __forceinline__ Geo fixed(Geo g) {
 // Column passes: G = PTS / M1 columns per block (16 at M1 = 512), column stride M1 + 1 (the
 // transposing global<->LDS copies then spread over the banks). Row pass: G = PTS / M2 rows.
 __host__ __device__ __forceinline__ int log_col_group(const Geo& g) {
-  return (13 - g.logM1) < g.logM2 ? (13 - g.logM1) : g.logM2;  // log2(min(PTS/M1, M2)), PTS = 2^13
+  return (LOG_PTS - g.logM1) < g.logM2 ? (LOG_PTS - g.logM1) : g.logM2;  // log2(min(PTS/M1, M2))
 }
 __host__ __device__ __forceinline__ int log_row_group(const Geo& g) {
-  return (13 - g.logM2) < g.logM1 ? (13 - g.logM2) : g.logM1;      // log2(min(PTS/M2, M1))
+  return (LOG_PTS - g.logM2) < g.logM1 ? (LOG_PTS - g.logM2) : g.logM1;      // log2(min(PTS/M2, M1))
 }
 
 // ---------------------------------------------------------------- A: column FFT over n1
@@ -549,7 +553,7 @@ inline dim3 row_grid(const Geo& g, int P) { return dim3(1 << (g.logM1 - log_row_
 
 template <typename Kern>
 inline void allow_lds(Kern k, size_t bytes) {
-  if (bytes > 65536) hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (bytes > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 // instantiated sizes: N = 2^16 .. 2^18 (L = 32,768 .. 131,072: HyenaDNA's long configs, config D
