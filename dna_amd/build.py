@@ -73,6 +73,13 @@ def build(verbose=False, jobs=None):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        # a kernel template whose host-side instantiation failed silently leaves its launch stub
+        # undefined (hipcc emits no diagnostic for it); the library would then fail at dlopen
+        r = subprocess.run(["nm", "-D", "--undefined-only", LIB], capture_output=True, text=True)
+        missing = [l.split()[-1] for l in r.stdout.splitlines() if "_ZN3dna" in l]
+        if missing:
+            os.remove(LIB)
+            raise RuntimeError(f"libdna_amd.so has undefined own symbols: {missing}")
     if verbose:
         print(f"built {LIB}")
     return LIB

@@ -556,7 +556,34 @@ __device__ __forceinline__ void unit_tile(const Args& a, int u, int& m0, int& n0
 // ABL (diagnostic ablations of the main loop, DNA_GEMM_ABL; results are garbage, timing only):
 // 1 = no LDS-DMA staging, 2 = no LDS reads (MFMAs on stale fragments), 4 = no barriers,
 // 8 = no B staging and no B reads, 16 = no B reads, 32 = no B staging
-template <int EPI, int ABL = 0>
+// SCH == 1 schedules: 16-B stores (per lane) issued after the stage of phase P-5 and before the
+// wait of phase P, for a K-step of role r (see gemmp_kernel) and phase p. The previous unit's
+// last K-step is phases -4..-1, the current unit's starts at lb. EPI_F32 = the weight-gradient
+// kernel (8 fp32 stores per quadrant), EPI_BF16 4 per quadrant, EPI_GEGLU 12 after phases 1, 3.
+template <int EPI>
+__host__ __device__ constexpr int pend_stores(int r, int p) {
+  const int P = r == 1 ? p : r == 3 ? 400 + p : 4 + p;
+  const int lb = r == 3 ? 400 : r == 4 ? 4 : 1 << 20;
+  int n = 0;
+  for (int q = 0; q < 4; ++q) {
+    const int st = EPI == EPI_F32 ? 8 : EPI == EPI_BF16 ? 4 : ((q & 1) ? 12 : 0);
+    const int sp = q - 4, sc = lb + q;
+    if (sp >= P - 5 && sp <= P - 1) n += st;
+    if (sc >= P - 5 && sc <= P - 1) n += st;
+  }
+  return n;
+}
+static_assert(pend_stores<EPI_BF16>(1, 0) == 16 && pend_stores<EPI_BF16>(1, 3) == 8 &&
+              pend_stores<EPI_BF16>(2, 0) == 4 && pend_stores<EPI_BF16>(2, 1) == 0 &&
+              pend_stores<EPI_BF16>(3, 0) == 0 && pend_stores<EPI_BF16>(3, 3) == 12 &&
+              pend_stores<EPI_BF16>(4, 0) == 4 && pend_stores<EPI_BF16>(4, 1) == 4 &&
+              pend_stores<EPI_GEGLU>(1, 3) == 12 && pend_stores<EPI_GEGLU>(4, 2) == 12,
+              "SCH 1 store counts");
+
+// SCH selects the half-tile schedule: 0 = the original 4-phase order (reads 12/4/8/0 per phase),
+// 1 = balanced reads (8/4/8/4: B_0 of the next K-step is read in phase 3) with 5 half-tiles in
+// flight -- see the comment above the SCH == 1 branch
+template <int EPI, int ABL = 0, int SCH = 0>
 __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU, "persistent kernel: bf16 / GeGLU epilogues");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
@@ -771,10 +798,13 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     }
   };
 
+  constexpr int QS = 4;  // 16-B stores per quadrant and lane (BF16)
+  constexpr int GS = 12;  // GeGLU: 16-B stores per half (g1, g2, a x 4 row blocks)
   Cur c0 = cur_at(0), c1 = c0, c2 = c0;
   advance(c1);
   advance(c2);
   advance(c2);
+  if constexpr (SCH == 0) {
   // prologue: all four halves of step 0, the A_0 / B_0 halves of step 1
   stage(c0, 0, 0);
   stage(c0, 0, 2);
@@ -793,8 +823,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   //           so phase p's wait also leaves the p * QS stores issued since phase 0 in flight
   //   role 2  a unit's first step after an epilogue: the stores issued behind the half-tiles it
   //           waits for stay in flight -- BF16 (4 - p) * QS, GeGLU (epilogue after the last step) S
-  constexpr int QS = 4;  // 16-B stores per quadrant and lane (BF16)
-  constexpr int GS = 12;  // GeGLU: 16-B stores per half (g1, g2, a x 4 row blocks)
   auto wait_vm = [&](auto phase, int role) {
     constexpr int p = decltype(phase)::value;
     // GeGLU: half 0 stored after phase 1's MFMAs, half 1 after phase 3's
@@ -873,6 +901,285 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     }
     c0 = cur_at(i + 1);
   }
+  } else if constexpr (SCH == 1) {
+    // SCH == 1. Per K-step v (quadrant order (0,0) (0,1) (1,1) (1,0)):
+    //   phase  reads        stages         MFMAs with
+    //   0      A_0(v)       S(v+1, A_1)    A_0, B_0(v) (read in phase 3 of step v-1)
+    //   1      B_1(v)       S(v+2, B_0)    A_0, B_1
+    //   2      A_1(v)       S(v+2, A_0)    A_1, B_1
+    //   3      B_0(v+1)     S(v+2, B_1)    A_1, B_0(v)
+    // Every phase reads at most 8 fragments per wave (the SCH 0 order reads 12 in phase 0, whose
+    // LDS time plus the DMA writes then outlasts the partner wave's 16-MFMA cluster). The two B
+    // register sets swap roles every K-step. WAR: every half is restaged 2 phases after its last
+    // read (the other wave group's reads of the phase before may still be in flight). RAW: a
+    // half read in phase P was staged in phase P-6 or earlier and is retired by the wait of phase
+    // P-1 (then a barrier), which leaves the 5 youngest half-tiles (10 LDS-DMA pieces per lane) in
+    // flight plus every epilogue store issued after the retiring stage -- the stores of a unit's
+    // last K-step sit in the same in-order VMEM count.
+    constexpr int hA0 = 0, hA1 = 1, hB0 = 2, hB1 = 3;
+    // step roles: 0 = no store pending in any wait window, 1 = a unit's first K-step after an
+    // epilogue, 2 = its second, 3 = a unit's last K-step (KT > 2, or the block's first unit),
+    // 4 = second and last at once (KT == 2 after an epilogue). pend_stores<EPI>(role, p) is the
+    // number of 16-B stores issued after the stage of phase P-5 and before the wait of phase P.
+    auto wait_p = [&](auto phase, int role) {
+      constexpr int p = decltype(phase)::value;
+      if (role == 0) __builtin_amdgcn_s_waitcnt(waitcnt_imm(10));
+      else if (role == 1) __builtin_amdgcn_s_waitcnt(waitcnt_imm(10 + pend_stores<EPI>(1, p)));
+      else if (role == 2) __builtin_amdgcn_s_waitcnt(waitcnt_imm(10 + pend_stores<EPI>(2, p)));
+      else if (role == 3) __builtin_amdgcn_s_waitcnt(waitcnt_imm(10 + pend_stores<EPI>(3, p)));
+      else __builtin_amdgcn_s_waitcnt(waitcnt_imm(10 + pend_stores<EPI>(4, p)));
+    };
+    auto lgkm0 = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto step = [&](int v, int kt, bool prev, bf16x8 (&bB0)[2][2], bf16x8 (&bB1)[2][2]) {
+      const bool last = kt == KT - 1;
+      const int role = __builtin_amdgcn_readfirstlane(
+          last ? (prev && kt == 1 ? 4 : 3) : prev && kt == 0 ? 1 : prev && kt == 1 ? 2 : 0);
+      const bool st = EPI == EPI_BF16 && last;
+      const bool sg = EPI == EPI_GEGLU && last;
+      // phase 0: quadrant (0,0)
+      stage(c1, v + 1, hA1);
+      wait_p(std::integral_constant<int, 0>{}, role);
+      readA(v, 0);
+      DNA_BARRIER();
+      lgkm0();
+      mma(0, 0, bB0);
+      if (st) store_quadrant(c0, 0, 0);
+      DNA_BARRIER();
+      // phase 1: quadrant (0,1)
+      stage(c2, v + 2, hB0);
+      wait_p(std::integral_constant<int, 1>{}, role);
+      readB(v, 1, bB1);
+      DNA_BARRIER();
+      lgkm0();
+      mma(0, 1, bB1);
+      if (st) store_quadrant(c0, 0, 1);
+      if (sg) store_geglu_half(c0, 0);
+      DNA_BARRIER();
+      // phase 2: quadrant (1,1)
+      stage(c2, v + 2, hA0);
+      wait_p(std::integral_constant<int, 2>{}, role);
+      readA(v, 1);
+      DNA_BARRIER();
+      lgkm0();
+      mma(1, 1, bB1);
+      if (st) store_quadrant(c0, 1, 1);
+      DNA_BARRIER();
+      // phase 3: quadrant (1,0); B_0 of the next K-step into the set B_1 just left
+      stage(c2, v + 2, hB1);
+      wait_p(std::integral_constant<int, 3>{}, role);
+      readB(v + 1, 0, bB1);
+      DNA_BARRIER();
+      lgkm0();
+      mma(1, 0, bB0);
+      if (st) store_quadrant(c0, 1, 0);
+      if (sg) store_geglu_half(c0, 1);
+      DNA_BARRIER();
+    };
+    // prologue = the stages of the virtual steps -2 and -1: S(0,B0) S(0,A0) S(0,B1) S(0,A1)
+    // S(1,B0) S(1,A0) S(1,B1); the wait retires the two oldest, then B_0(0) is read ("phase 3
+    // of step -1")
+    stage(c0, 0, hB0);
+    stage(c0, 0, hA0);
+    stage(c0, 0, hB1);
+    stage(c0, 0, hA1);
+    stage(c1, 1, hB0);
+    stage(c1, 1, hA0);
+    stage(c1, 1, hB1);
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(10));
+    DNA_BARRIER();
+    readB(0, 0, bf0);
+    if (wr == 1) DNA_BARRIER();  // stagger: waves 4-7 one barrier behind
+    int kt = 0, i = 0;
+    auto next = [&]() {
+      advance(c1);
+      advance(c2);
+      if (++kt == KT) {
+        kt = 0;
+        ++i;
+        c0 = cur_at(i);
+      }
+    };
+    for (int v = 0; v < V; v += 2) {
+      step(v, kt, i > 0, bf0, bf1);
+      next();
+      if (v + 1 < V) {
+        step(v + 1, kt, i > 0, bf1, bf0);
+        next();
+      }
+    }
+  } else {
+    // SCH == 2: the SCH 0 schedule with the per-phase instruction overhead taken out of the
+    // load half-phases (the half-phase in which a wave stages, waits and reads while its SIMD
+    // partner runs its MFMA cluster): K-steps unrolled by two so the LDS buffer parity is a
+    // compile-time constant, every fragment read is one ds_read_b128 off one of 8 per-lane base
+    // registers with an immediate offset (no address VALU), the stage offsets of a unit are
+    // computed once when a cursor enters it (one scalar add per stage), the wait role is one
+    // scalar per K-step, and the epilogue stores carry no diagnostic branches.
+    static_assert(EPI == EPI_BF16, "SCH 2: bf16 epilogue only");
+    const int l16 = lane & 15, lq = lane >> 4, sw = kswz(l16);  // kswz(row) == kswz(row & 15)
+    const uint32_t sbase = lds_addr(smem);
+    uint32_t rbA[2][2], rbB[2][2];  // [parity][k half]
+#pragma unroll
+    for (int par = 0; par < 2; ++par)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const uint32_t ch = (uint32_t)((((kk * 4 + lq) ^ sw)) << 4);
+        rbA[par][kk] = sbase + par * 4 * HALF + (wr * 64 + l16) * 128 + ch;
+        rbB[par][kk] = sbase + par * 4 * HALF + 2 * HALF + (wc * 32 + l16) * 128 + ch;
+      }
+    // a unit's tile and the byte offsets of its four half-tile row blocks
+    struct LCur { int o0, o1, o2, o3, m0, n0; };
+    auto lcur_at = [&](int i) {
+      LCur c;
+      unit_tile<EPI>(a, ubase + i * ustride, c.m0, c.n0);
+      c.o0 = __builtin_amdgcn_readfirstlane(c.m0 * a.lda * 2);
+      c.o1 = __builtin_amdgcn_readfirstlane((c.m0 + 128) * a.lda * 2);
+      c.o2 = __builtin_amdgcn_readfirstlane(c.n0 * a.ldb * 2);
+      c.o3 = __builtin_amdgcn_readfirstlane((c.n0 + 128) * a.ldb * 2);
+      return c;
+    };
+    // stage half h of K-step k of the current unit (k >= KT: step k - KT of the next unit; past
+    // the block's last unit "next" is the last unit again, re-staged into buffers nobody reads)
+    auto lstage = [&](const LCur& cur, const LCur& nxt, int k, auto par_c, auto h_c) {
+      constexpr int par = decltype(par_c)::value, h = decltype(h_c)::value;
+      const int oc = h == 0 ? cur.o0 : h == 1 ? cur.o1 : h == 2 ? cur.o2 : cur.o3;
+      const int on = h == 0 ? nxt.o0 : h == 1 ? nxt.o1 : h == 2 ? nxt.o2 : nxt.o3;
+      const uint32_t toff = (uint32_t)(k < KT ? oc + k * (BK * 2) : on + (k - KT) * (BK * 2));
+      char* d = smem + (par * 4 + h) * HALF;
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rA : rB, (lds_t*)(d + (p * 64 + wave * 8) * 128),
+                                                 16, (h < 2 ? voA[p] : voB[p]) + toff, 0, 0, 0);
+    };
+    auto rd16 = [](uint32_t addr, auto off_c) {
+      constexpr int off = decltype(off_c)::value;
+      u32x4 r;
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(off) : "memory");
+      return __builtin_bit_cast(bf16x8, r);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    auto lreadA = [&](auto par_c, auto mq_c) {
+      constexpr int par = decltype(par_c)::value, mq = decltype(mq_c)::value;
+      af[0][0] = rd16(rbA[par][0], std::integral_constant<int, mq * HALF>{});
+      af[0][1] = rd16(rbA[par][1], std::integral_constant<int, mq * HALF>{});
+      af[1][0] = rd16(rbA[par][0], std::integral_constant<int, mq * HALF + 2048>{});
+      af[1][1] = rd16(rbA[par][1], std::integral_constant<int, mq * HALF + 2048>{});
+      af[2][0] = rd16(rbA[par][0], std::integral_constant<int, mq * HALF + 4096>{});
+      af[2][1] = rd16(rbA[par][1], std::integral_constant<int, mq * HALF + 4096>{});
+      af[3][0] = rd16(rbA[par][0], std::integral_constant<int, mq * HALF + 6144>{});
+      af[3][1] = rd16(rbA[par][1], std::integral_constant<int, mq * HALF + 6144>{});
+    };
+    auto lreadB = [&](auto par_c, auto nq_c, bf16x8 (&bf)[2][2]) {
+      constexpr int par = decltype(par_c)::value, nq = decltype(nq_c)::value;
+      bf[0][0] = rd16(rbB[par][0], std::integral_constant<int, nq * HALF>{});
+      bf[0][1] = rd16(rbB[par][1], std::integral_constant<int, nq * HALF>{});
+      bf[1][0] = rd16(rbB[par][0], std::integral_constant<int, nq * HALF + 2048>{});
+      bf[1][1] = rd16(rbB[par][1], std::integral_constant<int, nq * HALF + 2048>{});
+    };
+    auto lstore = [&](const LCur& c, int mq, int nq) __attribute__((always_inline)) {
+      const f32x4 bj0 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + cq);
+      const f32x4 bj1 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + 16 + cq);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 v0 = acc[mq][nq][i][0] + bj0, v1 = acc[mq][nq][i][1] + bj1;
+        u32x2 h0 = __builtin_bit_cast(u32x2, bf16x4{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]});
+        u32x2 h1 = __builtin_bit_cast(u32x2, bf16x4{(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]});
+        const auto sx = __builtin_amdgcn_permlane16_swap(h0[0], h1[0], false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(h0[1], h1[1], false, false);
+        const u32x4 o = u32x4{sx[0], sy[0], sx[1], sy[1]};
+        const uint32_t off = voQ + (uint32_t)__builtin_amdgcn_readfirstlane(
+                                       ((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 0);
+        acc[mq][nq][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[mq][nq][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    // roles (compile-time, one step body per role): 0 ordinary, 1 a unit's last K-step (its
+    // quadrant stores sit between the stages), 2 the first K-step after an epilogue
+    auto lwait = [&](auto phase_c, auto role_c) {
+      constexpr int p = decltype(phase_c)::value, role = decltype(role_c)::value;
+      constexpr int n = role == 0 ? 8 : role == 1 ? 8 + p * QS : 8 + (4 - p) * QS;
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(n));
+    };
+    auto lgkm0 = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // one K-step k of the current unit in buffer parity par
+    auto lstep = [&](auto par_c, auto role_c, int k, const LCur& cur, const LCur& nxt) {
+      constexpr int par = decltype(par_c)::value, role = decltype(role_c)::value;
+      using Pc = std::integral_constant<int, par>;
+      using Qc = std::integral_constant<int, par ^ 1>;
+      // phase 0: quadrant (0,0)
+      lstage(cur, nxt, k + 1, Qc{}, I3{});
+      lwait(I0{}, role_c);
+      lreadA(Pc{}, I0{});
+      lreadB(Pc{}, I0{}, bf0);
+      DNA_BARRIER();
+      lgkm0();
+      mma(0, 0, bf0);
+      if constexpr (role == 1) lstore(cur, 0, 0);
+      DNA_BARRIER();
+      // phase 1: quadrant (0,1)
+      lstage(cur, nxt, k + 1, Qc{}, I1{});
+      lwait(I1{}, role_c);
+      lreadB(Pc{}, I1{}, bf1);
+      DNA_BARRIER();
+      lgkm0();
+      mma(0, 1, bf1);
+      if constexpr (role == 1) lstore(cur, 0, 1);
+      DNA_BARRIER();
+      // phase 2: quadrant (1,1)
+      lstage(cur, nxt, k + 2, Pc{}, I0{});
+      lwait(I2{}, role_c);
+      lreadA(Pc{}, I1{});
+      DNA_BARRIER();
+      lgkm0();
+      mma(1, 1, bf1);
+      if constexpr (role == 1) lstore(cur, 1, 1);
+      DNA_BARRIER();
+      // phase 3: quadrant (1,0)
+      lstage(cur, nxt, k + 2, Pc{}, I2{});
+      lwait(I3{}, role_c);
+      DNA_BARRIER();
+      mma(1, 0, bf0);
+      if constexpr (role == 1) lstore(cur, 1, 0);
+      DNA_BARRIER();
+    };
+    using R0 = std::integral_constant<int, 0>;
+    using RL = std::integral_constant<int, 1>;
+    using RF = std::integral_constant<int, 2>;
+    // KT is even (launcher), so every unit starts on buffer parity 0
+    LCur cur = lcur_at(0), nxt = lcur_at(nb > 1 ? 1 : 0);
+    // prologue (as SCH 0): all four halves of step 0, A_0 / B_0 of step 1
+    lstage(cur, nxt, 0, I0{}, I0{});
+    lstage(cur, nxt, 0, I0{}, I2{});
+    lstage(cur, nxt, 0, I0{}, I3{});
+    lstage(cur, nxt, 0, I0{}, I1{});
+    lstage(cur, nxt, 1, I1{}, I0{});
+    lstage(cur, nxt, 1, I1{}, I2{});
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
+    DNA_BARRIER();
+    if (wr == 1) DNA_BARRIER();  // stagger: waves 4-7 one barrier behind
+    lstep(I0{}, R0{}, 0, cur, nxt);
+    for (int i = 0;;) {
+      for (int k = 1; k < KT - 1; k += 2) {
+        lstep(I1{}, R0{}, k, cur, nxt);
+        lstep(I0{}, R0{}, k + 1, cur, nxt);
+      }
+      lstep(I1{}, RL{}, KT - 1, cur, nxt);
+      if (++i == nb) break;
+      cur = nxt;
+      nxt = lcur_at(i + 1 < nb ? i + 1 : i);
+      lstep(I0{}, RF{}, 0, cur, nxt);
+    }
+  }
   if (wr == 0) DNA_BARRIER();  // re-align the two wave groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the block
 }
@@ -895,7 +1202,7 @@ struct WArgs {
   int T, Nw, Kw, tilesM, tilesN, s, KTtot;
 };
 
-template <bool IMM>
+template <bool IMM, int SCH = 0>
 __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
   constexpr int QS = 8;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -1029,6 +1336,7 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
   advance(c1);
   advance(c2);
   advance(c2);
+  if constexpr (SCH == 0) {
   stage(c0, 0, 0);
   stage(c0, 0, 2);
   stage(c0, 0, 3);
@@ -1097,6 +1405,254 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
     }
     c0 = cur_at(i + 1);
   }
+  } else if constexpr (SCH == 1) {
+    // SCH == 1: gemmp_kernel's balanced-read schedule (reads A_0 / B_1 / A_1 / B_0(next) per
+    // phase, 5 half-tiles in flight; see there). Units have per-chunk lengths, so the current
+    // unit's last K-step starts at phase 4 * (len - 1).
+    constexpr int hA0 = 0, hA1 = 1, hB0 = 2, hB1 = 3;
+    auto wait_p = [&](auto phase, int role) {
+      constexpr int p = decltype(phase)::value;
+      if (role == 0) __builtin_amdgcn_s_waitcnt(waitcnt_imm(10));
+      else if (role == 1) __builtin_amdgcn_s_waitcnt(waitcnt_imm(10 + pend_stores<EPI_F32>(1, p)));
+      else if (role == 2) __builtin_amdgcn_s_waitcnt(waitcnt_imm(10 + pend_stores<EPI_F32>(2, p)));
+      else if (role == 3) __builtin_amdgcn_s_waitcnt(waitcnt_imm(10 + pend_stores<EPI_F32>(3, p)));
+      else __builtin_amdgcn_s_waitcnt(waitcnt_imm(10 + pend_stores<EPI_F32>(4, p)));
+    };
+    auto lgkm0 = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto step = [&](int v, int kt, bool prev, bf16x8 (&bB0)[2][2], bf16x8 (&bB1)[2][2]) {
+      const bool st = kt == c0.len - 1;
+      const int role = __builtin_amdgcn_readfirstlane(
+          st ? (prev && kt == 1 ? 4 : 3) : prev && kt == 0 ? 1 : prev && kt == 1 ? 2 : 0);
+      stage(c1, v + 1, hA1);
+      wait_p(std::integral_constant<int, 0>{}, role);
+      readA(v, 0);
+      DNA_BARRIER();
+      lgkm0();
+      mma(0, 0, bB0);
+      if (st) store_quadrant(c0, 0, 0);
+      DNA_BARRIER();
+      stage(c2, v + 2, hB0);
+      wait_p(std::integral_constant<int, 1>{}, role);
+      readB(v, 1, bB1);
+      DNA_BARRIER();
+      lgkm0();
+      mma(0, 1, bB1);
+      if (st) store_quadrant(c0, 0, 1);
+      DNA_BARRIER();
+      stage(c2, v + 2, hA0);
+      wait_p(std::integral_constant<int, 2>{}, role);
+      readA(v, 1);
+      DNA_BARRIER();
+      lgkm0();
+      mma(1, 1, bB1);
+      if (st) store_quadrant(c0, 1, 1);
+      DNA_BARRIER();
+      stage(c2, v + 2, hB1);
+      wait_p(std::integral_constant<int, 3>{}, role);
+      readB(v + 1, 0, bB1);
+      DNA_BARRIER();
+      lgkm0();
+      mma(1, 0, bB0);
+      if (st) store_quadrant(c0, 1, 0);
+      DNA_BARRIER();
+    };
+    stage(c0, 0, hB0);
+    stage(c0, 0, hA0);
+    stage(c0, 0, hB1);
+    stage(c0, 0, hA1);
+    stage(c1, 1, hB0);
+    stage(c1, 1, hA0);
+    stage(c1, 1, hB1);
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(10));
+    DNA_BARRIER();
+    readB(0, 0, bf0);
+    if (wr == 1) DNA_BARRIER();
+    int kt = 0, i = 0;
+    const int V = [&]() {  // K-steps of this block's units
+      int n = 0;
+      for (int j = 0; j < nb; ++j) n += cur_at(j).len;
+      return n;
+    }();
+    auto next = [&]() {
+      advance(c1);
+      advance(c2);
+      if (++kt == c0.len) {
+        kt = 0;
+        ++i;
+        c0 = cur_at(i);
+      }
+    };
+    for (int v = 0; v < V; v += 2) {
+      step(v, kt, i > 0, bf0, bf1);
+      next();
+      if (v + 1 < V) {
+        step(v + 1, kt, i > 0, bf1, bf0);
+        next();
+      }
+    }
+  } else {
+    // SCH == 2: the lean form of the SCH 0 schedule (see gemmp_kernel's SCH == 2): K-steps
+    // unrolled by two with compile-time buffer parity, fragment reads off per-lane base
+    // registers with immediate offsets, per-unit stage offsets and buffer resources computed once
+    // per unit, compile-time wait roles. Chunks are whole K-step pairs (WArgs.pairs), so every
+    // unit starts on parity 0.
+    uint32_t bA[2][4], bB[2][2];
+    const uint32_t sbase = lds_addr(smem);
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bA[par][i] = sbase + par * 4 * HALF + loA[i];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bB[par][j] = sbase + par * 4 * HALF + 2 * HALF + loB[j];
+    }
+    struct WCur { const bf16 *pA, *pB; uint32_t nA, nB; int len, m0, n0, c; };
+    auto wcur_at = [&](int i) {
+      WCur w;
+      const int u = i * G + L;
+      w.c = u / tiles;
+      const int tl = u - w.c * tiles;
+      w.m0 = (tl / a.tilesN) * BM;
+      w.n0 = (tl % a.tilesN) * BN;
+      const int KP = a.KTtot >> 1;
+      const int s0 = 2 * (int)((long long)w.c * KP / a.s), s1 = 2 * (int)((long long)(w.c + 1) * KP / a.s);
+      w.len = s1 - s0;
+      const long long r0 = (long long)s0 * BK;
+      const int rows = (int)(min((long long)a.T, (long long)s1 * BK) - r0);
+      w.pA = a.dy + r0 * a.ldy;
+      w.pB = a.x + r0 * a.ldx;
+      w.nA = (uint32_t)((size_t)rows * a.ldy * 2);
+      w.nB = (uint32_t)((size_t)rows * a.ldx * 2);
+      return w;
+    };
+    // stage half h of K-step k of the current unit (k >= len: step k - len of the next unit)
+    auto wstage = [&](const WCur& cur, const WCur& nxt, int k, auto par_c, auto h_c) {
+      constexpr int par = decltype(par_c)::value, h = decltype(h_c)::value;
+      constexpr bool isA = h < 2;
+      const bool in = k < cur.len;
+      const int kk = in ? k : k - cur.len;
+      const int col0 = isA ? (in ? cur.m0 : nxt.m0) + h * 128 : (in ? cur.n0 : nxt.n0) + (h - 2) * 128;
+      const int ld = isA ? a.ldy : a.ldx;
+      const bf16* base = isA ? (in ? cur.pA : nxt.pA) : (in ? cur.pB : nxt.pB);
+      const uint32_t bytes = isA ? (in ? cur.nA : nxt.nA) : (in ? cur.nB : nxt.nB);
+      const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane((kk * BK * ld + col0) * 2);
+      char* d = smem + (par * 4 + h) * HALF;
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(out_rsrc(base, bytes), (lds_t*)(d + (p * 32 + wave * 4) * 256),
+                                                 16, (isA ? voA[p] : voB[p]) + toff, 0, 0, 0);
+    };
+    auto rd2 = [](uint32_t addr, auto off_c, bf16x8& k0, bf16x8& k1) {
+      constexpr int off = decltype(off_c)::value;
+      const bf16x4 x0 = tr_read_imm<off>(addr), x1 = tr_read_imm<off + 1024>(addr);
+      const bf16x4 x2 = tr_read_imm<off + 8192>(addr), x3 = tr_read_imm<off + 9216>(addr);
+      k0 = bf16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      k1 = bf16x8{x2[0], x2[1], x2[2], x2[3], x3[0], x3[1], x3[2], x3[3]};
+    };
+    auto wreadA = [&](auto par_c, auto mq_c) {
+      constexpr int par = decltype(par_c)::value, mq = decltype(mq_c)::value;
+      using O = std::integral_constant<int, mq * HALF>;
+      rd2(bA[par][0], O{}, af[0][0], af[0][1]);
+      rd2(bA[par][1], O{}, af[1][0], af[1][1]);
+      rd2(bA[par][2], O{}, af[2][0], af[2][1]);
+      rd2(bA[par][3], O{}, af[3][0], af[3][1]);
+    };
+    auto wreadB = [&](auto par_c, auto nq_c, bf16x8 (&bf)[2][2]) {
+      constexpr int par = decltype(par_c)::value, nq = decltype(nq_c)::value;
+      using O = std::integral_constant<int, nq * HALF>;
+      rd2(bB[par][0], O{}, bf[0][0], bf[0][1]);
+      rd2(bB[par][1], O{}, bf[1][0], bf[1][1]);
+    };
+    auto wstore = [&](const WCur& w, int mq, int nq) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t toff = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)((((size_t)w.c * a.Nw + w.m0 + mq * 128 + i * 16) * a.Kw + w.n0 + nq * 128) * 4));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mq][nq][i][j]), rC,
+                                                 voC + toff + j * 64, 0, 0);
+          acc[mq][nq][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    };
+    auto wwait = [&](auto phase_c, auto role_c) {
+      constexpr int p = decltype(phase_c)::value, role = decltype(role_c)::value;
+      constexpr int n = role == 0 ? 8 : role == 1 ? 8 + p * QS : 8 + (4 - p) * QS;
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(n));
+    };
+    auto lgkm0 = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    auto wstep = [&](auto par_c, auto role_c, int k, const WCur& cur, const WCur& nxt) {
+      constexpr int par = decltype(par_c)::value, role = decltype(role_c)::value;
+      using Pc = std::integral_constant<int, par>;
+      using Qc = std::integral_constant<int, par ^ 1>;
+      wstage(cur, nxt, k + 1, Qc{}, I3{});
+      wwait(I0{}, role_c);
+      wreadA(Pc{}, I0{});
+      wreadB(Pc{}, I0{}, bf0);
+      DNA_BARRIER();
+      lgkm0();
+      mma(0, 0, bf0);
+      if constexpr (role == 1) wstore(cur, 0, 0);
+      DNA_BARRIER();
+      wstage(cur, nxt, k + 1, Qc{}, I1{});
+      wwait(I1{}, role_c);
+      wreadB(Pc{}, I1{}, bf1);
+      DNA_BARRIER();
+      lgkm0();
+      mma(0, 1, bf1);
+      if constexpr (role == 1) wstore(cur, 0, 1);
+      DNA_BARRIER();
+      wstage(cur, nxt, k + 2, Pc{}, I0{});
+      wwait(I2{}, role_c);
+      wreadA(Pc{}, I1{});
+      DNA_BARRIER();
+      lgkm0();
+      mma(1, 1, bf1);
+      if constexpr (role == 1) wstore(cur, 1, 1);
+      DNA_BARRIER();
+      wstage(cur, nxt, k + 2, Pc{}, I2{});
+      wwait(I3{}, role_c);
+      DNA_BARRIER();
+      mma(1, 0, bf0);
+      if constexpr (role == 1) wstore(cur, 1, 0);
+      DNA_BARRIER();
+    };
+    using R0 = std::integral_constant<int, 0>;
+    using RL = std::integral_constant<int, 1>;
+    using RF = std::integral_constant<int, 2>;
+    WCur cur = wcur_at(0), nxt = wcur_at(nb > 1 ? 1 : 0);
+    wstage(cur, nxt, 0, I0{}, I0{});
+    wstage(cur, nxt, 0, I0{}, I2{});
+    wstage(cur, nxt, 0, I0{}, I3{});
+    wstage(cur, nxt, 0, I0{}, I1{});
+    wstage(cur, nxt, 1, I1{}, I0{});
+    wstage(cur, nxt, 1, I1{}, I2{});
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
+    DNA_BARRIER();
+    if (wr == 1) DNA_BARRIER();
+    wstep(I0{}, R0{}, 0, cur, nxt);
+    for (int i = 0;;) {
+      for (int k = 1; k < cur.len - 1; k += 2) {
+        wstep(I1{}, R0{}, k, cur, nxt);
+        wstep(I0{}, R0{}, k + 1, cur, nxt);
+      }
+      wstep(I1{}, RL{}, cur.len - 1, cur, nxt);
+      if (++i == nb) break;
+      cur = nxt;
+      nxt = wcur_at(i + 1 < nb ? i + 1 : i);
+      wstep(I0{}, RF{}, 0, cur, nxt);
+    }
+  }
   if (wr == 0) DNA_BARRIER();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -1135,6 +1691,13 @@ inline bool persistent_enabled() {
   return on == 1;
 }
 
+// persistent-kernel half-tile schedule (DNA_GEMM_SCHED, read per call for in-process A/B):
+// 2 (default) = the lean K-step body, 0 = the original one, 1 = balanced reads (slower)
+inline int gemm_sched() {
+  const char* e = getenv("DNA_GEMM_SCHED");
+  return e ? atoi(e) : 2;
+}
+
 template <int EPI>
 int launchp(Args& a, hipStream_t s, const char* name) {
   a.tilesM = (a.M + BM - 1) / BM;
@@ -1156,7 +1719,10 @@ int launchp(Args& a, hipStream_t s, const char* name) {
   if (const char* e = getenv("DNA_GEMM_ORDER")) a.order = atoi(e);
   const char* ab = getenv("DNA_GEMM_ABL");
   const int abl = ab ? atoi(ab) : 0;
-  if (abl == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 1>), dim3(G), dim3(NTHR), 0, s, a);
+  if (abl == 0 && gemm_sched() == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 1>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (EPI == EPI_BF16 && abl == 0 && gemm_sched() == 2 && (a.K / BK) % 2 == 0)
+    hipLaunchKernelGGL((gemmp_kernel<EPI_BF16, 0, 2>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (abl == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 1>), dim3(G), dim3(NTHR), 0, s, a);
   else if (abl == 2) hipLaunchKernelGGL((gemmp_kernel<EPI, 2>), dim3(G), dim3(NTHR), 0, s, a);
   else if (abl == 3) hipLaunchKernelGGL((gemmp_kernel<EPI, 3>), dim3(G), dim3(NTHR), 0, s, a);
   else if (abl == 7) hipLaunchKernelGGL((gemmp_kernel<EPI, 7>), dim3(G), dim3(NTHR), 0, s, a);
@@ -1321,7 +1887,11 @@ extern "C" int dna_linear_wgrad_p(const void* dy, const void* x, int M, int N, i
   int G = num_cus() & ~7;
   G = U < G ? U : G;
   const char* ie = getenv("DNA_WGRAD_IMM");  // A/B: 0 = per-read address VALU
-  if (!ie || atoi(ie) != 0)
+  if (gemm_sched() == 2 && KTtot % 2 == 0 && KTtot / 2 / splits >= 1 && (!ie || atoi(ie) != 0))
+    hipLaunchKernelGGL((wgradp_kernel<true, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), a);
+  else if (gemm_sched() == 1 && (!ie || atoi(ie) != 0))
+    hipLaunchKernelGGL((wgradp_kernel<true, 1>), dim3(G), dim3(NTHR), 0, as_stream(stream), a);
+  else if (!ie || atoi(ie) != 0)
     hipLaunchKernelGGL(wgradp_kernel<true>, dim3(G), dim3(NTHR), 0, as_stream(stream), a);
   else
     hipLaunchKernelGGL(wgradp_kernel<false>, dim3(G), dim3(NTHR), 0, as_stream(stream), a);

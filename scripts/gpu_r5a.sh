@@ -1,0 +1,11 @@
+#!/bin/bash
+# Balanced-read GEMM schedule (DNA_GEMM_SCHED=1): GEMM parity tests under it, then an interleaved
+# per-shape A/B against the default schedule.
+set -o pipefail
+O=gpurun_out/${TAG:-r5a}
+mkdir -p $O
+DNA_GEMM_SCHED=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "gemm or wgrad" -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 400 python scripts/gemm_shapes.py --kinds fwd,dgrad,wgrad --rounds 3 --iters 10 \
+  --variants "base;sch1,DNA_GEMM_SCHED=1" > $O/ab.jsonl 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
+cat $O/ab.jsonl
