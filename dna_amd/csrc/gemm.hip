@@ -1082,9 +1082,15 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       bf[1][0] = rd16(rbB[par][0], std::integral_constant<int, nq * HALF + 2048>{});
       bf[1][1] = rd16(rbB[par][1], std::integral_constant<int, nq * HALF + 2048>{});
     };
-    auto lstore = [&](const LCur& c, int mq, int nq) __attribute__((always_inline)) {
-      const f32x4 bj0 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + cq);
-      const f32x4 bj1 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + 16 + cq);
+    // the bias of quadrant column block nq, read in the load half-phase (beside the fragment
+    // reads, retired by the same lgkmcnt wait) so the epilogue never waits on LDS
+    auto lbias = [&](const LCur& c, int nq, f32x4& bj0, f32x4& bj1) {
+      bj0 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + cq);
+      bj1 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + nq * 128 + wc * 32 + 16 + cq);
+    };
+    // stores quadrant (mq, nq) of the unit's tile; the accumulators are not re-zeroed: the next
+    // unit's first K-step starts its MFMA chains from a zero C operand (mmaz)
+    auto lstore = [&](const LCur& c, int mq, int nq, f32x4 bj0, f32x4 bj1) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const f32x4 v0 = acc[mq][nq][i][0] + bj0, v1 = acc[mq][nq][i][1] + bj1;
@@ -1093,12 +1099,24 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
         const auto sx = __builtin_amdgcn_permlane16_swap(h0[0], h1[0], false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(h0[1], h1[1], false, false);
         const u32x4 o = u32x4{sx[0], sy[0], sx[1], sy[1]};
-        const uint32_t off = voQ + (uint32_t)__builtin_amdgcn_readfirstlane(
-                                       ((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
-        __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 0);
-        acc[mq][nq][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc[mq][nq][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint32_t off = voQ + (uint32_t)__builtin_amdgcn_readfirstlane(
+                                 ((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
+        off = a.dbg == 1 ? kOOB : off;  // diagnostics: stores dropped by the range check
+        if (a.nt) __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 0);
       }
+    };
+    auto mmaz = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = mfma(bf[j][0], af[i][0], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = mfma(bf[j][1], af[i][1], acc[mq][nq][i][j]);
+      __builtin_amdgcn_s_setprio(0);
     };
     // roles (compile-time, one step body per role): 0 ordinary, 1 a unit's last K-step (its
     // quadrant stores sit between the stages), 2 the first K-step after an epilogue
@@ -1111,29 +1129,38 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     };
-    // one K-step k of the current unit in buffer parity par
-    auto lstep = [&](auto par_c, auto role_c, int k, const LCur& cur, const LCur& nxt) {
+    // one K-step k of the current unit in buffer parity par; ZI: the unit's first K-step (MFMA
+    // chains start from zero)
+    auto lstep = [&](auto par_c, auto role_c, auto zi_c, int k, const LCur& cur, const LCur& nxt) {
       constexpr int par = decltype(par_c)::value, role = decltype(role_c)::value;
+      constexpr bool ZI = decltype(zi_c)::value;
       using Pc = std::integral_constant<int, par>;
       using Qc = std::integral_constant<int, par ^ 1>;
+      auto mm = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+        if constexpr (ZI) mmaz(mq, nq, bf);
+        else mma(mq, nq, bf);
+      };
+      f32x4 bj0, bj1;
       // phase 0: quadrant (0,0)
       lstage(cur, nxt, k + 1, Qc{}, I3{});
       lwait(I0{}, role_c);
       lreadA(Pc{}, I0{});
       lreadB(Pc{}, I0{}, bf0);
+      if constexpr (role == 1) lbias(cur, 0, bj0, bj1);
       DNA_BARRIER();
       lgkm0();
-      mma(0, 0, bf0);
-      if constexpr (role == 1) lstore(cur, 0, 0);
+      mm(0, 0, bf0);
+      if constexpr (role == 1) lstore(cur, 0, 0, bj0, bj1);
       DNA_BARRIER();
       // phase 1: quadrant (0,1)
       lstage(cur, nxt, k + 1, Qc{}, I1{});
       lwait(I1{}, role_c);
       lreadB(Pc{}, I1{}, bf1);
+      if constexpr (role == 1) lbias(cur, 1, bj0, bj1);
       DNA_BARRIER();
       lgkm0();
-      mma(0, 1, bf1);
-      if constexpr (role == 1) lstore(cur, 0, 1);
+      mm(0, 1, bf1);
+      if constexpr (role == 1) lstore(cur, 0, 1, bj0, bj1);
       DNA_BARRIER();
       // phase 2: quadrant (1,1)
       lstage(cur, nxt, k + 2, Pc{}, I0{});
@@ -1141,17 +1168,21 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       lreadA(Pc{}, I1{});
       DNA_BARRIER();
       lgkm0();
-      mma(1, 1, bf1);
-      if constexpr (role == 1) lstore(cur, 1, 1);
+      mm(1, 1, bf1);
+      if constexpr (role == 1) lstore(cur, 1, 1, bj0, bj1);
       DNA_BARRIER();
       // phase 3: quadrant (1,0)
       lstage(cur, nxt, k + 2, Pc{}, I2{});
       lwait(I3{}, role_c);
+      if constexpr (role == 1) lbias(cur, 0, bj0, bj1);
       DNA_BARRIER();
-      mma(1, 0, bf0);
-      if constexpr (role == 1) lstore(cur, 1, 0);
+      if constexpr (role == 1) lgkm0();
+      mm(1, 0, bf0);
+      if constexpr (role == 1) lstore(cur, 1, 0, bj0, bj1);
       DNA_BARRIER();
     };
+    using ZN = std::false_type;
+    using ZY = std::true_type;
     using R0 = std::integral_constant<int, 0>;
     using RL = std::integral_constant<int, 1>;
     using RF = std::integral_constant<int, 2>;
@@ -1167,17 +1198,17 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
     DNA_BARRIER();
     if (wr == 1) DNA_BARRIER();  // stagger: waves 4-7 one barrier behind
-    lstep(I0{}, R0{}, 0, cur, nxt);
+    lstep(I0{}, R0{}, ZY{}, 0, cur, nxt);
     for (int i = 0;;) {
       for (int k = 1; k < KT - 1; k += 2) {
-        lstep(I1{}, R0{}, k, cur, nxt);
-        lstep(I0{}, R0{}, k + 1, cur, nxt);
+        lstep(I1{}, R0{}, ZN{}, k, cur, nxt);
+        lstep(I0{}, R0{}, ZN{}, k + 1, cur, nxt);
       }
-      lstep(I1{}, RL{}, KT - 1, cur, nxt);
+      lstep(I1{}, RL{}, ZN{}, KT - 1, cur, nxt);
       if (++i == nb) break;
       cur = nxt;
       nxt = lcur_at(i + 1 < nb ? i + 1 : i);
-      lstep(I0{}, RF{}, 0, cur, nxt);
+      lstep(I0{}, RF{}, ZY{}, 0, cur, nxt);
     }
   }
   if (wr == 0) DNA_BARRIER();  // re-align the two wave groups
@@ -1574,9 +1605,21 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
         for (int j = 0; j < 2; ++j) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mq][nq][i][j]), rC,
                                                  voC + toff + j * 64, 0, 0);
-          acc[mq][nq][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
+    };
+    auto& mma_acc = mma;
+    auto mmaz = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = mfma(bf[j][0], af[i][0], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mq][nq][i][j] = mfma(bf[j][1], af[i][1], acc[mq][nq][i][j]);
+      __builtin_amdgcn_s_setprio(0);
     };
     auto wwait = [&](auto phase_c, auto role_c) {
       constexpr int p = decltype(phase_c)::value, role = decltype(role_c)::value;
@@ -1591,10 +1634,15 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
-    auto wstep = [&](auto par_c, auto role_c, int k, const WCur& cur, const WCur& nxt) {
+    auto wstep = [&](auto par_c, auto role_c, auto zi_c, int k, const WCur& cur, const WCur& nxt) {
       constexpr int par = decltype(par_c)::value, role = decltype(role_c)::value;
+      constexpr bool ZI = decltype(zi_c)::value;
       using Pc = std::integral_constant<int, par>;
       using Qc = std::integral_constant<int, par ^ 1>;
+      auto mma = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+        if constexpr (ZI) mmaz(mq, nq, bf);
+        else mma_acc(mq, nq, bf);
+      };
       wstage(cur, nxt, k + 1, Qc{}, I3{});
       wwait(I0{}, role_c);
       wreadA(Pc{}, I0{});
@@ -1640,17 +1688,19 @@ __global__ __launch_bounds__(NTHR) void wgradp_kernel(WArgs a) {
     __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
     DNA_BARRIER();
     if (wr == 1) DNA_BARRIER();
-    wstep(I0{}, R0{}, 0, cur, nxt);
+    using ZN = std::false_type;
+    using ZY = std::true_type;
+    wstep(I0{}, R0{}, ZY{}, 0, cur, nxt);
     for (int i = 0;;) {
       for (int k = 1; k < cur.len - 1; k += 2) {
-        wstep(I1{}, R0{}, k, cur, nxt);
-        wstep(I0{}, R0{}, k + 1, cur, nxt);
+        wstep(I1{}, R0{}, ZN{}, k, cur, nxt);
+        wstep(I0{}, R0{}, ZN{}, k + 1, cur, nxt);
       }
-      wstep(I1{}, RL{}, cur.len - 1, cur, nxt);
+      wstep(I1{}, RL{}, ZN{}, cur.len - 1, cur, nxt);
       if (++i == nb) break;
       cur = nxt;
       nxt = wcur_at(i + 1 < nb ? i + 1 : i);
-      wstep(I0{}, RF{}, 0, cur, nxt);
+      wstep(I0{}, RF{}, ZY{}, 0, cur, nxt);
     }
   }
   if (wr == 0) DNA_BARRIER();
