@@ -1102,6 +1102,10 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
         uint32_t off = voQ + (uint32_t)__builtin_amdgcn_readfirstlane(
                                  ((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
         off = a.dbg == 1 ? kOOB : off;  // diagnostics: stores dropped by the range check
+        // DNA_GEMM_NT=1 (A/B): non-temporal stores. Measured (profiles/r03b): nt, sc1 and sc0 sc1
+        // stores and whole-line store patterns are all slower or equal; dropping the stores
+        // (DNA_GEMM_DBG=1) saves ~3.5 us per unit at every K: the in-order vmcnt makes the
+        // stages issued after a unit's stores wait for them
         if (a.nt) __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 2);
         else __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 0);
       }
