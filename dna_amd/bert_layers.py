@@ -242,8 +242,8 @@ class BertForMaskedLM(nn.Module):
             return None
         return self._lpt_provider(p)
 
-    def _linear(self, x, w, b=None):
-        return DF.linear(x, w, self._lp(w), b, w_lpt=self._lp_t(w))
+    def _linear(self, x, w, b=None, geglu=None):
+        return DF.linear(x, w, self._lp(w), b, w_lpt=self._lp_t(w), geglu=geglu)
 
     # -- the hot path ------------------------------------------------------------------------
     def mlm_logits(self, input_ids: torch.Tensor, index: MLMIndex) -> torch.Tensor:
@@ -287,8 +287,10 @@ class BertForMaskedLM(nn.Module):
                                               out.LayerNorm.bias, eps, 0, p_hidden, seed, off,
                                               True, bf16)
             mlp = layer.mlp
-            g = self._linear(yb if bf16 else y32, mlp.gated_layers.weight)
             seed, off = rng.take(n * cfg.intermediate_size) if p_hidden else (0, 0)
+            # the GeGLU forward runs in the gated_layers GEMM's epilogue where the kernel allows
+            g = self._linear(yb if bf16 else y32, mlp.gated_layers.weight,
+                             geglu=(p_hidden, seed, off))
             a = DF.GeGLU.apply(g, p_hidden, seed, off)
             o = self._linear(a, mlp.wo.weight)
             x32, xb = DF.FusedLayerNorm.apply(o, mlp.wo.bias, y32, mlp.layernorm.weight,

@@ -766,7 +766,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     const auto sy = __builtin_amdgcn_permlane16_swap(h0[1], h1[1], false, false);
     return u32x4{sx[0], sy[0], sx[1], sy[1]};
   };
-  auto store_geglu_half = [&](const Cur& c, int mq) __attribute__((always_inline)) {
+  auto store_geglu_half = [&](const auto& c, int mq) __attribute__((always_inline)) {
     const f32x4 b10 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + wc * 32 + cq);
     const f32x4 b11 = *reinterpret_cast<const f32x4*>(bias_lds + c.n0 + wc * 32 + 16 + cq);
     const f32x4 b20 = *reinterpret_cast<const f32x4*>(bias_lds + a.F + c.n0 + wc * 32 + cq);
@@ -1018,7 +1018,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     // registers with an immediate offset (no address VALU), the stage offsets of a unit are
     // computed once when a cursor enters it (one scalar add per stage), the wait role is one
     // scalar per K-step, and the epilogue stores carry no diagnostic branches.
-    static_assert(EPI == EPI_BF16, "SCH 2: bf16 epilogue only");
     const int l16 = lane & 15, lq = lane >> 4, sw = kswz(l16);  // kswz(row) == kswz(row & 15)
     const uint32_t sbase = lds_addr(smem);
     uint32_t rbA[2][2], rbB[2][2];  // [parity][k half]
@@ -1037,8 +1036,10 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       unit_tile<EPI>(a, ubase + i * ustride, c.m0, c.n0);
       c.o0 = __builtin_amdgcn_readfirstlane(c.m0 * a.lda * 2);
       c.o1 = __builtin_amdgcn_readfirstlane((c.m0 + 128) * a.lda * 2);
+      // weight rows of the two B halves: n0 + [0, 128) and n0 + [128, 256); GeGLU: the g1 rows
+      // n0 + [0, 128) and the g2 rows F + n0 + [0, 128)
       c.o2 = __builtin_amdgcn_readfirstlane(c.n0 * a.ldb * 2);
-      c.o3 = __builtin_amdgcn_readfirstlane((c.n0 + 128) * a.ldb * 2);
+      c.o3 = __builtin_amdgcn_readfirstlane((c.n0 + (EPI == EPI_GEGLU ? a.F : 128)) * a.ldb * 2);
       return c;
     };
     // stage half h of K-step k of the current unit (k >= KT: step k - KT of the next unit; past
@@ -1126,13 +1127,17 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     // quadrant stores sit between the stages), 2 the first K-step after an epilogue
     auto lwait = [&](auto phase_c, auto role_c) {
       constexpr int p = decltype(phase_c)::value, role = decltype(role_c)::value;
-      constexpr int n = role == 0 ? 8 : role == 1 ? 8 + p * QS : 8 + (4 - p) * QS;
+      // BF16: QS stores after every phase of a unit's last step; GeGLU: GS after phases 1 and 3
+      constexpr int n = EPI == EPI_BF16
+                            ? (role == 0 ? 8 : role == 1 ? 8 + p * QS : 8 + (4 - p) * QS)
+                            : (role == 0 ? 8 : role == 1 ? 8 + (p >= 2 ? GS : 0) : 8 + (p < 2 ? 2 * GS : GS));
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(n));
     };
     auto lgkm0 = [&]() {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     };
+    constexpr bool SB = EPI == EPI_BF16;  // per-quadrant stores (else GeGLU halves)
     // one K-step k of the current unit in buffer parity par; ZI: the unit's first K-step (MFMA
     // chains start from zero)
     auto lstep = [&](auto par_c, auto role_c, auto zi_c, int k, const LCur& cur, const LCur& nxt) {
@@ -1150,21 +1155,22 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       lwait(I0{}, role_c);
       lreadA(Pc{}, I0{});
       lreadB(Pc{}, I0{}, bf0);
-      if constexpr (role == 1) lbias(cur, 0, bj0, bj1);
+      if constexpr (SB && role == 1) lbias(cur, 0, bj0, bj1);
       DNA_BARRIER();
       lgkm0();
       mm(0, 0, bf0);
-      if constexpr (role == 1) lstore(cur, 0, 0, bj0, bj1);
+      if constexpr (SB && role == 1) lstore(cur, 0, 0, bj0, bj1);
       DNA_BARRIER();
       // phase 1: quadrant (0,1)
       lstage(cur, nxt, k + 1, Qc{}, I1{});
       lwait(I1{}, role_c);
       lreadB(Pc{}, I1{}, bf1);
-      if constexpr (role == 1) lbias(cur, 1, bj0, bj1);
+      if constexpr (SB && role == 1) lbias(cur, 1, bj0, bj1);
       DNA_BARRIER();
       lgkm0();
       mm(0, 1, bf1);
-      if constexpr (role == 1) lstore(cur, 0, 1, bj0, bj1);
+      if constexpr (SB && role == 1) lstore(cur, 0, 1, bj0, bj1);
+      if constexpr (!SB && role == 1) store_geglu_half(cur, 0);
       DNA_BARRIER();
       // phase 2: quadrant (1,1)
       lstage(cur, nxt, k + 2, Pc{}, I0{});
@@ -1173,16 +1179,17 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       DNA_BARRIER();
       lgkm0();
       mm(1, 1, bf1);
-      if constexpr (role == 1) lstore(cur, 1, 1, bj0, bj1);
+      if constexpr (SB && role == 1) lstore(cur, 1, 1, bj0, bj1);
       DNA_BARRIER();
       // phase 3: quadrant (1,0)
       lstage(cur, nxt, k + 2, Pc{}, I2{});
       lwait(I3{}, role_c);
-      if constexpr (role == 1) lbias(cur, 0, bj0, bj1);
+      if constexpr (SB && role == 1) lbias(cur, 0, bj0, bj1);
       DNA_BARRIER();
-      if constexpr (role == 1) lgkm0();
+      if constexpr (SB && role == 1) lgkm0();
       mm(1, 0, bf0);
-      if constexpr (role == 1) lstore(cur, 1, 0, bj0, bj1);
+      if constexpr (SB && role == 1) lstore(cur, 1, 0, bj0, bj1);
+      if constexpr (!SB && role == 1) store_geglu_half(cur, 1);
       DNA_BARRIER();
     };
     using ZN = std::false_type;
@@ -1774,8 +1781,8 @@ int launchp(Args& a, hipStream_t s, const char* name) {
   const char* ab = getenv("DNA_GEMM_ABL");
   const int abl = ab ? atoi(ab) : 0;
   if (abl == 0 && gemm_sched() == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 1>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (EPI == EPI_BF16 && abl == 0 && gemm_sched() == 2 && (a.K / BK) % 2 == 0)
-    hipLaunchKernelGGL((gemmp_kernel<EPI_BF16, 0, 2>), dim3(G), dim3(NTHR), 0, s, a);
+  else if (abl == 0 && gemm_sched() == 2 && (a.K / BK) % 2 == 0)
+    hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 2>), dim3(G), dim3(NTHR), 0, s, a);
   else if (abl == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 1>), dim3(G), dim3(NTHR), 0, s, a);
   else if (abl == 2) hipLaunchKernelGGL((gemmp_kernel<EPI, 2>), dim3(G), dim3(NTHR), 0, s, a);
   else if (abl == 3) hipLaunchKernelGGL((gemmp_kernel<EPI, 3>), dim3(G), dim3(NTHR), 0, s, a);
@@ -1893,9 +1900,24 @@ extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* b
   a.M = M; a.N = F; a.K = K; a.ksplit = K; a.F = F;
   a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed; a.off = offset;
-  if (persistent_enabled() && 2 * F <= BIAS_LDS / 4 && K >= 2 * BK &&
-      (size_t)M * (K > 2 * F ? K : 2 * F) * 2 < (1ull << 31))
-    return launchp<EPI_GEGLU>(a, as_stream(stream), "dna_geglu_linear_fwd");
+  if (persistent_enabled() && 2 * F <= BIAS_LDS / 4 && K >= 2 * BK && (size_t)2 * F * K * 2 < (1ull << 31)) {
+    // 32-bit byte offsets: row blocks of at most mc rows per launch (see dna_linear_fwd)
+    const size_t wide = (size_t)(K > 2 * F ? K : 2 * F) * 2;
+    const int mc = (int)(((1ull << 31) - 1) / wide / BM * BM);
+    if (mc >= BM) {
+      for (int r0 = 0; r0 < M; r0 += mc) {
+        Args c = a;
+        c.A = a.A + (size_t)r0 * K;
+        c.C = (bf16*)a.C + (size_t)r0 * 2 * F;
+        c.aux = a.aux + (size_t)r0 * F;
+        c.M = M - r0 < mc ? M - r0 : mc;
+        c.off = a.off + (uint64_t)r0 * F / 8;  // dropout groups of 8 elements, row-major
+        const int st = launchp<EPI_GEGLU>(c, as_stream(stream), "dna_geglu_linear_fwd");
+        if (st != DNA_OK) return st;
+      }
+      return DNA_OK;
+    }
+  }
   return launch<true, true, EPI_GEGLU>(a, 1, as_stream(stream), "dna_geglu_linear_fwd");
 }
 

@@ -297,12 +297,17 @@ class GeGLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, g, p, seed, off):
         _gpu(g)
-        g = g.contiguous()
-        n, F2 = g.shape
-        a = torch.empty(n, F2 // 2, device=g.device, dtype=g.dtype)
-        with _timed("geglu_fwd", n * F2 // 2 * 3 * g.element_size(), "byte"):
-            N.call("dna_geglu_fwd", g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off, a.data_ptr(),
-                   N.stream_ptr())
+        pre = getattr(g, "_dna_geglu", None)
+        if pre is not None and pre[1] == (p, seed, off):
+            a = pre[0]  # computed in the producing GEMM's epilogue (Linear, geglu=...)
+            del g._dna_geglu
+        else:
+            g = g.contiguous()
+            n, F2 = g.shape
+            a = torch.empty(n, F2 // 2, device=g.device, dtype=g.dtype)
+            with _timed("geglu_fwd", n * F2 // 2 * 3 * g.element_size(), "byte"):
+                N.call("dna_geglu_fwd", g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off, a.data_ptr(),
+                       N.stream_ptr())
         ctx.save_for_backward(g)
         ctx.cfg = (p, seed, off)
         return a
@@ -361,6 +366,24 @@ def _hip_gemm_ok(x, w_lp, n_out, k_red):
             and k_red % 64 == 0 and n_out % 8 == 0 and _gemm_impl() == "hip")
 
 
+def _geglu_fused_ok(x, w_lp):
+    F2, K = w_lp.shape
+    return (os.environ.get("DNA_GEGLU_FUSED", "1") != "0" and _hip_gemm_ok(x, w_lp, F2, K)
+            and F2 % 256 == 0 and K >= 128)
+
+
+def _hip_geglu_linear(x, w_nk, p, seed, off):
+    """g[M, 2F] = x . w^T and a[M, F] = dropout(gelu(g1) g2) (dna_geglu_linear_fwd)."""
+    x = x.contiguous()
+    M, K = x.shape
+    F2 = w_nk.shape[0]
+    g = torch.empty(M, F2, device=x.device, dtype=torch.bfloat16)
+    a = torch.empty(M, F2 // 2, device=x.device, dtype=torch.bfloat16)
+    N.call("dna_geglu_linear_fwd", x.data_ptr(), w_nk.data_ptr(), None, M, F2 // 2, K, float(p),
+           seed, off, g.data_ptr(), a.data_ptr(), N.stream_ptr())
+    return g, a
+
+
 def _hip_linear(x, w_nk, bias):
     """y[M, N] = x[M, K] . w_nk[N, K]^T (+ fp32 bias): the persistent MFMA GEMM (dna_linear_fwd)."""
     x = x.contiguous()
@@ -380,11 +403,19 @@ class Linear(torch.autograd.Function):
     folded into the flat gradient by dna_sum_slices_accum)."""
 
     @staticmethod
-    def forward(ctx, x, w, w_lp, b, w_lpt):
+    def forward(ctx, x, w, w_lp, b, w_lpt, geglu=None):
         ctx.save_for_backward(x, w_lp, w_lpt)
         ctx.weight = w
         ctx.has_b = b is not None
         flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
+        if geglu is not None and b is None and _geglu_fused_ok(x, w_lp):
+            # g = x . w^T and a = dropout(gelu(g1) g2) in one launch (the GeGLU epilogue of the
+            # persistent GEMM); `a` rides on g for the GeGLU node that follows (bit-identical to
+            # the separate dna_geglu_fwd pass, which then does not run)
+            with _timed("gemm_geglu", flops):
+                g, a = _hip_geglu_linear(x, w_lp, *geglu)
+            g._dna_geglu = (a, tuple(geglu))
+            return g
         if _hip_gemm_ok(x, w_lp, w_lp.shape[0], w_lp.shape[1]):
             with _timed("gemm_hip", flops):
                 return _hip_linear(x, w_lp, b if (b is None or b.dtype == torch.float32) else b.float())
@@ -440,7 +471,7 @@ class Linear(torch.autograd.Function):
             db = getattr(dy, "_dna_colsum", None)  # fused upstream (AlibiAttention.backward)
             if db is None:
                 db = dy.sum(0, dtype=torch.float32)
-        return dx, dw, None, db, None
+        return dx, dw, None, db, None, None
 
 
 # ------------------------------------------------------------------ weight-gradient side stream
@@ -565,5 +596,7 @@ def wgrad_accumulate(dy, x, grad):
     N.call("dna_sum_slices_accum", parts.data_ptr(), s, m * n, grad.data_ptr(), N.stream_ptr())
 
 
-def linear(x, w, w_lp, b=None, w_lpt=None):
-    return Linear.apply(x, w, w_lp if w_lp is not None else w, b, w_lpt)
+def linear(x, w, w_lp, b=None, w_lpt=None, geglu=None):
+    """geglu=(p, seed, offset): the output feeds GeGLU.apply(y, p, seed, offset) next -- fuse
+    that GeGLU forward into the GEMM epilogue when the shapes allow (DNA_GEGLU_FUSED=0: never)."""
+    return Linear.apply(x, w, w_lp if w_lp is not None else w, b, w_lpt, geglu)

@@ -538,6 +538,27 @@ def test_gemm_bench_shape_gated_fwd_and_k6144_dgrad():
     assert _rel(dx[rows], dy[rows].float() @ w.float()) < 1e-2
 
 
+def test_gemm_geglu_fused_bench_shape_row_blocks():
+    """The fused gated_layers GEMM + GeGLU forward at T = 262,144 (g is 3.2 GB: two row-block
+    launches, the dropout counter advanced per block) equals the unfused pair bit for bit: g vs
+    dna_linear_fwd, a vs dna_geglu_fwd on that g, incl. rows on both sides of the block seam."""
+    T, F, H = BENCH_T, 3072, 768
+    g0 = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn(T, H, device=DEV, generator=g0).bfloat16()
+    w = (torch.randn(2 * F, H, device=DEV, generator=g0) * 0.05).bfloat16()
+    g = torch.empty(T, 2 * F, device=DEV, dtype=torch.bfloat16)
+    a = torch.empty(T, F, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_geglu_linear_fwd", x.data_ptr(), w.data_ptr(), None, T, F, H, 0.1, 123, 77,
+               g.data_ptr(), a.data_ptr())
+    g2 = torch.empty_like(g)
+    _gemm_call("dna_linear_fwd", x.data_ptr(), w.data_ptr(), None, T, 2 * F, H, g2.data_ptr())
+    assert torch.equal(g, g2)
+    del g2
+    a2 = torch.empty_like(a)
+    _gemm_call("dna_geglu_fwd", g.data_ptr(), 1, T, F, 0.1, 123, 77, a2.data_ptr())
+    assert torch.equal(a, a2)
+
+
 @pytest.mark.parametrize("n,k", [(2304, 768), (768, 768), (6144, 768), (768, 3072)])
 def test_wgrad_p_bench_shapes(n, k):
     """dna_linear_wgrad_p (the hand-written token-major weight gradient, fp32 chunk partials +
