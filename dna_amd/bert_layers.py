@@ -291,8 +291,14 @@ class BertForMaskedLM(nn.Module):
             # the GeGLU forward runs in the gated_layers GEMM's epilogue where the kernel allows
             g = self._linear(yb if bf16 else y32, mlp.gated_layers.weight,
                              geglu=(p_hidden, seed, off))
-            a = DF.GeGLU.apply(g, p_hidden, seed, off)
-            o = self._linear(a, mlp.wo.weight)
+            wo_lp, wo_lpt = self._lp(mlp.wo.weight), self._lp_t(mlp.wo.weight)
+            if DF.geglu_out_fused_ok(g, wo_lp, wo_lpt):
+                # GeGLU + wo as one node: backward = wo's data gradient with the GeGLU backward
+                # in its epilogue (da never in memory), then wo's weight gradient
+                o = DF.geglu_out(g, p_hidden, seed, off, mlp.wo.weight, wo_lp, wo_lpt)
+            else:
+                a = DF.GeGLU.apply(g, p_hidden, seed, off)
+                o = DF.linear(a, mlp.wo.weight, wo_lp, None, w_lpt=wo_lpt)
             x32, xb = DF.FusedLayerNorm.apply(o, mlp.wo.bias, y32, mlp.layernorm.weight,
                                               mlp.layernorm.bias, eps, 0, 0.0, 0, 0, True, bf16)
             xin = xb if bf16 else x32

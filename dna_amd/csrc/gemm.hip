@@ -585,7 +585,8 @@ static_assert(pend_stores<EPI_BF16>(1, 0) == 16 && pend_stores<EPI_BF16>(1, 3) =
 // flight -- see the comment above the SCH == 1 branch
 template <int EPI, int ABL = 0, int SCH = 0>
 __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
-  static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU, "persistent kernel: bf16 / GeGLU epilogues");
+  static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU || (EPI == EPI_GEGLU_BWD && SCH == 2 && ABL == 0),
+                "persistent kernel: bf16 / GeGLU epilogues (GeGLU backward: lean body only)");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -613,7 +614,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   const int KT = a.K / BK;
   const int V = nb * KT;
   float* bias_lds = reinterpret_cast<float*>(smem + LDS_BYTES);
-  const int nbias = EPI == EPI_GEGLU ? 2 * a.F : a.N;
+  const int nbias = EPI == EPI_GEGLU ? 2 * a.F : EPI == EPI_GEGLU_BWD ? 0 : a.N;
   for (int c = tid * 4; c < nbias; c += NTHR * 4)
     *reinterpret_cast<f32x4*>(bias_lds + c) =
         a.bias ? *reinterpret_cast<const f32x4*>(a.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -714,7 +715,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   // past M fall outside the resource and are dropped
   const int cq = 4 * (lane >> 4);
   const int ldo = EPI == EPI_GEGLU ? 2 * a.F : a.ldc;
-  const auto rC = out_rsrc(a.C, (uint32_t)((size_t)a.M * ldo * 2));
+  const auto rC = out_rsrc(EPI == EPI_GEGLU_BWD ? (void*)a.aux : a.C, (uint32_t)((size_t)a.M * ldo * 2));
   const uint32_t voC = (uint32_t)(((wr * 64 + (lane & 15)) * ldo + wc * 32 + cq) * 2);
   // BF16: a quadrant (mq, nq) is final right after its MFMAs in a unit's last K-step, so it is
   // stored there (bias from LDS), overlapping the remaining phases. For each (row block i) the
@@ -1111,6 +1112,45 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
         else __builtin_amdgcn_raw_buffer_store_b128(o, rC, off, 0, 0);
       }
     };
+    // GeGLU backward (dg = geglu_bwd(da, g) with da = this GEMM's output, never stored): quadrant
+    // (mq, nq)'s saved g1 / g2 (8 columns per lane and row block, the layout after the permlane16
+    // exchange) are loaded in the phase's load half-phase, beside the fragment reads, and used
+    // after its MFMAs -- the compiler's own vmcnt waits count them against the LDS-DMA stages
+    // issued before; da is rounded to bf16 first, as the separate pass reads it
+    const auto rGi = out_rsrc(a.g, (uint32_t)((size_t)a.M * 2 * a.F * 2));
+    const uint32_t voGB = (uint32_t)(((wr * 64 + l16) * 2 * a.F + colq) * 2);
+    auto lgload = [&](const LCur& c, int mq, int nq, bf16x8 (&gv)[4][2]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
+                                        ((c.m0 + mq * 128 + i * 16) * 2 * a.F + c.n0 + nq * 128) * 2);
+        gv[i][0] = load_b128h(rGi, off);
+        gv[i][1] = load_b128h(rGi, off + a.F * 2);
+      }
+    };
+    auto lgstore = [&](const LCur& c, int mq, int nq, const bf16x8 (&gv)[4][2]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 d = __builtin_bit_cast(bf16x8, swap8(acc[mq][nq][i][0], acc[mq][nq][i][1]));
+        const int row = c.m0 + mq * 128 + i * 16;
+        const size_t e = (size_t)(row + wr * 64 + l16) * a.F + c.n0 + nq * 128 + colq;  // e % 8 == 0
+        const uint32_t keep = a.p > 0.f ? dropout_keep8(a.seed, a.off, e >> 3, a.th) : 0xFFu;
+        bf16x8 o1, o2;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float dd = (float)d[q];
+          if (a.p > 0.f) dd = ((keep >> q) & 1) ? dd * a.ks : 0.f;
+          float ge, dge;
+          gelu_erf_and_grad((float)gv[i][0][q], ge, dge);
+          o1[q] = (bf16)(dd * (float)gv[i][1][q] * dge);
+          o2[q] = (bf16)(dd * ge);
+        }
+        const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
+                                        (row * 2 * a.F + c.n0 + nq * 128) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o1), rC, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o2), rC, off + a.F * 2, 0, 0);
+      }
+    };
     auto mmaz = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1128,8 +1168,13 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     auto lwait = [&](auto phase_c, auto role_c) {
       constexpr int p = decltype(phase_c)::value, role = decltype(role_c)::value;
       // BF16: QS stores after every phase of a unit's last step; GeGLU: GS after phases 1 and 3
+      // GeGLU backward: 8 stores after every phase of the last step, each after a wait that
+      // retired everything older (its g loads are the youngest VMEM operations then)
+      constexpr int QB = 8;
       constexpr int n = EPI == EPI_BF16
                             ? (role == 0 ? 8 : role == 1 ? 8 + p * QS : 8 + (4 - p) * QS)
+                            : EPI == EPI_GEGLU_BWD
+                            ? (role == 0 ? 8 : role == 1 ? 8 + p * QB : 8 + (4 - p) * QB)
                             : (role == 0 ? 8 : role == 1 ? 8 + (p >= 2 ? GS : 0) : 8 + (p < 2 ? 2 * GS : GS));
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(n));
     };
@@ -1138,6 +1183,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       __builtin_amdgcn_sched_barrier(0);
     };
     constexpr bool SB = EPI == EPI_BF16;  // per-quadrant stores (else GeGLU halves)
+    constexpr bool GB = EPI == EPI_GEGLU_BWD;  // per-quadrant GeGLU-backward epilogue
     // one K-step k of the current unit in buffer parity par; ZI: the unit's first K-step (MFMA
     // chains start from zero)
     auto lstep = [&](auto par_c, auto role_c, auto zi_c, int k, const LCur& cur, const LCur& nxt) {
@@ -1150,46 +1196,55 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
         else mma(mq, nq, bf);
       };
       f32x4 bj0, bj1;
+      bf16x8 gv[4][2];
       // phase 0: quadrant (0,0)
       lstage(cur, nxt, k + 1, Qc{}, I3{});
       lwait(I0{}, role_c);
       lreadA(Pc{}, I0{});
       lreadB(Pc{}, I0{}, bf0);
       if constexpr (SB && role == 1) lbias(cur, 0, bj0, bj1);
+      if constexpr (GB && role == 1) lgload(cur, 0, 0, gv);
       DNA_BARRIER();
       lgkm0();
       mm(0, 0, bf0);
       if constexpr (SB && role == 1) lstore(cur, 0, 0, bj0, bj1);
+      if constexpr (GB && role == 1) lgstore(cur, 0, 0, gv);
       DNA_BARRIER();
       // phase 1: quadrant (0,1)
       lstage(cur, nxt, k + 1, Qc{}, I1{});
       lwait(I1{}, role_c);
       lreadB(Pc{}, I1{}, bf1);
       if constexpr (SB && role == 1) lbias(cur, 1, bj0, bj1);
+      if constexpr (GB && role == 1) lgload(cur, 0, 1, gv);
       DNA_BARRIER();
       lgkm0();
       mm(0, 1, bf1);
       if constexpr (SB && role == 1) lstore(cur, 0, 1, bj0, bj1);
-      if constexpr (!SB && role == 1) store_geglu_half(cur, 0);
+      if constexpr (GB && role == 1) lgstore(cur, 0, 1, gv);
+      if constexpr (!SB && !GB && role == 1) store_geglu_half(cur, 0);
       DNA_BARRIER();
       // phase 2: quadrant (1,1)
       lstage(cur, nxt, k + 2, Pc{}, I0{});
       lwait(I2{}, role_c);
       lreadA(Pc{}, I1{});
+      if constexpr (GB && role == 1) lgload(cur, 1, 1, gv);
       DNA_BARRIER();
       lgkm0();
       mm(1, 1, bf1);
       if constexpr (SB && role == 1) lstore(cur, 1, 1, bj0, bj1);
+      if constexpr (GB && role == 1) lgstore(cur, 1, 1, gv);
       DNA_BARRIER();
       // phase 3: quadrant (1,0)
       lstage(cur, nxt, k + 2, Pc{}, I2{});
       lwait(I3{}, role_c);
       if constexpr (SB && role == 1) lbias(cur, 0, bj0, bj1);
+      if constexpr (GB && role == 1) lgload(cur, 1, 0, gv);
       DNA_BARRIER();
       if constexpr (SB && role == 1) lgkm0();
       mm(1, 0, bf0);
       if constexpr (SB && role == 1) lstore(cur, 1, 0, bj0, bj1);
-      if constexpr (!SB && role == 1) store_geglu_half(cur, 1);
+      if constexpr (GB && role == 1) lgstore(cur, 1, 0, gv);
+      if constexpr (!SB && !GB && role == 1) store_geglu_half(cur, 1);
       DNA_BARRIER();
     };
     using ZN = std::false_type;
@@ -1936,6 +1991,48 @@ extern "C" int dna_geglu_linear_dgrad(const void* dy, const void* w, const void*
   a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed; a.off = offset;
   return launch<true, false, EPI_GEGLU_BWD>(a, 1, as_stream(stream), "dna_geglu_linear_dgrad");
+}
+
+// dg[M, 2F] = geglu_bwd(dy[M, N] . Wt[F, N]^T, g) on the persistent kernel: the data gradient of
+// `wo` through its transposed bf16 copy (both operands K-major, as dna_linear_fwd's dgrad use),
+// with the GeGLU backward of bert_layers.py:292-296 in the epilogue; da never reaches memory.
+// Row blocks past 2^31-byte operands as dna_geglu_linear_fwd (dropout offset advanced per block).
+extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const void* g, int M, int F,
+                                        int N, float p_drop, uint64_t seed, uint64_t offset,
+                                        void* dg, void* stream) {
+  DNA_CHECK_ARG(dy && wt && g && dg, "dna_geglu_linear_dgrad_p: null pointer");
+  DNA_CHECK_ARG(M >= 0 && N % BK == 0 && (N / BK) % 2 == 0 && N >= 2 * BK && F % BN == 0,
+                "dna_geglu_linear_dgrad_p: hidden %% 128 and F %% 256 required (N=%d F=%d)", N, F);
+  DNA_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "dna_geglu_linear_dgrad_p: bad p");
+  DNA_CHECK_ARG((size_t)F * N * 2 < (1ull << 31), "dna_geglu_linear_dgrad_p: weight too large");
+  if (M == 0) return DNA_OK;
+  Args a = base_args();
+  a.A = (const bf16*)dy; a.lda = N;
+  a.B = (const bf16*)wt; a.ldb = N;
+  a.C = nullptr; a.ldc = 2 * F; a.g = (const bf16*)g; a.aux = (bf16*)dg;
+  a.N = F; a.K = N; a.ksplit = N; a.F = F;
+  a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
+  a.seed = seed;
+  a.tilesN = F / BN;
+  a.GM = 8;
+  if (const char* e = getenv("DNA_GEMM_GM")) a.GM = atoi(e);
+  const size_t wide = (size_t)(N > 2 * F ? N : 2 * F) * 2;
+  const int mc = (int)(((1ull << 31) - 1) / wide / BM * BM);
+  for (int r0 = 0; r0 < M; r0 += mc) {
+    Args c = a;
+    c.A = a.A + (size_t)r0 * N;
+    c.g = a.g + (size_t)r0 * 2 * F;
+    c.aux = a.aux + (size_t)r0 * 2 * F;
+    c.M = M - r0 < mc ? M - r0 : mc;
+    c.off = offset + (uint64_t)r0 * F / 8;  // dropout groups of 8 elements, row-major
+    c.tilesM = (c.M + BM - 1) / BM;
+    const int U = c.tilesM * c.tilesN;
+    int G = num_cus();
+    G = U < G ? U : (G & ~7);
+    hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 0, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
+    DNA_LAUNCH_CHECK("dna_geglu_linear_dgrad_p");
+  }
+  return DNA_OK;
 }
 
 extern "C" int dna_linear_wgrad_p_splits(int M, int N, int K) {

@@ -291,23 +291,28 @@ def alibi_attention(qkv, key_valid, slopes, b, S, H, scale=None, bias_grad=False
 
 
 # ----------------------------------------------------------------------------------- GeGLU
+def _geglu_forward(g, p, seed, off):
+    pre = getattr(g, "_dna_geglu", None)
+    if pre is not None and pre[1] == (p, seed, off):
+        a = pre[0]  # computed in the producing GEMM's epilogue (Linear, geglu=...)
+        del g._dna_geglu
+        return a
+    g = g.contiguous()
+    n, F2 = g.shape
+    a = torch.empty(n, F2 // 2, device=g.device, dtype=g.dtype)
+    with _timed("geglu_fwd", n * F2 // 2 * 3 * g.element_size(), "byte"):
+        N.call("dna_geglu_fwd", g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off, a.data_ptr(),
+               N.stream_ptr())
+    return a
+
+
 class GeGLU(torch.autograd.Function):
     """dropout(gelu(g[:, :F]) * g[:, F:])   (bert_layers.py:292-296)."""
 
     @staticmethod
     def forward(ctx, g, p, seed, off):
         _gpu(g)
-        pre = getattr(g, "_dna_geglu", None)
-        if pre is not None and pre[1] == (p, seed, off):
-            a = pre[0]  # computed in the producing GEMM's epilogue (Linear, geglu=...)
-            del g._dna_geglu
-        else:
-            g = g.contiguous()
-            n, F2 = g.shape
-            a = torch.empty(n, F2 // 2, device=g.device, dtype=g.dtype)
-            with _timed("geglu_fwd", n * F2 // 2 * 3 * g.element_size(), "byte"):
-                N.call("dna_geglu_fwd", g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off, a.data_ptr(),
-                       N.stream_ptr())
+        a = _geglu_forward(g, p, seed, off)
         ctx.save_for_backward(g)
         ctx.cfg = (p, seed, off)
         return a
@@ -440,32 +445,7 @@ class Linear(torch.autograd.Function):
             else:
                 with _timed("gemm", flops):
                     dx = torch.mm(dy, w_lp)
-        w = ctx.weight
-        direct = getattr(w, "_dna_direct", False) and w.grad is not None and x.dtype != torch.float32
-        side = _side_stream() if direct else None
-        if side is not None:
-            # wgrad beside the rest of the backward; dy / x must outlive it on the side stream
-            side.wait_stream(torch.cuda.current_stream())
-            _KEEP.append((dy, x))  # (record_stream instead made the allocator thrash)
-            with torch.cuda.stream(side), _timed("gemm_wgrad", flops):
-                wgrad_accumulate(dy, x, w.grad)
-            _queue_join()
-            notify = getattr(w, "_dna_notify", None)
-            if notify is not None:
-                notify(w)
-            dw = None
-        else:
-          with _timed("gemm_wgrad", flops):
-            if direct:
-                # write straight into the flat fp32 gradient buffer (dna_amd.flat) and tell the
-                # gradient-bucket reducer, instead of returning dW to AccumulateGrad
-                wgrad_accumulate(dy, x, w.grad)
-                notify = getattr(w, "_dna_notify", None)
-                if notify is not None:
-                    notify(w)
-                dw = None
-            else:
-                dw = wgrad(dy, x)
+        dw = _weight_grad(ctx.weight, dy, x, flops)
         db = None
         if ctx.has_b:
             db = getattr(dy, "_dna_colsum", None)  # fused upstream (AlibiAttention.backward)
@@ -594,6 +574,85 @@ def wgrad_accumulate(dy, x, grad):
         parts = torch.bmm(dy.view(s, rows // s, m).transpose(1, 2), x.view(s, rows // s, n),
                           out_dtype=torch.float32)
     N.call("dna_sum_slices_accum", parts.data_ptr(), s, m * n, grad.data_ptr(), N.stream_ptr())
+
+
+def _weight_grad(w, dy, x, flops):
+    """dW = dy^T x of the projection with fp32 master weight w: straight into the flat gradient
+    buffer when a FlatParams owns w (None returned, bucket reducer notified), else returned."""
+    direct = getattr(w, "_dna_direct", False) and w.grad is not None and x.dtype != torch.float32
+    side = _side_stream() if direct else None
+    if side is not None:
+        # wgrad beside the rest of the backward; dy / x must outlive it on the side stream
+        side.wait_stream(torch.cuda.current_stream())
+        _KEEP.append((dy, x))  # (record_stream instead made the allocator thrash)
+        with torch.cuda.stream(side), _timed("gemm_wgrad", flops):
+            wgrad_accumulate(dy, x, w.grad)
+        _queue_join()
+        notify = getattr(w, "_dna_notify", None)
+        if notify is not None:
+            notify(w)
+        return None
+    with _timed("gemm_wgrad", flops):
+        if direct:
+            # write straight into the flat fp32 gradient buffer (dna_amd.flat) and tell the
+            # gradient-bucket reducer, instead of returning dW to AccumulateGrad
+            wgrad_accumulate(dy, x, w.grad)
+            notify = getattr(w, "_dna_notify", None)
+            if notify is not None:
+                notify(w)
+            return None
+        return wgrad(dy, x)
+
+
+def geglu_out_fused_ok(g, w_lp, w_lpt):
+    """GeGLUOut applies: bf16 path, the transposed wo copy present, kernel-legal shapes
+    (hidden % 128, F % 256), DNA_GEGLU_BWD_FUSED not 0."""
+    if w_lpt is None or os.environ.get("DNA_GEGLU_BWD_FUSED", "1") == "0":
+        return False
+    Nh, F = w_lp.shape
+    return (g.dtype == torch.bfloat16 and _hip_gemm_ok(g, w_lp, Nh, F) and w_lpt.shape == (F, Nh)
+            and g.shape[1] == 2 * F and Nh % 128 == 0 and F % 256 == 0)
+
+
+class GeGLUOut(torch.autograd.Function):
+    """o = dropout(gelu(g[:, :F]) * g[:, F:]) . wo^T  (bert_layers.py:292-297, the bias going to
+    the LayerNorm that follows) as ONE autograd node, so its backward runs the data gradient of
+    wo and the GeGLU backward in one launch (dna_geglu_linear_dgrad_p: dg straight from dy, da
+    never in memory) beside wo's weight gradient. Forward: the GeGLU output `a` from the
+    gated_layers epilogue (Linear, geglu=...) or the separate pass, then the persistent GEMM."""
+
+    @staticmethod
+    def forward(ctx, g, p, seed, off, w, w_lp, w_lpt):
+        _gpu(g)
+        g = g.contiguous()
+        a = _geglu_forward(g, p, seed, off)  # the same `a` (fused epilogue or dna_geglu_fwd)
+        n, F2 = g.shape
+        flops = 2.0 * n * w_lp.shape[0] * w_lp.shape[1]
+        with _timed("gemm_hip", flops):
+            o = _hip_linear(a, w_lp, None)
+        ctx.save_for_backward(g, a, w_lpt)
+        ctx.weight = w
+        ctx.cfg = (p, seed, off)
+        return o
+
+    @staticmethod
+    def backward(ctx, dy):
+        g, a, w_lpt = ctx.saved_tensors
+        p, seed, off = ctx.cfg
+        dy = dy.contiguous()
+        n, F2 = g.shape
+        Nh = dy.shape[1]
+        flops = 2.0 * n * Nh * (F2 // 2)
+        dg = torch.empty_like(g)
+        with _timed("gemm_geglu_bwd", flops):
+            N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), w_lpt.data_ptr(), g.data_ptr(), n,
+                   F2 // 2, Nh, float(p), seed, off, dg.data_ptr(), N.stream_ptr())
+        dw = _weight_grad(ctx.weight, dy, a, flops)
+        return dg, None, None, None, dw, None, None
+
+
+def geglu_out(g, p, seed, off, w, w_lp, w_lpt):
+    return GeGLUOut.apply(g, p, seed, off, w, w_lp, w_lpt)
 
 
 def linear(x, w, w_lp, b=None, w_lpt=None, geglu=None):

@@ -226,6 +226,12 @@ int dna_geglu_linear_fwd(const void* x, const void* wg, const float* bias, int M
  * dg[M, 2F] = dna_geglu_bwd(da, g). N % 64 == 0, F % 8 == 0. */
 int dna_geglu_linear_dgrad(const void* dy, const void* wo, const void* g, int M, int F, int N,
                            float p_drop, uint64_t seed, uint64_t offset, void* dg, void* stream);
+/* The same on the persistent kernel (the training step's path), with wo's transposed bf16 copy
+ * wt [F, N] (dna_transpose_bf16) as the K-major operand: dg[M, 2F] = dna_geglu_bwd(dy . wt^T, g);
+ * da never reaches memory. N % 128 == 0, F % 256 == 0. Replaces the backward of wo's nn.Linear
+ * and of the GeGLU (bert_layers.py:292-297). */
+int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const void* g, int M, int F, int N,
+                             float p_drop, uint64_t seed, uint64_t offset, void* dg, void* stream);
 
 /* ------------------------------------------------------------------ HyenaDNA FFT long convolution
  * fftconv_ref (src/models/sequence/hyena.py:60-92) as used by HyenaFilter.forward (:253-280):

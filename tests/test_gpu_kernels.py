@@ -559,6 +559,68 @@ def test_gemm_geglu_fused_bench_shape_row_blocks():
     assert torch.equal(a, a2)
 
 
+def _geglu_dgrad_pair(dy, wt, g, M, F, H, p, seed, off):
+    """The unfused pair the fused kernel replaces: da = dy . wt^T (dna_linear_fwd, the dgrad
+    through the transposed copy), then dg = dna_geglu_bwd(da, g)."""
+    da = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, M, F, H, da.data_ptr())
+    dg = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, M, F, p, seed, off, dg.data_ptr())
+    return dg
+
+
+@pytest.mark.parametrize("M", [1, 257, 1000, 4096])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_geglu_dgrad_p_equals_pair_and_writes_nothing_past_m(M, p):
+    """wo's data gradient with the GeGLU backward in the persistent kernel's epilogue
+    (dna_geglu_linear_dgrad_p) equals the separate pair bit for bit, dropout on or off; the
+    output is the head of a NaN-filled buffer and g's rows past M are NaN: rows past M read as
+    zero and are never written."""
+    F, H = 3072, 768
+    gen = torch.Generator(device="cpu").manual_seed(M + int(p * 10))
+    dy = torch.randn(M, H, generator=gen).to(DEV).bfloat16()
+    wt = (torch.randn(F, H, generator=gen) * 0.05).to(DEV).bfloat16()
+    gb = torch.full((M + 256, 2 * F), float("nan"), device=DEV, dtype=torch.bfloat16)
+    gb[:M] = torch.randn(M, 2 * F, generator=gen).to(DEV).bfloat16()
+    g = gb[:M]
+    dgb = torch.full((M + 256, 2 * F), float("nan"), device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), M, F, H, p,
+               91, 13, dgb.data_ptr())
+    torch.cuda.synchronize()
+    ref = _geglu_dgrad_pair(dy, wt, g, M, F, H, p, 91, 13)
+    assert torch.equal(dgb[:M], ref)
+    assert torch.isnan(dgb[M:]).all()
+
+
+def test_gemm_geglu_dgrad_p_bench_shape_row_blocks():
+    """The fused wo dgrad + GeGLU backward at T = 262,144 (g / dg are 3.2 GB: two row-block
+    launches, the dropout counter advanced per block) equals the separate pair bit for bit,
+    incl. the rows on both sides of the block seam, and matches fp32 torch on sampled rows."""
+    T, F, H = BENCH_T, 3072, 768
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    dy = torch.randn(T, H, device=DEV, generator=gen).bfloat16()
+    wt = (torch.randn(F, H, device=DEV, generator=gen) * 0.05).bfloat16()
+    g = torch.randn(T, 2 * F, device=DEV, generator=gen).bfloat16()
+    dg = torch.empty_like(g)
+    _gemm_call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), T, F, H,
+               0.1, 321, 9, dg.data_ptr())
+    ref = _geglu_dgrad_pair(dy, wt, g, T, F, H, 0.1, 321, 9)
+    assert torch.equal(dg, ref)
+    del ref
+    # fp32 restatement on sampled rows, dropout off (bf16 da rounding as the reference's bf16 step)
+    _gemm_call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), T, F, H,
+               0.0, 0, 0, dg.data_ptr())
+    mc = ((1 << 31) - 1) // (2 * F * 2) // 256 * 256
+    rows = torch.cat([_sample_rows(T), torch.tensor([mc - 1, mc, mc + 1], device=DEV)])
+    da = dy[rows].float() @ wt.float().t()
+    g1, g2 = g[rows, :F].float(), g[rows, F:].float()
+    cdf = 0.5 * (1 + torch.erf(g1 / math.sqrt(2)))
+    gelu = g1 * cdf
+    dgelu = cdf + g1 * torch.exp(-0.5 * g1 * g1) / math.sqrt(2 * math.pi)
+    want = torch.cat([da * g2 * dgelu, da * gelu], 1)
+    assert _rel(dg[rows], want) < 1e-2
+
+
 @pytest.mark.parametrize("n,k", [(2304, 768), (768, 768), (6144, 768), (768, 3072)])
 def test_wgrad_p_bench_shapes(n, k):
     """dna_linear_wgrad_p (the hand-written token-major weight gradient, fp32 chunk partials +

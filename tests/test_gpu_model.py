@@ -195,6 +195,32 @@ def test_geglu_fused_into_gemm_same_step(monkeypatch, tag):
     assert torch.equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize("tag", ["cfgA", "117m"])
+def test_geglu_bwd_fused_into_wo_dgrad_same_step(monkeypatch, tag):
+    """GeGLU + wo as one autograd node whose backward runs wo's data gradient with the GeGLU
+    backward in the epilogue (default) vs the separate Linear + GeGLU nodes
+    (DNA_GEGLU_BWD_FUSED=0): bit-identical loss and flat gradients, training mode with dropout."""
+    from dna_amd.bert_layers import BertForMaskedLM, MLMIndex
+    from dna_amd.flat import FlatParams
+    z, cfg = _golden(tag)
+    ids, mask, labels = _batch(z)
+    idx = MLMIndex.build(ids, labels)
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DNA_GEGLU_BWD_FUSED", fused)
+        torch.manual_seed(0)
+        m = BertForMaskedLM(cfg, precision="bf16").to(DEV).train()
+        flat = FlatParams(m, DEV)
+        flat.enable_direct_grad(True)
+        flat.zero_grad()
+        loss, _ = m.mlm_loss(ids, mask, idx)
+        loss.backward()
+        torch.cuda.synchronize()
+        out.append((loss.detach().clone(), flat.grad.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
 def test_wgrad_side_stream_same_gradients(monkeypatch):
     """DNA_WGRAD_STREAM=1 (weight gradients on a side stream, joined at the end of backward) gives
     bit-identical flat gradients to the single-stream path (same kernels, same split-K order)."""
