@@ -1118,13 +1118,19 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     // after its MFMAs -- the compiler's own vmcnt waits count them against the LDS-DMA stages
     // issued before; da is rounded to bf16 first, as the separate pass reads it
     const auto rGi = out_rsrc(a.g, (uint32_t)((size_t)a.M * 2 * a.F * 2));
-    const uint32_t voGB = (uint32_t)(((wr * 64 + l16) * 2 * a.F + colq) * 2);
+    // g / dg rows are 2F wide = a.ldc (launcher), so the lane offset is voQ's (no extra VGPR)
+    const uint32_t voGB = voQ;
     auto lgload = [&](const LCur& c, int mq, int nq, bf16x8 (&gv)[4][2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
                                         ((c.m0 + mq * 128 + i * 16) * 2 * a.F + c.n0 + nq * 128) * 2);
         gv[i][0] = load_b128h(rGi, off);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
+                                        ((c.m0 + mq * 128 + i * 16) * 2 * a.F + c.n0 + nq * 128) * 2);
         gv[i][1] = load_b128h(rGi, off + a.F * 2);
       }
     };
@@ -1133,8 +1139,10 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       for (int i = 0; i < 4; ++i) {
         const bf16x8 d = __builtin_bit_cast(bf16x8, swap8(acc[mq][nq][i][0], acc[mq][nq][i][1]));
         const int row = c.m0 + mq * 128 + i * 16;
-        const size_t e = (size_t)(row + wr * 64 + l16) * a.F + c.n0 + nq * 128 + colq;  // e % 8 == 0
-        const uint32_t keep = a.p > 0.f ? dropout_keep8(a.seed, a.off, e >> 3, a.th) : 0xFFu;
+        // element index within the launch's row block (< 2^31: the launcher's row blocks keep
+        // M * 2F * 2 bytes below 2^31); e % 8 == 0
+        const uint32_t e = (uint32_t)(row + wr * 64 + l16) * (uint32_t)a.F + (uint32_t)(c.n0 + nq * 128 + colq);
+        const uint32_t keep = a.p > 0.f ? dropout_keep8(a.seed, a.off, (uint64_t)(e >> 3), a.th) : 0xFFu;
         bf16x8 o1, o2;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -1168,13 +1176,14 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     auto lwait = [&](auto phase_c, auto role_c) {
       constexpr int p = decltype(phase_c)::value, role = decltype(role_c)::value;
       // BF16: QS stores after every phase of a unit's last step; GeGLU: GS after phases 1 and 3
-      // GeGLU backward: 8 stores after every phase of the last step, each after a wait that
-      // retired everything older (its g loads are the youngest VMEM operations then)
+      // GeGLU backward: each phase of the last step issues its quadrant's 8 g loads before its
+      // stage (they stay in flight through the wait: + 8) and 8 stores after its MFMAs, each
+      // group after an epilogue wait that retired everything older than its g loads
       constexpr int QB = 8;
       constexpr int n = EPI == EPI_BF16
                             ? (role == 0 ? 8 : role == 1 ? 8 + p * QS : 8 + (4 - p) * QS)
                             : EPI == EPI_GEGLU_BWD
-                            ? (role == 0 ? 8 : role == 1 ? 8 + p * QB : 8 + (4 - p) * QB)
+                            ? (role == 0 ? 8 : role == 1 ? 16 + p * QB : 8 + (4 - p) * QB)
                             : (role == 0 ? 8 : role == 1 ? 8 + (p >= 2 ? GS : 0) : 8 + (p < 2 ? 2 * GS : GS));
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(n));
     };
@@ -1198,12 +1207,12 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       f32x4 bj0, bj1;
       bf16x8 gv[4][2];
       // phase 0: quadrant (0,0)
+      if constexpr (GB && role == 1) lgload(cur, 0, 0, gv);
       lstage(cur, nxt, k + 1, Qc{}, I3{});
       lwait(I0{}, role_c);
       lreadA(Pc{}, I0{});
       lreadB(Pc{}, I0{}, bf0);
       if constexpr (SB && role == 1) lbias(cur, 0, bj0, bj1);
-      if constexpr (GB && role == 1) lgload(cur, 0, 0, gv);
       DNA_BARRIER();
       lgkm0();
       mm(0, 0, bf0);
@@ -1211,11 +1220,11 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       if constexpr (GB && role == 1) lgstore(cur, 0, 0, gv);
       DNA_BARRIER();
       // phase 1: quadrant (0,1)
+      if constexpr (GB && role == 1) lgload(cur, 0, 1, gv);
       lstage(cur, nxt, k + 1, Qc{}, I1{});
       lwait(I1{}, role_c);
       lreadB(Pc{}, I1{}, bf1);
       if constexpr (SB && role == 1) lbias(cur, 1, bj0, bj1);
-      if constexpr (GB && role == 1) lgload(cur, 0, 1, gv);
       DNA_BARRIER();
       lgkm0();
       mm(0, 1, bf1);
@@ -1224,10 +1233,10 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       if constexpr (!SB && !GB && role == 1) store_geglu_half(cur, 0);
       DNA_BARRIER();
       // phase 2: quadrant (1,1)
+      if constexpr (GB && role == 1) lgload(cur, 1, 1, gv);
       lstage(cur, nxt, k + 2, Pc{}, I0{});
       lwait(I2{}, role_c);
       lreadA(Pc{}, I1{});
-      if constexpr (GB && role == 1) lgload(cur, 1, 1, gv);
       DNA_BARRIER();
       lgkm0();
       mm(1, 1, bf1);
@@ -1235,10 +1244,10 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       if constexpr (GB && role == 1) lgstore(cur, 1, 1, gv);
       DNA_BARRIER();
       // phase 3: quadrant (1,0)
+      if constexpr (GB && role == 1) lgload(cur, 1, 0, gv);
       lstage(cur, nxt, k + 2, Pc{}, I2{});
       lwait(I3{}, role_c);
       if constexpr (SB && role == 1) lbias(cur, 0, bj0, bj1);
-      if constexpr (GB && role == 1) lgload(cur, 1, 0, gv);
       DNA_BARRIER();
       if constexpr (SB && role == 1) lgkm0();
       mm(1, 0, bf0);

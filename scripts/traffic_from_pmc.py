@@ -19,11 +19,13 @@ import sys
 # family -> (regex selecting its kernels, regex selecting the one kernel counted per op launch)
 FAMILIES = {
     # csrc/gemm.hip: EPI 0 = bf16 epilogue (forward / data gradient), EPI 2 = the GeGLU epilogue
-    # of the fused gated_layers GEMM (its own op family, gemm_geglu)
+    # of the fused gated_layers GEMM (its own op family, gemm_geglu), EPI 3 = gemm_geglu_bwd
     "gemm_hip": (r"gemmp_kernel<0|gemm_kernel<(true|false), (true|false), 0|gemmp_kernelILi0|gemm_kernelILb[01]ELb[01]ELi0",
                  r"gemmp_kernel<0|gemm_kernel<(true|false), (true|false), 0|gemmp_kernelILi0|gemm_kernelILb[01]ELb[01]ELi0"),
     "gemm_geglu": (r"gemmp_kernel<2|gemmp_kernelILi2|gemm_kernel<true, true, 2|gemm_kernelILb1ELb1ELi2",
                    r"gemmp_kernel<2|gemmp_kernelILi2|gemm_kernel<true, true, 2|gemm_kernelILb1ELb1ELi2"),
+    # EPI 3: wo's data gradient with the GeGLU backward in the epilogue (GeGLUOut)
+    "gemm_geglu_bwd": (r"gemmp_kernel<3|gemmp_kernelILi3", r"gemmp_kernel<3|gemmp_kernelILi3"),
     "gemm_wgrad": (r"Cijk_|sum_slices_kernel|wgradp_kernel", r"Cijk_|wgradp_kernel"),
     "attn_fwd": (r"attn::fwd2?_bf16_kernel|attn4fwd_bf16|attn16fwd2_bf16",
                  r"attn::fwd2?_bf16_kernel|attn4fwd_bf16|attn16fwd2_bf16"),
