@@ -47,10 +47,13 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 struct Philox {
   __device__ __forceinline__ static uint4 gen(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1) {
+    // each round's two 32x32 -> 64-bit products as one 64-bit multiply apiece (the pair
+    // v_mul_hi_u32 + v_mul_lo_u32 per product otherwise; same bits either way)
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-      uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-      uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+      const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+      const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+      const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
       uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
       c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
       k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;

@@ -21,20 +21,25 @@ def main():
     da = torch.empty(T, F, device="cuda", dtype=torch.bfloat16)
     s = N.stream_ptr()
 
+    pdrop = float(os.environ.get("P", "0.1"))
+
     def fused():
-        N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), T, F, H, 0.1,
+        N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), T, F, H, pdrop,
                7, 0, dg.data_ptr(), s)
+
+    def gemm():  # the same GEMM with the plain bf16 epilogue (da stored, no GeGLU)
+        N.call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, T, F, H, da.data_ptr(), s)
 
     def pair():
         N.call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, T, F, H, da.data_ptr(), s)
-        N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, T, F, 0.1, 7, 0, dg.data_ptr(), s)
+        N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, T, F, pdrop, 7, 0, dg.data_ptr(), s)
 
     variants = [v for v in os.environ.get("VARS", "2").split(",") if v]
     iters = int(os.environ.get("ITERS", "20"))
     for rnd in range(int(os.environ.get("ROUNDS", "3"))):
-        for v in variants + ["pair"]:
-            fn = pair if v == "pair" else fused
-            if v != "pair":
+        for v in variants + ["pair", "gemm"]:
+            fn = {"pair": pair, "gemm": gemm}.get(v, fused)
+            if v not in ("pair", "gemm"):
                 os.environ["DNA_GEGLU_BWD_VAR"] = v
             for _ in range(3):
                 fn()
@@ -46,7 +51,7 @@ def main():
             b.record()
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / iters
-            print(json.dumps({"variant": v, "round": rnd, "ms": round(ms, 4),
+            print(json.dumps({"variant": v, "p": pdrop, "round": rnd, "ms": round(ms, 4),
                               "tflops": round(2 * T * F * H / ms / 1e9, 1),
                               "hbm_gbs_min_bytes": round((T * H * 2 + 4 * T * F * 2) / ms / 1e6, 1)}),
                   flush=True)
