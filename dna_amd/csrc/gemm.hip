@@ -585,7 +585,8 @@ static_assert(pend_stores<EPI_BF16>(1, 0) == 16 && pend_stores<EPI_BF16>(1, 3) =
 // flight -- see the comment above the SCH == 1 branch
 template <int EPI, int ABL = 0, int SCH = 0>
 __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
-  static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU || (EPI == EPI_GEGLU_BWD && SCH == 2 && ABL == 0),
+  static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU ||
+                    (EPI == EPI_GEGLU_BWD && SCH == 2 && (ABL == 0 || ABL == 64 || ABL == 128)),
                 "persistent kernel: bf16 / GeGLU epilogues (GeGLU backward: lean body only)");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1125,13 +1126,13 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       for (int i = 0; i < 4; ++i) {
         const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
                                         ((c.m0 + mq * 128 + i * 16) * 2 * a.F + c.n0 + nq * 128) * 2);
-        gv[i][0] = load_b128h(rGi, off);
+        gv[i][0] = load_b128h(rGi, (ABL & 128) ? kOOB : off);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
                                         ((c.m0 + mq * 128 + i * 16) * 2 * a.F + c.n0 + nq * 128) * 2);
-        gv[i][1] = load_b128h(rGi, off + a.F * 2);
+        gv[i][1] = load_b128h(rGi, (ABL & 128) ? kOOB : off + a.F * 2);
       }
     };
     auto lgstore = [&](const LCur& c, int mq, int nq, const bf16x8 (&gv)[4][2]) __attribute__((always_inline)) {
@@ -1144,6 +1145,13 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
         const uint32_t e = (uint32_t)(row + wr * 64 + l16) * (uint32_t)a.F + (uint32_t)(c.n0 + nq * 128 + colq);
         const uint32_t keep = a.p > 0.f ? dropout_keep8(a.seed, a.off, (uint64_t)(e >> 3), a.th) : 0xFFu;
         bf16x8 o1, o2;
+        if constexpr ((ABL & 64) != 0) {  // diagnostics (timing only): no GeGLU math
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            o1[q] = (bf16)((float)d[q] * (float)gv[i][1][q]);
+            o2[q] = (bf16)((float)d[q] * (float)gv[i][0][q]);
+          }
+        } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           float dd = (float)d[q];
@@ -1152,6 +1160,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
           gelu_erf_and_grad((float)gv[i][0][q], ge, dge);
           o1[q] = (bf16)(dd * (float)gv[i][1][q] * dge);
           o2[q] = (bf16)(dd * ge);
+        }
         }
         const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
                                         (row * 2 * a.F + c.n0 + nq * 128) * 2);
@@ -2020,6 +2029,10 @@ extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const vo
   a.B = (const bf16*)wt; a.ldb = N;
   a.C = nullptr; a.ldc = 2 * F; a.g = (const bf16*)g; a.aux = (bf16*)dg;
   a.N = F; a.K = N; a.ksplit = N; a.F = F;
+  // DNA_GEMM_ABL (timing-only diagnostics, results invalid): 64 = epilogue without the GeGLU
+  // math (g loads + dg stores), 128 = without the g loads (math on zeros)
+  const char* ab = getenv("DNA_GEMM_ABL");
+  const int abl = ab ? atoi(ab) : 0;
   a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed;
   a.tilesN = F / BN;
@@ -2038,7 +2051,9 @@ extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const vo
     const int U = c.tilesM * c.tilesN;
     int G = num_cus();
     G = U < G ? U : (G & ~7);
-    hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 0, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
+    if (abl == 64) hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 64, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
+    else if (abl == 128) hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 128, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
+    else hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 0, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
     DNA_LAUNCH_CHECK("dna_geglu_linear_dgrad_p");
   }
   return DNA_OK;

@@ -34,13 +34,17 @@ def main():
         N.call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, T, F, H, da.data_ptr(), s)
         N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, T, F, pdrop, 7, 0, dg.data_ptr(), s)
 
-    variants = [v for v in os.environ.get("VARS", "2").split(",") if v]
+    variants = [v for v in os.environ.get("VARS", "0").split(",") if v]
     iters = int(os.environ.get("ITERS", "20"))
     for rnd in range(int(os.environ.get("ROUNDS", "3"))):
         for v in variants + ["pair", "gemm"]:
             fn = {"pair": pair, "gemm": gemm}.get(v, fused)
-            if v not in ("pair", "gemm"):
-                os.environ["DNA_GEGLU_BWD_VAR"] = v
+            os.environ["DNA_GEMM_ABL"] = "0"
+            os.environ["DNA_GEGLU_BWD_SCHED"] = "2"
+            if v.startswith("s"):  # s4: the deferred-epilogue schedule
+                os.environ["DNA_GEGLU_BWD_SCHED"] = v[1:]
+            elif v not in ("pair", "gemm"):
+                os.environ["DNA_GEMM_ABL"] = v  # 0 = the real kernel, 64 / 128 diagnostics
             for _ in range(3):
                 fn()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
