@@ -1884,6 +1884,16 @@ inline int wgrad_chunks(int tiles, int KTtot, int G, double nk) {
   return best;
 }
 
+// Row-block size for an operand past 32-bit byte offsets: the fewest blocks of at most `cap` rows
+// (cap a multiple of the 256-row tile), split as evenly as the tile allows -- so every launch
+// gets about the same unit count (a max-size-first split left the K = 6144 data gradient's second
+// launch 4.01 rounds of units: a fifth round with 2 units, ~0.1 ms of idle chip per call)
+inline int row_block(int M, int cap) {
+  const int nblk = (M + cap - 1) / cap;
+  const int per = (M + nblk - 1) / nblk;
+  return (per + BM - 1) / BM * BM;
+}
+
 inline Args base_args() {
   Args a{};
   a.GM = 4;
@@ -1913,8 +1923,9 @@ extern "C" int dna_linear_fwd(const void* x, const void* w, const float* bias, i
     // mc rows (a multiple of the 256-row tile) per launch, so e.g. T = 262,144 tokens (b = 512)
     // at N = 6144 runs as two launches of the b = 256 shape instead of the non-persistent kernel
     const size_t wide = (size_t)(K > N ? K : N) * 2;
-    const int mc = (int)(((1ull << 31) - 1) / wide / BM * BM);
-    if (mc >= BM) {
+    const int cap = (int)(((1ull << 31) - 1) / wide / BM * BM);
+    if (cap >= BM) {
+      const int mc = row_block(M, cap);
       for (int r0 = 0; r0 < M; r0 += mc) {
         Args c = a;
         c.A = a.A + (size_t)r0 * K;
@@ -1976,8 +1987,9 @@ extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* b
   if (persistent_enabled() && 2 * F <= BIAS_LDS / 4 && K >= 2 * BK && (size_t)2 * F * K * 2 < (1ull << 31)) {
     // 32-bit byte offsets: row blocks of at most mc rows per launch (see dna_linear_fwd)
     const size_t wide = (size_t)(K > 2 * F ? K : 2 * F) * 2;
-    const int mc = (int)(((1ull << 31) - 1) / wide / BM * BM);
-    if (mc >= BM) {
+    const int cap = (int)(((1ull << 31) - 1) / wide / BM * BM);
+    if (cap >= BM) {
+      const int mc = row_block(M, cap);
       for (int r0 = 0; r0 < M; r0 += mc) {
         Args c = a;
         c.A = a.A + (size_t)r0 * K;
@@ -2039,7 +2051,7 @@ extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const vo
   a.GM = 8;
   if (const char* e = getenv("DNA_GEMM_GM")) a.GM = atoi(e);
   const size_t wide = (size_t)(N > 2 * F ? N : 2 * F) * 2;
-  const int mc = (int)(((1ull << 31) - 1) / wide / BM * BM);
+  const int mc = row_block(M, (int)(((1ull << 31) - 1) / wide / BM * BM));
   for (int r0 = 0; r0 < M; r0 += mc) {
     Args c = a;
     c.A = a.A + (size_t)r0 * N;
