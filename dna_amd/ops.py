@@ -274,6 +274,46 @@ def transpose_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
     N.call("dna_transpose_bf16", src.data_ptr(), r, c, dst.data_ptr(), N.stream_ptr())
 
 
+@torch.library.custom_op("dna_amd::geglu_linear_fwd", mutates_args=("g", "a"))
+def geglu_linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, p: float,
+                     seed: int, offset: int, g: torch.Tensor, a: torch.Tensor) -> None:
+    """g = x . w^T (+ bias) and a = dropout(gelu(g[:, :F]) * g[:, F:]) in one launch
+    (gated_layers + GeGLU, bert_layers.py:292-296); same Philox mask as geglu_fwd."""
+    _cuda_contig("x", x, (torch.bfloat16,))
+    _cuda_contig("w", w, (torch.bfloat16,))
+    _cuda_contig("g", g, (torch.bfloat16,))
+    _cuda_contig("a", a, (torch.bfloat16,))
+    M, K = x.shape
+    F2 = w.shape[0]
+    _check(w.shape[1] == K and tuple(g.shape) == (M, F2) and tuple(a.shape) == (M, F2 // 2),
+           "shapes: x[M,K], w[2F,K], g[M,2F], a[M,F]")
+    _check(K % 64 == 0 and F2 % 256 == 0, f"K % 64 and 2F % 256 required (K={K}, 2F={F2})")
+    if bias is not None:
+        _cuda_contig("bias", bias, (torch.float32,))
+        _check(bias.numel() == F2, "bias must hold 2F floats")
+    N.call("dna_geglu_linear_fwd", x.data_ptr(), w.data_ptr(), _p(bias), M, F2 // 2, K, float(p),
+           seed, offset, g.data_ptr(), a.data_ptr(), N.stream_ptr())
+
+
+@torch.library.custom_op("dna_amd::geglu_linear_dgrad", mutates_args=("dg",))
+def geglu_linear_dgrad(dy: torch.Tensor, wt: torch.Tensor, g: torch.Tensor, p: float, seed: int,
+                       offset: int, dg: torch.Tensor) -> None:
+    """dg = geglu_bwd(dy . wt^T, g) in one launch: wo's data gradient (wt = wo^T, [F, hidden])
+    with the GeGLU backward in the epilogue (bert_layers.py:292-297); == linear_fwd + geglu_bwd."""
+    _cuda_contig("dy", dy, (torch.bfloat16,))
+    _cuda_contig("wt", wt, (torch.bfloat16,))
+    _cuda_contig("g", g, (torch.bfloat16,))
+    _cuda_contig("dg", dg, (torch.bfloat16,))
+    M, H = dy.shape
+    F = wt.shape[0]
+    _check(wt.shape[1] == H and tuple(g.shape) == (M, 2 * F) and dg.shape == g.shape,
+           "shapes: dy[M,H], wt[F,H], g / dg[M,2F]")
+    _check(H % 128 == 0 and H >= 256 and F % 256 == 0,
+           f"hidden % 128, hidden >= 256 and F % 256 required (H={H}, F={F})")
+    N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), M, F, H,
+           float(p), seed, offset, dg.data_ptr(), N.stream_ptr())
+
+
 # ------------------------------------------------------------------------------- elementwise
 @torch.library.custom_op("dna_amd::geglu_fwd", mutates_args=("a",))
 def geglu_fwd(g: torch.Tensor, p: float, seed: int, offset: int, a: torch.Tensor) -> None:
@@ -309,5 +349,5 @@ def xent_fwd(logits: torch.Tensor, target: torch.Tensor, loss: torch.Tensor,
 
 
 OPS = ("attn_fwd", "attn_bwd", "alibi_attn_qkvpacked", "flash_attn_qkvpacked", "linear_fwd",
-       "transpose_bf16",
+       "transpose_bf16", "geglu_linear_fwd", "geglu_linear_dgrad",
        "geglu_fwd", "geglu_bwd", "xent_fwd")

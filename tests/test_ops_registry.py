@@ -73,3 +73,31 @@ def test_linear_geglu_xent_ops_vs_torch():
     lref = torch.nn.functional.cross_entropy(logits.float(), tgt, reduction="none")
     assert torch.allclose(loss, lref, atol=1e-4, rtol=1e-4)
     assert torch.allclose(lse, torch.logsumexp(logits.float(), 1), atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_fused_geglu_linear_ops_equal_separate_ops():
+    """The fused gated_layers + GeGLU forward and wo-dgrad + GeGLU backward operators equal the
+    separate linear_fwd / geglu_fwd / geglu_bwd operators bit for bit, dropout on."""
+    from dna_amd import ops  # noqa: F401
+    g0 = torch.Generator().manual_seed(9)
+    M, H, F = 1000, 768, 3072
+    x = torch.randn(M, H, generator=g0).cuda().bfloat16()
+    wg = (torch.randn(2 * F, H, generator=g0) * 0.05).cuda().bfloat16()
+    g = torch.empty(M, 2 * F, device="cuda", dtype=torch.bfloat16)
+    a = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    torch.ops.dna_amd.geglu_linear_fwd(x, wg, None, 0.1, 5, 3, g, a)
+    g2 = torch.empty_like(g)
+    torch.ops.dna_amd.linear_fwd(x, wg, None, g2)
+    a2 = torch.empty_like(a)
+    torch.ops.dna_amd.geglu_fwd(g2, 0.1, 5, 3, a2)
+    assert torch.equal(g, g2) and torch.equal(a, a2)
+    dy = torch.randn(M, H, generator=g0).cuda().bfloat16()
+    wo_t = (torch.randn(F, H, generator=g0) * 0.05).cuda().bfloat16()
+    dg = torch.empty_like(g)
+    torch.ops.dna_amd.geglu_linear_dgrad(dy, wo_t, g, 0.1, 5, 3, dg)
+    da = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    torch.ops.dna_amd.linear_fwd(dy, wo_t, None, da)
+    dg2 = torch.empty_like(g)
+    torch.ops.dna_amd.geglu_bwd(da, g, 0.1, 5, 3, dg2)
+    assert torch.equal(dg, dg2)
