@@ -137,11 +137,34 @@ __global__ __launch_bounds__(256) void segsum_join_kernel(const int64_t* __restr
   float acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = work[((size_t)chunk * 2 + 1) * cols + k * 64 + lane];
-  for (int c = chunk + 1;; ++c) {
-    const int q0 = c * SEG_CHUNK, q1 = min(rows, q0 + SEG_CHUNK);
+  // the run's partials are added in chunk order as before (same bits), but JU chunks' partials
+  // and run-end tests are loaded at once: a frequent token's run spans thousands of chunks, and
+  // one dependent load per chunk made this the embedding gradient's longest kernel
+  constexpr int JU = 8;
+  const int nch = (rows + SEG_CHUNK - 1) / SEG_CHUNK;
+  for (int c = chunk + 1;; c += JU) {
+    float part[JU][NV];
+    bool more[JU];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] += work[((size_t)c * 2) * cols + k * 64 + lane];
-    if (sorted_ids[q1 - 1] != id || !seg_cont(sorted_ids, q1 - 1, q1, rows)) break;
+    for (int u = 0; u < JU; ++u) {
+      const int cu = min(c + u, nch - 1);  // past the last chunk: a harmless re-read, never added
+      const int q1 = min(rows, (cu + 1) * SEG_CHUNK);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) part[u][k] = work[((size_t)cu * 2) * cols + k * 64 + lane];
+      // branch-free run-end test (a short-circuit && put a branch and a vmcnt(0) around each)
+      const long a = (long)sorted_ids[q1 - 1], b = (long)sorted_ids[min(q1, rows - 1)];
+      more[u] = (a == id) & (b == id) & (q1 < rows);
+    }
+    bool done = false;
+#pragma unroll
+    for (int u = 0; u < JU; ++u) {
+      if (!done) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] += part[u][k];
+        done = !more[u];
+      }
+    }
+    if (done) break;
   }
   float* dst = dE + (size_t)id * cols;
 #pragma unroll
