@@ -2096,8 +2096,15 @@ extern "C" int dna_linear_wgrad_p(const void* dy, const void* x, int M, int N, i
   int G = num_cus() & ~7;
   G = U < G ? U : G;
   const char* ie = getenv("DNA_WGRAD_IMM");  // A/B: 0 = per-read address VALU
-  if (gemm_sched() == 2 && KTtot % 2 == 0 && KTtot / 2 / splits >= 1 && (!ie || atoi(ie) != 0))
+  // the lean kernel works in K-step pairs: an odd step count (e.g. the MLM head's masked rows)
+  // gets one more step past T, which reads zeros (rows past T lie outside the chunk resources)
+  const int KTe = KTtot + (KTtot & 1);
+  const bool pairs_ok = KTe / 2 / splits >= 1 &&
+                        (size_t)((KTe / 2 + splits - 1) / splits) * 2 * BK * (N > K ? N : K) * 2 < (1ull << 31);
+  if (gemm_sched() == 2 && pairs_ok && (!ie || atoi(ie) != 0)) {
+    a.KTtot = KTe;
     hipLaunchKernelGGL((wgradp_kernel<true, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), a);
+  }
   else if (gemm_sched() == 1 && (!ie || atoi(ie) != 0))
     hipLaunchKernelGGL((wgradp_kernel<true, 1>), dim3(G), dim3(NTHR), 0, as_stream(stream), a);
   else if (!ie || atoi(ie) != 0)
