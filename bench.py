@@ -158,44 +158,6 @@ CONFIG_A = dict(vocab_size=4096, hidden_size=128, num_hidden_layers=2, num_atten
                 intermediate_size=512)
 
 
-def launch_ranks(n, argv):
-    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N rank processes of this
-    script -- torchrun-style env (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT) --
-    before this process touches the GPU, wait for all of them, and exit with the first failing
-    rank's status. Rank r binds cuda:r; rank 0 prints the JSON line (stdout is inherited)."""
-    import signal
-    import socket
-    import subprocess
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
-    rc = 0
-    try:
-        pending = list(procs)
-        while pending:
-            for p in list(pending):
-                code = p.poll()
-                if code is None:
-                    continue
-                pending.remove(p)
-                if code != 0 and rc == 0:
-                    rc = code
-                    for q in pending:  # one rank failed: the others would hang in a collective
-                        q.send_signal(signal.SIGTERM)
-            time.sleep(0.2)
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-    return rc if rc >= 0 else 128 - rc
-
-
 def dist_skeleton(args, world, rank):
     """--dist-dry-run: the multi-rank measurement protocol without the model (CPU, gloo): the
     same barrier / timed region / max-over-ranks / one-JSON-line path, with a gradient-sized
@@ -232,11 +194,13 @@ def main():
     ap.add_argument("--no-b64", action="store_true", help="skip the extra per-GPU b=64 measurement")
     ap.add_argument("--no-data-pipeline", action="store_true", help="skip the host data-path timing")
     ap.add_argument("--dist-dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dump-params", default=None, help=argparse.SUPPRESS)  # debug: per-rank digest
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: become one (N rank processes), before any GPU call in this process
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        from dna_amd.launch import launch_ranks
+        sys.exit(launch_ranks(args.gpus, __file__, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -253,17 +217,11 @@ def main():
         data_pipeline = measure_data_pipeline(args.batch, torch.device("cuda", local))
     # DNA_DIST_BACKEND=gloo (rehearsal only): every rank on the visible GPUs round-robin, gradient
     # all-reduce over gloo -- exercises the multi-rank bench path on a one-GPU box
-    backend = os.environ.get("DNA_DIST_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
+    from dna_amd.launch import init_rank_process_group, rank_device_index
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    device = torch.device("cuda", local)
+        device = init_rank_process_group(local)
+    else:
+        device = torch.device("cuda", rank_device_index(local))
     torch.cuda.set_device(device)
 
     from dna_amd.bert_layers import BertForMaskedLM
@@ -372,6 +330,13 @@ def main():
                              label="config A (2 layers, d=128, S=128)")
             ca["single_thread" if th == 1 else "all_threads"] = {k: r[k] for k in ("value", "cores", "sample")}
         cpu["config_a"] = ca
+
+    if args.dump_params:  # debug dump: every rank's flat parameters after the timed steps
+        from dna_amd.launch import flat_digest
+        os.makedirs(args.dump_params, exist_ok=True)
+        with open(os.path.join(args.dump_params, f"rank{rank}.json"), "w") as f:
+            json.dump(dict(flat_digest(trainer.flat.flat), rank=rank, world=world,
+                           loss=final_loss, global_step=trainer.global_step), f)
 
     if rank == 0:
         line = {

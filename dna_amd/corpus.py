@@ -211,8 +211,8 @@ class DNABERT2Pretrain(SequenceDataset):
         return self._data_loader(self.dataset_train, self.batch_size,
                                  shuffle=self.shuffle and sampler is None, sampler=sampler)
 
-    def val_dataloader(self, **kwargs):
-        return self._data_loader(self.dataset_val, self.batch_size_eval)
+    def val_dataloader(self, sampler=None, **kwargs):
+        return self._data_loader(self.dataset_val, self.batch_size_eval, sampler=sampler)
 
-    def test_dataloader(self, **kwargs):
-        return self._data_loader(self.dataset_test, self.batch_size_eval)
+    def test_dataloader(self, sampler=None, **kwargs):
+        return self._data_loader(self.dataset_test, self.batch_size_eval, sampler=sampler)

@@ -303,3 +303,30 @@ def test_bf16_train_step_vs_reference_fixture():
         count += gi.size
     assert abs(math.sqrt(total_sq) - float(z["clip_total_norm"])) <= 1e-2 * float(z["clip_total_norm"])
     assert flips <= 2 * flips_ref + 0.005 * count, (flips, flips_ref, count)
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 5e-3)])
+def test_train_evaluate_equals_reference_loss(precision, tol):
+    """train.evaluate (the validation / test epoch, reference train.py:339-406,442-460) on the
+    config-A golden batch: val/loss == the reference's bert_cross_entropy task loss, perplexity
+    == exp(loss), the model is back in training mode afterwards; a 2-batch loader weights the
+    batches by size."""
+    import types
+
+    import train
+    z, cfg = _golden("cfgA")
+    m = _model(cfg, precision).train()
+    ids, mask, labels = (t.cpu() for t in _batch(z))
+    target = torch.as_tensor(z["target"].astype(np.int64))
+    batch = ((ids, mask, labels), target)
+    tr = types.SimpleNamespace(model=m)
+    tokens = {}
+    res = train.evaluate(tr, [("val", [batch]), ("test", [batch, batch])], DEV, 3, tokens=tokens)
+    assert m.training
+    ref = float(z["task_loss"])
+    assert abs(res["val/loss"] - ref) < tol and abs(res["test/loss"] - ref) < tol
+    assert abs(res["val/perplexity"] - math.exp(res["val/loss"])) < 1e-9 * res["val/perplexity"] + 1e-12
+    assert res["val/num_tokens"] == target.numel() and res["test/num_tokens"] == 2 * target.numel()
+    res2 = train.evaluate(tr, [("val", [batch])], DEV, 3, tokens=tokens)
+    assert res2["val/num_tokens"] == 2 * target.numel()  # NumTokens is never reset
+    assert res2["val/loss"] == res["val/loss"]  # eval mode: no dropout, deterministic

@@ -2,7 +2,10 @@
 own configs/ tree compose and build the run unchanged; GPU test runs real steps of config A."""
 import io
 import json
+import math
 import os
+import subprocess
+import sys
 
 import pytest
 
@@ -98,9 +101,24 @@ def test_train_config_a_runs_on_gpu(data_root, monkeypatch, tmp_path):
     buf = io.StringIO()
     tr = train.train(cfg, out=buf)
     logs = [json.loads(l) for l in buf.getvalue().splitlines()]
-    assert tr.global_step == 6 and logs[-1]["step"] == 6
-    assert all(l["train/loss"] == l["train/loss"] for l in logs)  # finite
+    assert logs[0]["event"] == "start" and logs[0]["world"] == 1
+    train_logs = [l for l in logs if "train/loss" in l]
+    assert tr.global_step == 6 and train_logs[-1]["step"] == 6
+    assert all(l["train/loss"] == l["train/loss"] for l in train_logs)  # finite
     assert os.path.exists(tmp_path / "checkpoints" / "last.ckpt")
+    # the validation epoch at the end of the run: val + test loaders, then ModelCheckpoint
+    # (monitor test/loss, mode min) writes checkpoints/test/loss.ckpt
+    ev = [l for l in logs if "val/loss" in l]
+    assert len(ev) == 1 and ev[0]["step"] == 6
+    for k in ("val/loss", "val/perplexity", "test/loss", "test/perplexity"):
+        assert math.isfinite(ev[0][k]), k
+    assert abs(ev[0]["val/perplexity"] - math.exp(ev[0]["val/loss"])) < 1e-3 * ev[0]["val/perplexity"]
+    assert ev[0]["val/num_tokens"] > 0
+    best = tmp_path / "checkpoints" / "test" / "loss.ckpt"
+    assert os.path.exists(best)
+    import torch
+    ck = torch.load(best, map_location="cpu", weights_only=True)
+    assert ck["callbacks"]["ModelCheckpoint"]["best_model_score"] == pytest.approx(ev[0]["test/loss"])
     # resume from the Lightning-layout checkpoint
     cfg2 = compose(os.path.join(ROOT, "configs"), "config",
                    ["experiment=dnabert2/dnabert2_hg38_pretrain"] + CFG_A[:-1] +
@@ -132,3 +150,82 @@ def test_text_corpus_experiment_builds(cdir, tmp_path, monkeypatch):
     res = json.loads(buf.getvalue())
     assert res["train_windows"] == len(z["lines"]) and cfg.dataset.max_length == 128
     assert list(cfg.optimizer.betas) == [0.9, 0.98] and cfg.scheduler.warmup_t == 60000
+
+
+def test_devices_world_size_mismatch_raises(data_root, monkeypatch):
+    """trainer.devices must equal the launcher's WORLD_SIZE (the reference's Lightning would
+    start `devices` processes; a silent one-GPU run is an error here)."""
+    import train
+    from dna_amd.compose import compose
+    monkeypatch.setenv("DATA_PATH", data_root)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    cfg = compose(os.path.join(ROOT, "configs"), "config", CFG_A)
+    with pytest.raises(ValueError, match="WORLD_SIZE"):
+        train.train(cfg, out=io.StringIO())
+    monkeypatch.delenv("WORLD_SIZE")
+    assert train.n_devices(compose(os.path.join(ROOT, "configs"), "config",
+                                   CFG_A + ["trainer.devices=[0,3]"]).trainer) == 2
+
+
+def _two_rank_env(data_root, dump):
+    env = dict(os.environ, DATA_PATH=data_root, DNA_DIST_BACKEND="gloo", DNA_DUMP_PARAMS=dump,
+               PYTHONUNBUFFERED="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _digests(dump, n):
+    ds = [json.load(open(os.path.join(dump, f"rank{r}.json"))) for r in range(n)]
+    assert all(d["world"] == n for d in ds)
+    return ds
+
+
+@pytest.mark.gpu
+def test_train_devices_2_starts_two_ranks(data_root, tmp_path):
+    """`python train.py ... trainer.devices=2` without a launcher starts two rank processes (the
+    reference's Lightning DDP launch, train.py:630-639) that train the config-A model together:
+    one log stream (rank 0) with world=2, identical parameters on both ranks afterwards, the
+    evaluation epoch and the monitored checkpoint. gloo backend: both ranks share the one GPU
+    of the test box (the RCCL run is the driver's 8-GPU bench)."""
+    dump = str(tmp_path / "dump")
+    cmd = [sys.executable, os.path.join(ROOT, "train.py"), "experiment=dnabert2/dnabert2_hg38_pretrain"] + \
+        [o for o in CFG_A if not o.startswith("trainer.devices")] + \
+        ["trainer.devices=2", "train.max_steps=3", "trainer.accumulate_grad_batches=1",
+         "trainer.log_every_n_steps=1"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=_two_rank_env(data_root, dump),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    logs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert logs[0]["event"] == "start" and logs[0]["world"] == 2 and logs[0]["parallelism"] == "dp2"
+    steps = [l["step"] for l in logs if "train/loss" in l]
+    assert steps == [1, 2, 3]  # one stream: rank 0 prints, every step once
+    assert all(math.isfinite(l["train/loss"]) for l in logs if "train/loss" in l)
+    assert any("test/loss" in l for l in logs)
+    d0, d1 = _digests(dump, 2)
+    assert d0["global_step"] == d1["global_step"] == 3
+    assert d0["sha256"] == d1["sha256"], (d0, d1)
+    assert os.path.exists(tmp_path / "checkpoints" / "test" / "loss.ckpt")
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_real_model(tmp_path):
+    """bench.py's own world > 1 path with the real DNABERT-2 step (not the --dist-dry-run
+    skeleton): process group init, the model step with GradBucketReducer, max-over-ranks timing,
+    one JSON line from rank 0 -- two gloo ranks on the test box's GPU."""
+    dump = str(tmp_path / "dump")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--batch", "8", "--no-cpu-baseline", "--no-b64", "--no-data-pipeline",
+           "--dump-params", dump]
+    env = _two_rank_env("", dump)
+    env.pop("DNA_DUMP_PARAMS")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
+    assert line["config"]["global_batch"] == 16 and line["value"] > 0
+    assert math.isfinite(line["final_loss"])
+    d0, d1 = _digests(dump, 2)
+    assert d0["sha256"] == d1["sha256"], (d0, d1)

@@ -12,6 +12,18 @@ train() :668-694 -> Lightning fit) for the DNABERT-2 MLM path, without Hydra or 
     optimizer step, `accumulate_grad_batches`), DistributedSampler sharding across ranks
     (one process per GPU, torch.distributed.run), metrics train/loss, trainer/loss,
     train/perplexity, train/num_tokens, timer/step;
+  * one process per device: `trainer.devices=N` (N > 1) without a launcher starts N rank
+    processes of this script (dna_amd.launch, as Lightning's DDP does for the reference,
+    train.py:630-639); under a launcher WORLD_SIZE must equal devices x num_nodes;
+  * evaluation (train.py:339-406,442-460,547-596): after every training epoch (and when
+    train.max_steps ends the run) the val and test loaders run forward-only on the same kernels
+    (dropout off, compact masked rows, no dense logits), each rank on its DistributedSampler
+    shard, logging {val,test}/{loss,perplexity,num_tokens} through one packed all-reduce;
+    `train.validate_at_start` and `train.test` (final/val, final/test) as the reference;
+  * ModelCheckpoint (configs/callbacks/checkpoint.yaml): the top-1 checkpoint by
+    callbacks.model_checkpoint.monitor (${train.monitor}, e.g. test/loss, mode min) saved as
+    <dirpath>/<filename>.ckpt (filename defaults to the monitor name, so test/loss.ckpt), plus
+    last.ckpt; the best score survives a resume;
   * checkpoints in Lightning's layout ({"state_dict": {"model.<key>": ...}, ...}) so
     `train.pretrained_model_path` / `trainer.resume_from_checkpoint` interoperate; a missing
     resume path (the reference configs carry cluster paths) is a warning, not a crash.
@@ -67,7 +79,7 @@ def load_lightning_state(model, path, strict):
     return missing, unexpected
 
 
-def save_checkpoint(path, trainer, epoch, batches_done=0, metrics=None):
+def save_checkpoint(path, trainer, epoch, batches_done=0, metrics=None, best=None):
     """Lightning-1.8 checkpoint layout: state_dict with the "model." prefix, torch AdamW
     optimizer state, timm scheduler state, epoch / global_step; plus this engine's dropout-stream
     position and the count of batches already consumed in `epoch` (mid-epoch resume). Written to
@@ -80,9 +92,127 @@ def save_checkpoint(path, trainer, epoch, batches_done=0, metrics=None):
           "lr_schedulers": [trainer.sched.state_dict()] if trainer.sched else [],
           "dna_amd": {"dropout_rng": trainer.rng_state(), "batches_done": int(batches_done),
                       "metrics": metrics or {}}}
+    if best is not None:  # ModelCheckpoint state, as Lightning keeps it under "callbacks"
+        ck["callbacks"] = {"ModelCheckpoint": {"monitor": best.monitor, "mode": best.mode,
+                                               "best_model_score": best.score,
+                                               "best_model_path": best.path}}
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     tmp = path + ".tmp"
     torch.save(ck, tmp)
     os.replace(tmp, path)
+
+
+def n_devices(tr):
+    """Processes the run wants: trainer.devices (an int, or a list of device ids as in the
+    reference, train.py:631-633) x trainer.num_nodes (one node only here)."""
+    d = tr.get("devices", 1)
+    if isinstance(d, (list, tuple)) or hasattr(d, "to_container"):
+        d = len(list(d))
+    elif d in (None, "auto", -1, "-1"):
+        d = max(1, torch.cuda.device_count())  # counts devices without initialising HIP
+    nodes = int(tr.get("num_nodes", 1) or 1)
+    if nodes != 1:
+        raise NotImplementedError(f"trainer.num_nodes={nodes}: one node (up to 8 MI355X) only")
+    return int(d)
+
+
+class BestCheckpoint:
+    """ModelCheckpoint(monitor, mode, save_top_k=1, filename) of configs/callbacks/checkpoint.yaml:
+    keeps the best-so-far file <dirpath>/<filename>.ckpt (Lightning's format_checkpoint_name with
+    auto_insert_metric_name=False: the filename is the monitor name, "/" making a sub-directory),
+    overwritten in place whenever the monitored value improves."""
+
+    def __init__(self, dirpath, monitor, mode="min", filename=None, save_top_k=1):
+        if mode not in ("min", "max"):
+            raise ValueError(f"model_checkpoint.mode={mode!r}: min or max")
+        self.monitor, self.mode = monitor, mode
+        self.enabled = bool(monitor) and int(save_top_k) != 0
+        if self.enabled and int(save_top_k) != 1:
+            raise NotImplementedError(f"model_checkpoint.save_top_k={save_top_k} (1 or 0)")
+        self.path = os.path.join(dirpath, (filename or monitor or "best") + ".ckpt")
+        self.score = None
+
+    def improves(self, value):
+        if self.score is None:
+            return True
+        return value < self.score if self.mode == "min" else value > self.score
+
+
+def eval_loaders(cfg, ds, world, rank, final=False):
+    """The reference's _eval_dataloaders (train.py:559-582): val then test loaders, named
+    "val" / "test" ("final/val" / "final/test" for trainer.test), one dropped by
+    train.remove_test_loader_in_eval / remove_val_loader_in_eval. Each rank reads its
+    DistributedSampler shard (Lightning replaces the eval samplers under DDP, shuffle off)."""
+    from torch.utils.data.distributed import DistributedSampler
+    out = []
+    for name, dset, make in (("val", ds.dataset_val, ds.val_dataloader),
+                             ("test", ds.dataset_test, ds.test_dataloader)):
+        if name == "test" and cfg.train.get("remove_test_loader_in_eval", False):
+            continue
+        if name == "val" and cfg.train.get("remove_val_loader_in_eval", False):
+            continue
+        if len(dset) == 0:
+            warnings.warn(f"{name} split is empty; skipped in evaluation")
+            continue
+        sampler = DistributedSampler(dset, num_replicas=world, rank=rank, shuffle=False)
+        out.append((("final/" if final else "") + name, make(sampler=sampler)))
+    return out
+
+
+def evaluate(trainer, loaders, device, pad_id, limit=1.0, tokens=None):
+    """validation_step / test_step through _shared_step (train.py:339-380, 442-460) for the MLM
+    task: forward-only on the training kernels in eval mode (dropout off), the task loss
+    bert_cross_entropy on the compact masked rows (no dense [b, S, V] logits), per loader
+      <name>/loss        batch-size-weighted mean over all batches of all ranks (Lightning's
+                         on_epoch mean with sync_dist)
+      <name>/perplexity  exp(sum loss*numel / sum numel) over the epoch (Perplexity, reset per
+                         evaluation, torchmetrics.py:24-73)
+      <name>/num_tokens  running target-token count (NumTokens, never reset: `tokens` carries it)
+    All sums of all loaders travel in ONE all-reduce. Returns {metric: float}."""
+    from dna_amd.ddp import reduce_metrics
+    from dna_amd.trainer import DeviceBatch
+    model = trainer.model
+    was_training = model.training
+    model.eval()
+    tokens = tokens if tokens is not None else {}
+    sums, names = [], []
+    try:
+        with torch.no_grad():
+            for name, loader in loaders:
+                n = len(loader)
+                if isinstance(limit, float) and limit <= 1.0:
+                    n = max(1, int(n * limit)) if n else 0
+                elif limit is not None:
+                    n = min(n, int(limit))
+                loss_w = torch.zeros((), dtype=torch.float64, device=device)
+                nll = torch.zeros((), dtype=torch.float64, device=device)
+                bs_sum, numel_sum = 0, 0
+                for bi, ((masked, mask, labels), target) in enumerate(loader):
+                    if bi >= n:
+                        break
+                    db = DeviceBatch.from_host(masked, mask, labels, target, device, pad_id)
+                    loss, _ = model.mlm_loss(db.masked_ids, db.mask, db.index, db.n_mask,
+                                             db.n_unk_masked)
+                    bs, numel = int(target.shape[0]), int(target.numel())
+                    loss_w += loss.double() * bs
+                    nll += loss.double() * numel
+                    bs_sum += bs
+                    numel_sum += numel
+                tokens[name] = tokens.get(name, 0) + numel_sum
+                sums += [loss_w, bs_sum, nll, numel_sum, tokens[name]]
+                names.append(name)
+    finally:
+        model.train(was_training)
+    if not names:
+        return {}
+    _, g = reduce_metrics(torch.zeros(()), 0, extra=sums)
+    res = {}
+    for i, name in enumerate(names):
+        lw, bs, nl, ne, tk = g[5 * i: 5 * i + 5]
+        res[f"{name}/loss"] = lw / max(bs, 1)
+        res[f"{name}/perplexity"] = math.exp(nl / max(ne, 1))
+        res[f"{name}/num_tokens"] = int(round(tk))
+    return res
 
 
 def train(cfg, dry_run=False, out=sys.stdout):
@@ -127,12 +257,22 @@ def train(cfg, dry_run=False, out=sys.stdout):
                           "scheduler": sched, "optimizer": opt.to_container()}), file=out)
         return None
 
+    want = n_devices(tr)
+    if want != world:
+        raise ValueError(f"trainer.devices={want} but WORLD_SIZE={world}: start the run with "
+                         f"`python train.py ...` (it launches one process per device) or a "
+                         f"launcher with --nproc-per-node {want}")
+    from dna_amd.launch import init_rank_process_group, rank_device_index
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        device = init_rank_process_group(local)
+    else:
+        device = torch.device("cuda", rank_device_index(local))
     torch.cuda.set_device(device)
+    if rank == 0:
+        print(json.dumps({"event": "start", "world": world, "parallelism": f"dp{world}",
+                          "backend": dist.get_backend() if world > 1 else None,
+                          "global_batch": int(cfg.dataset.get("batch_size", 0) or 0) * world}),
+              file=out, flush=True)
     trainer = MLMTrainer(model, device, lr=float(opt.lr),
                          weight_decay=float(opt.get("weight_decay", 0.0)),
                          betas=tuple(opt.get("betas", (0.9, 0.999))),
@@ -178,12 +318,26 @@ def train(cfg, dry_run=False, out=sys.stdout):
     pad_id = getattr(ds.tokenizer, "pad_token_id", 3)
     ck_cfg = cfg.get("callbacks", {}) or {}
     mc = ck_cfg.get("model_checkpoint") if ck_cfg else None
-    ck_path = None
-    if rank == 0 and mc is not None:
+    ck_path, best = None, None
+    if mc is not None:
         d = mc.get("dirpath", "checkpoints/")
-        os.makedirs(d, exist_ok=True)
-        ck_path = os.path.join(d, "last.ckpt")
+        if rank == 0:
+            os.makedirs(d, exist_ok=True)
+        if mc.get("save_last", True):
+            ck_path = os.path.join(d, "last.ckpt")
+        # configs/callbacks/checkpoint.yaml: monitor ${train.monitor}, mode ${train.mode},
+        # save_top_k 1, filename ${train.monitor}
+        monitor = mc.get("monitor", cfg.train.get("monitor"))
+        best = BestCheckpoint(d, monitor, mode=mc.get("mode", cfg.train.get("mode", "min")),
+                              filename=mc.get("filename", monitor),
+                              save_top_k=mc.get("save_top_k", 1))
+        prev = (ck.get("callbacks") or {}).get("ModelCheckpoint") if resume and os.path.exists(resume) else None
+        if prev and prev.get("monitor") == best.monitor:
+            best.score = prev.get("best_model_score")
     ck_every = int((mc.get("every_n_train_steps") if mc is not None else 0) or 1000)
+    limit_val = tr.get("limit_val_batches", 1.0)
+    limit_test = tr.get("limit_test_batches", 1.0)
+    eval_tokens = {}  # NumTokens per eval loader: never reset (torchmetrics.py:75-115)
     # task torchmetrics (torchmetrics.py:24-115): Perplexity reset each epoch, NumTokens never.
     # Both are updated per micro-batch with that micro-batch's loss and target.numel(), and
     # SUM-reduced over ranks when logged (dist_reduce_fx="sum", sync_dist=True).
@@ -218,10 +372,39 @@ def train(cfg, dry_run=False, out=sys.stdout):
                   file=out, flush=True)
         t_last = now
 
-    def checkpoint(ep, batches_done):
-        if ck_path is not None:
-            save_checkpoint(ck_path, trainer, ep, batches_done,
-                            {"num_tokens_local": int(ntok.count)})
+    eval_cache = {}
+
+    def run_eval(final=False):
+        if final not in eval_cache:  # built once: persistent workers live across epochs
+            eval_cache[final] = eval_loaders(cfg, ds, world, rank, final=final)
+        loaders = eval_cache[final]
+        res = evaluate(trainer, loaders, device, pad_id,
+                       limit=limit_test if final else limit_val, tokens=eval_tokens)
+        if rank == 0 and res:
+            print(json.dumps(dict({"step": trainer.global_step, "epoch": epoch},
+                                  **{k: (round(v, 6) if isinstance(v, float) else v)
+                                     for k, v in res.items()})), file=out, flush=True)
+        return res
+
+    def checkpoint(ep, batches_done, metrics=None):
+        """last.ckpt, and the monitored top-1 file when `metrics` (an evaluation) improve it.
+        Rank 0 writes; every rank keeps the same best score (the metrics are all-reduced)."""
+        state = {"num_tokens_local": int(ntok.count)}
+        if best is not None and best.enabled and metrics:
+            if best.monitor not in metrics:
+                warnings.warn(f"model_checkpoint.monitor={best.monitor!r} was not logged "
+                              f"(have {sorted(metrics)}); no best checkpoint")
+            elif best.improves(metrics[best.monitor]):
+                best.score = float(metrics[best.monitor])
+                if rank == 0:
+                    save_checkpoint(best.path, trainer, ep, batches_done, state, best)
+                    print(json.dumps({"step": trainer.global_step, "checkpoint": best.path,
+                                      best.monitor: best.score}), file=out, flush=True)
+        if ck_path is not None and rank == 0:
+            save_checkpoint(ck_path, trainer, ep, batches_done, state, best)
+
+    if cfg.train.get("validate_at_start", False):  # trainer.validate(model), train.py:684-687
+        run_eval()
 
     for epoch in range(start_epoch, max_epochs):
         if hasattr(loader.sampler, "set_epoch"):
@@ -260,10 +443,21 @@ def train(cfg, dry_run=False, out=sys.stdout):
             loss = optimizer_step(micro)
             log_line(loss)
         skip_batches = 0
-        # epoch finished (or max_steps reached inside it): resume starts at the next batch
-        checkpoint(epoch + 1, 0) if not done else checkpoint(epoch, bi + 1)
+        # end of the epoch (or of the run at max_steps): the validation epoch (val + test
+        # loaders), then ModelCheckpoint on its metrics; a resume starts at the next batch
+        metrics = run_eval()
+        checkpoint(epoch + 1, 0, metrics) if not done else checkpoint(epoch, bi + 1, metrics)
         if done:
             break
+    if cfg.train.get("test", False):  # trainer.test(model) after fit, train.py:693-694
+        run_eval(final=True)
+    dump = os.environ.get("DNA_DUMP_PARAMS")
+    if dump:  # debug: every rank's parameter digest (multi-rank tests compare them)
+        from dna_amd.launch import flat_digest
+        os.makedirs(dump, exist_ok=True)
+        with open(os.path.join(dump, f"rank{rank}.json"), "w") as f:
+            json.dump(dict(flat_digest(trainer.flat.flat), rank=rank, world=world,
+                           global_step=trainer.global_step), f)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -282,6 +476,12 @@ def main(argv=None):
     cfg = compose(a.config_dir, a.config_name, a.overrides)
     if a.print_config:
         print(json.dumps(cfg.to_container(skip_errors=True), indent=1, default=str))
+    want = n_devices(cfg.trainer)
+    if want > 1 and "WORLD_SIZE" not in os.environ and not a.dry_run:
+        # Lightning's DDP launch (train.py:630-639): one process per device, started before
+        # this process touches the GPU; rank 0 prints the log stream
+        from dna_amd.launch import launch_ranks
+        sys.exit(launch_ranks(want, __file__, sys.argv[1:] if argv is None else list(argv)))
     return train(cfg, dry_run=a.dry_run)
 
 
