@@ -55,6 +55,29 @@ def _compile(src):
     return obj, None
 
 
+def _check_asm_lds_waits():
+    """gemm.hip's inline-asm ds_read_b64_tr_b16 results are settled only by explicit
+    lgkmcnt(0) waits the compiler does not know about: fail the build if any instruction names a
+    destination VGPR between such a read and its wait (scripts/check_lds_asm_waits.py). Run
+    once per rebuilt object (a stamp file next to it)."""
+    obj = os.path.join(BUILD, "gemm.hip.o")
+    stamp = obj + ".ldscheck"
+    if not os.path.exists(obj) or (os.path.exists(stamp) and
+                                   os.path.getmtime(stamp) >= os.path.getmtime(obj)):
+        return
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    try:
+        import check_lds_asm_waits as chk
+    finally:
+        sys.path.pop(0)
+    n, bad = chk.check(chk.disassemble(obj))
+    if bad or n == 0:
+        os.remove(obj)
+        raise RuntimeError(f"gemm.hip: {len(bad)} instructions touch an inline-asm LDS read's "
+                           f"destination before its lgkmcnt(0) ({n} reads):\n" + "\n".join(bad[:20]))
+    open(stamp, "w").close()
+
+
 def build(verbose=False, jobs=None):
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
@@ -68,6 +91,7 @@ def build(verbose=False, jobs=None):
                 errors.append(err)
     if errors:
         raise RuntimeError("native build failed:\n" + "\n".join(errors))
+    _check_asm_lds_waits()
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-pthread", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)

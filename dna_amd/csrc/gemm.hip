@@ -2051,7 +2051,9 @@ extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const vo
   a.GM = 8;
   if (const char* e = getenv("DNA_GEMM_GM")) a.GM = atoi(e);
   const size_t wide = (size_t)(N > 2 * F ? N : 2 * F) * 2;
-  const int mc = row_block(M, (int)(((1ull << 31) - 1) / wide / BM * BM));
+  const int cap = (int)(((1ull << 31) - 1) / wide / BM * BM);
+  DNA_CHECK_ARG(cap >= BM, "dna_geglu_linear_dgrad_p: rows of %zu bytes exceed 32-bit offsets", wide);
+  const int mc = row_block(M, cap);
   for (int r0 = 0; r0 < M; r0 += mc) {
     Args c = a;
     c.A = a.A + (size_t)r0 * N;

@@ -519,8 +519,10 @@ def _hip_wgrad_ok(dy, x):
     0.34-0.42; profiles/r03/wgrad_ab*.jsonl). DNA_WGRAD_IMPL=torch is the A/B arm."""
     rows, m = dy.shape
     n = x.shape[1]
+    # the kernel needs two 64-row K-steps per split: a handful of rows (the MLM head's masked rows
+    # of a tiny micro-batch, or none) goes to the torch split-K path
     return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.is_cuda
-            and m % 256 == 0 and n % 256 == 0 and _gemm_impl() == "hip"
+            and rows >= 128 and m % 256 == 0 and n % 256 == 0 and _gemm_impl() == "hip"
             and os.environ.get("DNA_WGRAD_IMPL", "hip") == "hip")
 
 

@@ -307,24 +307,58 @@ class ExponentialModulation(_OptimModule):
         return x * (torch.exp(-t * self.deltas.abs()) + self.shift)
 
 
+class _ChunkedLinear(torch.autograd.Function):
+    """y[L, N] = x[L, K] . w^T + b as c chunk products; dW and db reduced in fp32 over the chunks
+    and rounded once (as one GEMM with fp32 accumulation would), x / w / b in one dtype."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, c):
+        L, K = x.shape
+        N = w.shape[0]
+        xc = x.view(c, L // c, K)
+        wt = w.t().unsqueeze(0).expand(c, K, N)
+        y = torch.baddbmm(b.view(1, 1, N), xc, wt) if b is not None else torch.bmm(xc, wt)
+        ctx.save_for_backward(x, w)
+        ctx.c, ctx.has_b = c, b is not None
+        return y.view(L, N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        c = ctx.c
+        L, K = x.shape
+        N = w.shape[0]
+        dy = dy.contiguous()
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        dw = torch.bmm(dy.view(c, L // c, N).transpose(1, 2), x.view(c, L // c, K),
+                       out_dtype=torch.float32).sum(0).to(w.dtype)
+        db = dy.float().sum(0).to(dy.dtype) if ctx.has_b else None
+        return dx, dw, db, None
+
+
 def _split_k_linear(x, lin, rows_per_chunk=512):
     """nn.Linear over the L positions of the implicit filter MLP ([1, L, K] -> [1, L, N], K and N
     64-256). As one GEMM its weight gradient is a 64 x 64 (or 256 x 64) output reduced over all
     L = 65,536 positions, which hipBLASLt ran as one or four workgroups (≈210 us per call, 12 % of
-    the config-D step). Written as a batched product against the weight expanded over L / 512
-    chunks, autograd computes that gradient as a batched GEMM over the chunks plus the expand's sum:
-    split-K with every CU busy. Same math; the forward is the same GEMM batched. Short or odd
-    lengths and CPU tensors keep the plain linear."""
+    the config-D step). Here the product runs batched over L / 512 chunks and the weight gradient
+    as a batched GEMM over the chunks with fp32 partials summed in fp32: split-K with every CU
+    busy. Same dtype flow as nn.Linear: under autocast x, W and b are cast to the autocast dtype
+    and the output is in it (bias added inside the product, as addmm does); the gradients are
+    rounded once. Short or odd lengths and CPU tensors keep the plain linear."""
     L = x.shape[-2]
     if not x.is_cuda or os.environ.get("DNA_HYENA_FILTER_SPLITK", "1") == "0" or L < 8 * rows_per_chunk \
             or L % rows_per_chunk or x.dim() != 3 or x.shape[0] != 1:
         return lin(x)
-    c = L // rows_per_chunk
-    K, N = lin.in_features, lin.out_features
-    y = torch.bmm(x.reshape(c, rows_per_chunk, K), lin.weight.t().unsqueeze(0).expand(c, K, N))
-    if lin.bias is not None:
-        y = y + lin.bias
-    return y.reshape(1, L, N)
+    w, b = lin.weight, lin.bias
+    if torch.is_autocast_enabled(x.device.type):
+        dt = torch.get_autocast_dtype(x.device.type)
+        x, w, b = x.to(dt), w.to(dt), (b.to(dt) if b is not None else None)
+    else:
+        b = b.to(x.dtype) if b is not None else None
+        w = w.to(x.dtype)
+    with torch.autocast(x.device.type, enabled=False):
+        y = _ChunkedLinear.apply(x.reshape(L, -1), w, b, L // rows_per_chunk)
+    return y.reshape(1, L, -1)
 
 
 class HyenaFilter(_OptimModule):

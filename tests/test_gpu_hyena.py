@@ -249,3 +249,36 @@ def test_hyena_operator_bpe_length_vs_oracle():
         if n.endswith("freq"):
             ref = sum(ref_sd[kk].grad for kk in ref_sd if kk.endswith("freq"))
         assert _rel(p.grad.cpu().numpy(), ref.numpy()) < 2e-4, n
+
+
+@pytest.mark.parametrize("K,N", [(3, 64), (64, 64), (64, 256)])
+def test_filter_split_k_linear_matches_linear_under_autocast(K, N):
+    """The implicit-filter MLP's chunked linear (hyena._split_k_linear, config D: L = 65,536)
+    against the plain nn.Linear it replaces, under bf16 autocast and in fp32: same output dtype
+    (bf16 under autocast, as addmm gives), output within bf16 rounding, and input / weight / bias
+    gradients within the rounding of one bf16 GEMM (the chunk partials are summed in fp32 and
+    rounded once). ADVICE r3; the reference path is hyena.py:197-212 (nn.Linear in
+    implicit_filter)."""
+    from dna_amd.hyena import _split_k_linear
+    torch.manual_seed(K + N)
+    L = 65536
+    lin = torch.nn.Linear(K, N).to(DEV)
+    with torch.no_grad():
+        lin.bias.normal_()
+    x0 = torch.randn(1, L, K, device=DEV)
+    gy0 = torch.randn(1, L, N, device=DEV)
+    for ac in (True, False):
+        outs = []
+        for fn in (_split_k_linear, lambda x, l: l(x)):
+            lin.zero_grad()
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=ac):
+                y = fn(x, lin)
+            y.backward(gy0.to(y.dtype))
+            outs.append((y.detach(), x.grad.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()))
+        (y1, dx1, dw1, db1), (y2, dx2, dw2, db2) = outs
+        assert y1.dtype == y2.dtype == (torch.bfloat16 if ac else torch.float32)
+        tol = 2e-2 if ac else 1e-5
+        for a, b in ((y1, y2), (dx1, dx2), (dw1, dw2), (db1, db2)):
+            a, b = a.float(), b.float()
+            assert (a - b).abs().max().item() <= tol * max(1.0, b.abs().max().item()), (ac, K, N)

@@ -641,6 +641,27 @@ def test_wgrad_p_bench_shapes(n, k):
         assert _rel(grad - prev, ref) < 1e-5, (T, s)
 
 
+@pytest.mark.parametrize("rows", [0, 1, 64, 65, 127, 128, 129])
+def test_wgrad_few_rows(rows):
+    """Weight gradients over a handful of rows (the MLM head's masked rows of a tiny micro-batch,
+    or none): DF.wgrad / wgrad_accumulate take the torch split-K path below two 64-row K-steps
+    and the hand-written kernel from 128 rows; both equal fp32 torch."""
+    from dna_amd import functional as DF
+    n, k = 256, 768
+    g = torch.Generator(device=DEV).manual_seed(rows)
+    dy = torch.randn(rows, n, device=DEV, generator=g).bfloat16()
+    x = torch.randn(rows, k, device=DEV, generator=g).bfloat16()
+    ref = dy.float().t() @ x.float()
+    assert DF._hip_wgrad_ok(dy, x) == (rows >= 128)
+    out = DF.wgrad(dy, x)
+    assert out.shape == (n, k) and out.dtype == torch.float32
+    assert (out - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+    prev = torch.randn(n, k, device=DEV, generator=g)
+    grad = prev.clone()
+    DF.wgrad_accumulate(dy, x, grad)
+    assert (grad - prev - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+
+
 @pytest.mark.parametrize("V", [4096, 1000])
 def test_masked_cross_entropy_fwd_bwd_vs_torch(V):
     """MaskedCrossEntropy (csrc/xent.hip; V = 4096 bf16 takes the one-read vector kernels) vs
