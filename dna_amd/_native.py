@@ -64,6 +64,10 @@ _SIGS = {
     "dna_linear_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_transpose_bf16": (_i, [_vp, _i, _i, _vp, _vp]),
     "dna_linear_wgrad_p_splits": (_i, [_i, _i, _i]),
+    "dna_linear_fwd_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
+    "dna_linear_dgrad_f32": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
+    "dna_linear_wgrad_f32_splits": (_i, [_i, _i, _i]),
+    "dna_linear_wgrad_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_linear_wgrad_p": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_geglu_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
     "dna_geglu_linear_dgrad": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),

@@ -14,8 +14,9 @@ namespace dna {
 namespace gacc {
 
 __global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict__ parts, int s,
-                                                         size_t n, float* __restrict__ out) {
-  const size_t n4 = n / 4;
+                                                         size_t n, float* __restrict__ out,
+                                                         int vec) {
+  const size_t n4 = vec ? n / 4 : 0;  // 16-B path when every slice starts 16-B aligned
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
     f32x4 acc = reinterpret_cast<const f32x4*>(out)[i];
@@ -178,12 +179,13 @@ using namespace dna;
 
 extern "C" int dna_sum_slices_accum(const float* parts, int s, size_t n, float* out, void* stream) {
   DNA_CHECK_ARG(parts && out && s >= 1, "dna_sum_slices_accum: bad args");
-  DNA_CHECK_ARG((((uintptr_t)parts | (uintptr_t)out) & 15) == 0 && n % 4 == 0,
-                "dna_sum_slices_accum: needs 16-byte aligned buffers and n %% 4 == 0");
-  size_t blocks = (n / 4 + 255) / 256;
+  if (n == 0) return DNA_OK;
+  // 16-byte loads when the buffers and every slice are 16-B aligned; element-wise otherwise
+  const int vec = (((uintptr_t)parts | (uintptr_t)out) & 15) == 0 && n % 4 == 0;
+  size_t blocks = ((vec ? n / 4 : n) + 255) / 256;
   int nb = (int)(blocks < 4096 ? (blocks ? blocks : 1) : 4096);
   hipLaunchKernelGGL(gacc::sum_slices_kernel, dim3(nb), dim3(256), 0, as_stream(stream), parts, s,
-                     n, out);
+                     n, out, vec);
   DNA_LAUNCH_CHECK("dna_sum_slices_accum");
   return DNA_OK;
 }

@@ -371,6 +371,47 @@ def _hip_gemm_ok(x, w_lp, n_out, k_red):
             and k_red % 64 == 0 and n_out % 8 == 0 and _gemm_impl() == "hip")
 
 
+def _f32_gemm_ok(x, w):
+    """fp32 parity mode: exact-fp32 MFMA kernels (csrc/gemm_f32.hip) for every projection."""
+    return (x.dtype == torch.float32 and w.dtype == torch.float32 and x.is_cuda
+            and _gemm_impl() == "hip")
+
+
+def _hip_linear_f32(x, w, bias):
+    """y[M, N] = x[M, K] . w[N, K]^T (+ b), fp32 in / fp32 out (dna_linear_fwd_f32)."""
+    x, w = x.contiguous(), w.contiguous()
+    M, K = x.shape
+    Nn = w.shape[0]
+    y = torch.empty(M, Nn, device=x.device, dtype=torch.float32)
+    b = None if bias is None else bias.float().contiguous()
+    N.call("dna_linear_fwd_f32", x.data_ptr(), w.data_ptr(), _p(b), M, Nn, K, y.data_ptr(),
+           N.stream_ptr())
+    return y
+
+
+def _hip_dgrad_f32(dy, w):
+    """dx[M, K] = dy[M, N] . w[N, K], fp32 (dna_linear_dgrad_f32)."""
+    dy, w = dy.contiguous(), w.contiguous()
+    M, Nn = dy.shape
+    K = w.shape[1]
+    dx = torch.empty(M, K, device=dy.device, dtype=torch.float32)
+    N.call("dna_linear_dgrad_f32", dy.data_ptr(), w.data_ptr(), M, Nn, K, dx.data_ptr(),
+           N.stream_ptr())
+    return dx
+
+
+def _hip_wgrad_f32_parts(dy, x):
+    """fp32 split-K partials [s, m, n] of dy^T x (dna_linear_wgrad_f32)."""
+    dy, x = dy.contiguous(), x.contiguous()
+    rows, m = dy.shape
+    n = x.shape[1]
+    s = N.lib().dna_linear_wgrad_f32_splits(rows, m, n)
+    parts = torch.empty(s, m, n, device=dy.device, dtype=torch.float32)
+    N.call("dna_linear_wgrad_f32", dy.data_ptr(), x.data_ptr(), rows, m, n, s, parts.data_ptr(),
+           N.stream_ptr())
+    return parts, s
+
+
 def _geglu_fused_ok(x, w_lp):
     F2, K = w_lp.shape
     return (os.environ.get("DNA_GEGLU_FUSED", "1") != "0" and _hip_gemm_ok(x, w_lp, F2, K)
@@ -424,6 +465,9 @@ class Linear(torch.autograd.Function):
         if _hip_gemm_ok(x, w_lp, w_lp.shape[0], w_lp.shape[1]):
             with _timed("gemm_hip", flops):
                 return _hip_linear(x, w_lp, b if (b is None or b.dtype == torch.float32) else b.float())
+        if _f32_gemm_ok(x, w_lp):
+            with _timed("gemm_f32", flops):
+                return _hip_linear_f32(x, w_lp, b)
         with _timed("gemm", flops):
             if b is not None:
                 return torch.addmm(b.to(x.dtype), x, w_lp.t())
@@ -442,6 +486,9 @@ class Linear(torch.autograd.Function):
             if w_lpt is not None and _hip_gemm_ok(dy, w_lpt, w_lpt.shape[0], w_lpt.shape[1]):
                 with _timed("gemm_hip", flops):
                     dx = _hip_linear(dy, w_lpt, None)
+            elif _f32_gemm_ok(dy, w_lp):
+                with _timed("gemm_f32", flops):
+                    dx = _hip_dgrad_f32(dy, w_lp)
             else:
                 with _timed("gemm", flops):
                     dx = torch.mm(dy, w_lp)
@@ -540,7 +587,14 @@ def _hip_wgrad_parts(dy, x):
 
 
 def wgrad(dy, x):
-    """fp32 dW [m, n] = dy[rows, m]^T x[rows, n] (split-K partials + fp32 sum for bf16)."""
+    """fp32 dW [m, n] = dy[rows, m]^T x[rows, n] (split-K partials + fp32 sum for bf16; the
+    exact-fp32 MFMA kernel's slices for fp32)."""
+    if _f32_gemm_ok(x, dy):
+        parts, s = _hip_wgrad_f32_parts(dy, x)
+        out = torch.zeros(parts.shape[1:], device=dy.device, dtype=torch.float32)
+        N.call("dna_sum_slices_accum", parts.data_ptr(), s, out.numel(), out.data_ptr(),
+               N.stream_ptr())
+        return out
     if x.dtype == torch.float32:
         return torch.mm(dy.t(), x)
     if _hip_wgrad_ok(dy, x):

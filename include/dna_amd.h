@@ -178,7 +178,8 @@ int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_ids, const i
  * dy.sum(0)). */
 int dna_colsum_f32(const float* part, int rows, int cols, float* out, int accumulate, void* stream);
 /* out[i] += sum_{k<s} parts[k*n + i]: split-K partials of a weight gradient folded straight
- * into the flat fp32 gradient buffer (16-byte aligned, n % 4 == 0). */
+ * into the flat fp32 gradient buffer (16-byte loads when the buffers are 16-byte aligned and
+ * n % 4 == 0, element-wise otherwise). */
 int dna_sum_slices_accum(const float* parts, int s, size_t n, float* out, void* stream);
 
 /* ------------------------------------------------------------------ GeGLU (+ dropout)
@@ -202,6 +203,22 @@ int dna_linear_fwd(const void* x, const void* w, const float* bias, int M, int N
 int dna_linear_dgrad(const void* dy, const void* w, int M, int N, int K, void* dx, void* stream);
 int dna_linear_wgrad(const void* dy, const void* x, int M, int N, int K, int splits,
                      float* partials, void* stream);
+
+/* Exact-fp32 projections (csrc/gemm_f32.hip, v_mfma_f32_16x16x4_f32): the fp32 parity mode of
+ * the same nn.Linear layers (bert_layers.py:158,214,292,297,560,664) and their backward -- the
+ * f32 path of the reference's torch fp32 forward, without a vendor GEMM. Any shape (edges
+ * zero-filled), fp32 in / fp32 out.
+ *   fwd    y[M,N]  = x[M,K] . w[N,K]^T (+ bias[N], may be null)
+ *   dgrad  dx[M,K] = dy[M,N] . w[N,K]
+ *   wgrad  partials[s][N][K] = slice s of dy[T,N]^T . x[T,K] (token split from
+ *          dna_linear_wgrad_f32_splits); reduce with dna_sum_slices_accum. */
+int dna_linear_fwd_f32(const float* x, const float* w, const float* bias, int M, int N, int K,
+                       float* y, void* stream);
+int dna_linear_dgrad_f32(const float* dy, const float* w, int M, int N, int K, float* dx,
+                         void* stream);
+int dna_linear_wgrad_f32_splits(int T, int N, int K);
+int dna_linear_wgrad_f32(const float* dy, const float* x, int T, int N, int K, int splits,
+                         float* partials, void* stream);
 /* dst[cols][rows] = src[rows][cols] (bf16; rows, cols % 8 == 0): the transposed weight copy kept
  * beside the bf16 weights, so the data gradient dx = dy . w runs as
  * dna_linear_fwd(dy, w^T, NULL, M, K, N, dx) on both-operands-K-major MFMA tiles (replaces the

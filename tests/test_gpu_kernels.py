@@ -641,6 +641,40 @@ def test_wgrad_p_bench_shapes(n, k):
         assert _rel(grad - prev, ref) < 1e-5, (T, s)
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 2304, 768), (1000, 768, 3072), (777, 4096, 768),
+                                   (129, 192, 64), (3, 5, 7), (0, 64, 64), (515, 130, 33)])
+def test_gemm_f32_fwd_dgrad_wgrad_vs_fp64(M, N, K):
+    """Exact-fp32 MFMA projections (csrc/gemm_f32.hip) vs float64 torch: forward with bias,
+    data gradient, weight-gradient slices + dna_sum_slices_accum, at the model's shapes and at
+    ragged / tiny / misaligned ones (odd leading dimensions take the scalar load path). The
+    kernel is a k-ordered fp32 fma chain: error <= 1e-6 relative to sum |a.b|."""
+    from dna_amd import functional as DF
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
+    x = torch.randn(M, K, device=DEV, generator=g)
+    w = torch.randn(N, K, device=DEV, generator=g)
+    b = torch.randn(N, device=DEV, generator=g)
+    dy = torch.randn(M, N, device=DEV, generator=g)
+
+    def close(got, ref, a, bm):
+        scale = (a.abs().double() @ bm.abs().double()).max().item() if a.numel() and bm.numel() else 1.0
+        assert got.shape == ref.shape
+        if got.numel():
+            assert (got.double() - ref).abs().max().item() <= 1e-6 * max(scale, 1.0)
+    y = DF._hip_linear_f32(x, w, b)
+    close(y, x.double() @ w.double().t() + b.double(), x, w.t())
+    dx = DF._hip_dgrad_f32(dy, w)
+    close(dx, dy.double() @ w.double(), dy, w)
+    dw = DF.wgrad(dy, x)
+    close(dw, dy.double().t() @ x.double(), dy.t(), x)
+    grad = torch.randn(N, K, device=DEV, generator=g)
+    prev = grad.clone()
+    parts, s = DF._hip_wgrad_f32_parts(dy, x)
+    assert parts.shape == (s, N, K)
+    from dna_amd import _native as NN
+    NN.call("dna_sum_slices_accum", parts.data_ptr(), s, N * K, grad.data_ptr(), NN.stream_ptr())
+    close(grad - prev, dy.double().t() @ x.double(), dy.t(), x)
+
+
 @pytest.mark.parametrize("rows", [0, 1, 64, 65, 127, 128, 129])
 def test_wgrad_few_rows(rows):
     """Weight gradients over a handful of rows (the MLM head's masked rows of a tiny micro-batch,

@@ -42,6 +42,20 @@ def _model(cfg, precision):
     return m.to(DEV).eval()
 
 
+def _ban_library_gemm(mp):
+    """Any torch GEMM entry point raises: the fp32 parity mode must run every projection, its
+    data gradient and its weight gradient on the hand-written kernels (csrc/gemm_f32.hip), never
+    on hipBLASLt / rocBLAS."""
+    def banned(name):
+        def f(*a, **k):
+            raise AssertionError(f"library GEMM torch.{name} called in the fp32 hot path")
+        return f
+    for name in ("mm", "addmm", "bmm", "baddbmm", "matmul", "einsum"):
+        mp.setattr(torch, name, banned(name))
+    mp.setattr(torch.nn.functional, "linear", banned("nn.functional.linear"))
+    mp.setattr(torch.Tensor, "__matmul__", banned("Tensor.__matmul__"))
+
+
 def _batch(z):
     return (torch.as_tensor(z["masked_ids"].astype(np.int64), device=DEV),
             torch.as_tensor(z["mask"], device=DEV),
@@ -58,11 +72,13 @@ def test_state_dict_keys_match_reference():
 
 
 @pytest.mark.parametrize("tag", ["tiny", "cfgA", "117m"])
-def test_forward_fp32_within_1e3(tag):
+def test_forward_fp32_within_1e3(tag, monkeypatch):
     z, cfg = _golden(tag)
     m = _model(cfg, "fp32")
-    with torch.no_grad():
-        out, state = m(_batch(z), state=None)
+    batch = _batch(z)
+    with monkeypatch.context() as mp, torch.no_grad():
+        _ban_library_gemm(mp)
+        out, state = m(batch, state=None)
     assert state is None
     scores, mask = out.logits
     labels = torch.as_tensor(z["labels"].astype(np.int64))
@@ -91,15 +107,17 @@ def test_forward_bf16_tolerance(tag, tol):
 
 
 @pytest.mark.parametrize("tag", ["tiny", "cfgA"])
-def test_grads_fp32_match_reference(tag):
+def test_grads_fp32_match_reference(tag, monkeypatch):
     from dna_amd.bert_layers import MLMIndex
     z, cfg = _golden(tag)
     m = _model(cfg, "fp32")
     ids, mask, labels = _batch(z)
     idx = MLMIndex.build(ids, labels)
-    loss, _ = m.mlm_loss(ids, mask, idx)
+    with monkeypatch.context() as mp:
+        _ban_library_gemm(mp)  # forward, data and weight gradients on csrc/gemm_f32.hip
+        loss, _ = m.mlm_loss(ids, mask, idx)
+        loss.backward()
     assert abs(loss.item() - float(z["task_loss"])) < 1e-4
-    loss.backward()
     for n, p in m.named_parameters():
         g = p.grad.detach().cpu().numpy()
         ref_norm = float(z["gradnorm/" + n])
@@ -303,6 +321,39 @@ def test_bf16_train_step_vs_reference_fixture():
         count += gi.size
     assert abs(math.sqrt(total_sq) - float(z["clip_total_norm"])) <= 1e-2 * float(z["clip_total_norm"])
     assert flips <= 2 * flips_ref + 0.005 * count, (flips, flips_ref, count)
+
+
+def test_grads_fp32_117m_vs_reference_fixture(monkeypatch):
+    """fp32 parity mode at the full 117M shape (S=512): logits, task loss and every parameter's
+    gradient (norm, and 1024 sampled elements) against the reference's own fp32 run
+    (model_117m_grads.npz), with every projection, data gradient and weight gradient on the
+    exact-fp32 MFMA kernels (library GEMMs banned)."""
+    from dna_amd.bert_layers import MLMIndex
+    z = np.load(os.path.join(GOLDEN, "model_117m_grads.npz"))
+    L, d, H, Fd = json.loads(z["config"].tobytes().decode())
+    cfg = dict(vocab_size=4096, hidden_size=d, num_hidden_layers=L, num_attention_heads=H,
+               intermediate_size=Fd, hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.0,
+               layer_norm_eps=1e-12, max_position_embeddings=512, type_vocab_size=2,
+               pad_token_id=0, alibi_starting_size=512, hidden_act="gelu",
+               initializer_range=0.02, hyena_framework=True)
+    m = _model(cfg, "fp32")
+    ids = torch.as_tensor(z["masked_ids"].astype(np.int64), device=DEV)
+    mask = torch.as_tensor(z["mask"], device=DEV)
+    labels = torch.as_tensor(z["labels"].astype(np.int64), device=DEV)
+    idx = MLMIndex.build(ids, labels)
+    with monkeypatch.context() as mp:
+        _ban_library_gemm(mp)
+        loss, logits = m.mlm_loss(ids, mask, idx)
+        loss.backward()
+    l32 = z["logits_rows32"]
+    assert np.abs(logits.detach().float().cpu().numpy()[:l32.shape[0]] - l32).max() < 1e-3
+    assert abs(loss.item() - float(z["task_loss32"])) < 1e-4
+    for n, p in m.named_parameters():
+        g = p.grad.detach().reshape(-1).cpu().numpy()
+        g32 = z["gs32/" + n]
+        assert np.linalg.norm(g[z["gidx/" + n]] - g32) <= 2e-3 * np.linalg.norm(g32) + 1e-12, n
+        gn = float(np.linalg.norm(g.astype(np.float64)))
+        assert abs(gn - float(z["gradnorm32/" + n])) <= 2e-3 * float(z["gradnorm32/" + n]), n
 
 
 @pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 5e-3)])
