@@ -187,9 +187,9 @@ using namespace dna::gemm32;
 
 extern "C" int dna_linear_fwd_f32(const float* x, const float* w, const float* bias, int M, int N,
                                   int K, float* y, void* stream) {
-  DNA_CHECK_ARG(x && w && y, "dna_linear_fwd_f32: null pointer");
   DNA_CHECK_ARG(M >= 0 && N > 0 && K > 0, "dna_linear_fwd_f32: bad shape");
   if (M == 0) return DNA_OK;
+  DNA_CHECK_ARG(x && w && y, "dna_linear_fwd_f32: null pointer");
   Args a{};
   a.A = x; a.sam = K; a.sak = 1;
   a.B = w; a.sbk = 1; a.sbn = K;
@@ -200,9 +200,9 @@ extern "C" int dna_linear_fwd_f32(const float* x, const float* w, const float* b
 
 extern "C" int dna_linear_dgrad_f32(const float* dy, const float* w, int M, int N, int K, float* dx,
                                     void* stream) {
-  DNA_CHECK_ARG(dy && w && dx, "dna_linear_dgrad_f32: null pointer");
   DNA_CHECK_ARG(M >= 0 && N > 0 && K > 0, "dna_linear_dgrad_f32: bad shape");
   if (M == 0) return DNA_OK;
+  DNA_CHECK_ARG(dy && w && dx, "dna_linear_dgrad_f32: null pointer");
   Args a{};  // dx[M, K] = dy[M, N] . w[N, K]: reduction over N
   a.A = dy; a.sam = N; a.sak = 1;
   a.B = w; a.sbk = K; a.sbn = 1;
@@ -221,8 +221,8 @@ extern "C" int dna_linear_wgrad_f32_splits(int T, int N, int K) {
 
 extern "C" int dna_linear_wgrad_f32(const float* dy, const float* x, int T, int N, int K,
                                     int splits, float* partials, void* stream) {
-  DNA_CHECK_ARG(dy && x && partials, "dna_linear_wgrad_f32: null pointer");
   DNA_CHECK_ARG(T >= 0 && N > 0 && K > 0 && splits >= 1, "dna_linear_wgrad_f32: bad shape");
+  DNA_CHECK_ARG(partials && (T == 0 || (dy && x)), "dna_linear_wgrad_f32: null pointer");
   DNA_CHECK_ARG((long long)splits * N * K < (1ll << 40), "dna_linear_wgrad_f32: too many partials");
   Args a{};  // dW[N, K] = sum_t dy[t, n] x[t, k]
   a.A = dy; a.sam = 1; a.sak = N;
