@@ -60,8 +60,6 @@ _SIGS = {
     "dna_geglu_fwd": (_i, [_vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_geglu_bwd": (_i, [_vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
-    "dna_linear_fwd_pk": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
-    "dna_pack_frag_bf16": (_i, [_vp, _i, _i, _i, _vp, _vp]),
     "dna_linear_dgrad": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_linear_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_transpose_bf16": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -72,7 +70,6 @@ _SIGS = {
     "dna_linear_wgrad_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_linear_wgrad_p": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_geglu_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
-    "dna_geglu_linear_fwd_pk": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
     "dna_geglu_linear_dgrad": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_geglu_linear_dgrad_p": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_fftconv_workspace": (_sz, [_i, _i, _i]),

@@ -163,8 +163,6 @@ struct Args {
   int nt;                     // persistent kernel: non-temporal output stores (DNA_GEMM_NT, default 0)
   int order;                  // persistent kernel unit order: 0 = round-robin over the grid (XCD-
                               // remapped), 1 = XCD-major (each XCD sweeps one contiguous unit range)
-  const bf16* Bp;             // persistent kernel, SCH 3: the weight in packed fragment order
-                              // (dna_pack_frag_bf16), loaded straight into registers
 };
 
 __device__ __forceinline__ void tile_of(const Args& a, int& mt, int& nt) {
@@ -582,64 +580,6 @@ static_assert(pend_stores<EPI_BF16>(1, 0) == 16 && pend_stores<EPI_BF16>(1, 3) =
               pend_stores<EPI_GEGLU>(1, 3) == 12 && pend_stores<EPI_GEGLU>(4, 2) == 12,
               "SCH 1 store counts");
 
-// SCH == 3 (packed weight): the weight operand is never staged through LDS. It is kept in packed
-// fragment order in HBM (dna_pack_frag_bf16: fragment (nb, kb) = rows 16nb..+15 x k 32kb..+31 =
-// 1 KB, lane l's 16 B = row 16nb + (l & 15), k 32kb + 8(l >> 4) + 0..7 -- exactly the MFMA
-// operand of lane l), so each of a wave's 8 fragments of a K-step is ONE fully coalesced 1-KB
-// buffer_load_dwordx4 straight into registers, one K-step ahead (two register sets by buffer
-// parity). Per K-step and wave the VMEM issue order is
-//   phase 0: 4 B loads (next step, nq 0)    phase 1: 2 A pieces (A_1 of step + 1), 4 B loads (nq 1)
-//   phase 2: 2 A pieces (A_0 of step + 2)   phase 3: -
-// and a unit's last step (role 1) adds its epilogue stores after the MFMAs (BF16: QS per phase,
-// GeGLU: GS after phases 1 and 3). Phase 0 needs this step's nq-0 fragments, phase 1 its nq-1
-// ones, phase 3 the next step's A_0 (read in the next phase 0, one phase after the wait + barrier
-// that retire it; A_1 is retired by phase 1's wait, as it is older than the nq-1 loads). The
-// wait immediate = VMEM ops issued after the needed one; role 2 = the first step after a last
-// step (whose stores are then still in the window).
-template <int EPI>
-__host__ __device__ constexpr int pk_wait(int role, int p) {
-  const bool prev_last = role == 2, cur_last = role == 1;
-  const int qn = p == 0 ? 0 : p == 1 ? 1 : 2;  // phase of the previous step that issued it
-  int n = 0;
-  auto issued = [](int q) { return q == 0 ? 4 : q == 1 ? 6 : q == 2 ? 2 : 0; };
-  auto stores = [](bool last, int q) {
-    return !last ? 0 : EPI == EPI_BF16 ? 4 : ((q & 1) ? 12 : 0);
-  };
-  n += stores(prev_last, qn);
-  for (int q = qn + 1; q < 4; ++q) n += issued(q) + stores(prev_last, q);
-  for (int q = 0; q <= p; ++q) n += issued(q) + (q < p ? stores(cur_last, q) : 0);
-  return n;
-}
-static_assert(pk_wait<EPI_BF16>(0, 0) == 12 && pk_wait<EPI_BF16>(0, 1) == 12 &&
-              pk_wait<EPI_BF16>(0, 3) == 12 && pk_wait<EPI_BF16>(1, 1) == 16 &&
-              pk_wait<EPI_BF16>(1, 3) == 24 && pk_wait<EPI_BF16>(2, 0) == 28 &&
-              pk_wait<EPI_BF16>(2, 1) == 24 && pk_wait<EPI_BF16>(2, 3) == 20 &&
-              pk_wait<EPI_GEGLU>(1, 3) == 24 && pk_wait<EPI_GEGLU>(2, 0) == 36 &&
-              pk_wait<EPI_GEGLU>(2, 3) == 24,
-              "packed-B wait immediates");
-
-// dst = the packed fragment order of a [R][C] bf16 operand (R % 16 == 0, C % 32 == 0), read from
-// src[r][c] (trans = 0) or from src[c][r] (trans = 1: the transposed operand of the data gradient,
-// packed straight from the row-major weight). One thread per 16-B lane chunk.
-__global__ __launch_bounds__(256) void pack_frag_kernel(const bf16* __restrict__ src, int R, int C,
-                                                        int trans, bf16* __restrict__ dst) {
-  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  const size_t total = (size_t)R * C / 8;
-  if (t >= total) return;
-  const int l = (int)(t & 63);
-  const size_t f = t >> 6;
-  const int KB = C / 32;
-  const int r = (int)(f / KB) * 16 + (l & 15), c0 = (int)(f % KB) * 32 + 8 * (l >> 4);
-  bf16x8 v;
-  if (trans) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = src[(size_t)(c0 + j) * R + r];
-  } else {
-    v = *reinterpret_cast<const bf16x8*>(src + (size_t)r * C + c0);
-  }
-  *reinterpret_cast<bf16x8*>(dst + t * 8) = v;
-}
-
 // SCH selects the half-tile schedule: 0 = the original 4-phase order (reads 12/4/8/0 per phase),
 // 1 = balanced reads (8/4/8/4: B_0 of the next K-step is read in phase 3) with 5 half-tiles in
 // flight -- see the comment above the SCH == 1 branch
@@ -648,8 +588,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU ||
                     (EPI == EPI_GEGLU_BWD && SCH == 2 && (ABL == 0 || ABL == 64 || ABL == 128)),
                 "persistent kernel: bf16 / GeGLU epilogues (GeGLU backward: lean body only)");
-  static_assert(SCH != 3 || ((EPI == EPI_BF16 || EPI == EPI_GEGLU) && ABL == 0),
-                "packed-weight body: bf16 / GeGLU epilogues");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1075,9 +1013,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       }
     }
   } else {
-    // SCH == 3 = this body with the weight operand in packed fragment order, loaded straight into
-    // registers (PK; see pk_wait): no B stages, no B LDS reads.
-    constexpr bool PK = SCH == 3;
     // SCH == 2: the SCH 0 schedule with the per-phase instruction overhead taken out of the
     // load half-phases (the half-phase in which a wave stages, waits and reads while its SIMD
     // partner runs its MFMA cluster): K-steps unrolled by two so the LDS buffer parity is a
@@ -1096,24 +1031,11 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
         rbA[par][kk] = sbase + par * 4 * HALF + (wr * 64 + l16) * 128 + ch;
         rbB[par][kk] = sbase + par * 4 * HALF + 2 * HALF + (wc * 32 + l16) * 128 + ch;
       }
-    // packed weight: this wave's first fragment of quadrant column nq at K-step 0 is fragment
-    // (nb, 0), nb = (weight row of the wave's 32-column slab) / 16; (j, kk) add j * KB + kk
-    const int KB = a.K / 32;
-    const auto rBp = out_rsrc(PK ? a.Bp : a.B, (uint32_t)((size_t)NB * a.K * 2));
-    const uint32_t voP = (uint32_t)lane * 16;
-    bf16x8 bpk[2][2][2][2];  // [buffer parity][nq][j][kk]
     // a unit's tile and the byte offsets of its four half-tile row blocks
-    struct LCur { int o0, o1, o2, o3, m0, n0, p0, p1; };
+    struct LCur { int o0, o1, o2, o3, m0, n0; };
     auto lcur_at = [&](int i) {
       LCur c;
       unit_tile<EPI>(a, ubase + i * ustride, c.m0, c.n0);
-      if constexpr (PK) {
-        const int r0 = c.n0 + wc * 32, r1 = c.n0 + (EPI == EPI_GEGLU ? a.F : 128) + wc * 32;
-        c.p0 = __builtin_amdgcn_readfirstlane((r0 / 16) * KB * 1024);
-        c.p1 = __builtin_amdgcn_readfirstlane((r1 / 16) * KB * 1024);
-      } else {
-        c.p0 = c.p1 = 0;
-      }
       c.o0 = __builtin_amdgcn_readfirstlane(c.m0 * a.lda * 2);
       c.o1 = __builtin_amdgcn_readfirstlane((c.m0 + 128) * a.lda * 2);
       // weight rows of the two B halves: n0 + [0, 128) and n0 + [128, 256); GeGLU: the g1 rows
@@ -1134,18 +1056,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       for (int p = 0; p < 2; ++p)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rA : rB, (lds_t*)(d + (p * 64 + wave * 8) * 128),
                                                  16, (h < 2 ? voA[p] : voB[p]) + toff, 0, 0, 0);
-    };
-    // the 4 fragments (j, kk) of quadrant column nq, K-step k (>= KT: the next unit's), into set par
-    auto lloadB = [&](const LCur& cur, const LCur& nxt, int k, auto par_c, auto nq_c) {
-      constexpr int par = decltype(par_c)::value, nq = decltype(nq_c)::value;
-      const int base = k < KT ? (nq ? cur.p1 : cur.p0) + k * 2048 : (nq ? nxt.p1 : nxt.p0) + (k - KT) * 2048;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          bpk[par][nq][j][kk] = __builtin_bit_cast(
-              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                          rBp, voP + kk * 1024, (uint32_t)__builtin_amdgcn_readfirstlane(base + j * KB * 1024), 0));
     };
     auto rd16 = [](uint32_t addr, auto off_c) {
       constexpr int off = decltype(off_c)::value;
@@ -1286,10 +1196,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
                             : (role == 0 ? 8 : role == 1 ? 8 + (p >= 2 ? GS : 0) : 8 + (p < 2 ? 2 * GS : GS));
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(n));
     };
-    auto pwait = [&](auto phase_c, auto role_c) {
-      constexpr int p = decltype(phase_c)::value, role = decltype(role_c)::value;
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(pk_wait<EPI>(role, p)));
-    };
     auto lgkm0 = [&]() {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -1309,40 +1215,28 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       };
       f32x4 bj0, bj1;
       bf16x8 gv[4][2];
-      auto& b0 = PK ? bpk[par][0] : bf0;
-      auto& b1 = PK ? bpk[par][1] : bf1;
       // phase 0: quadrant (0,0)
       if constexpr (GB && role == 1) lgload(cur, 0, 0, gv);
-      if constexpr (PK) {
-        lloadB(cur, nxt, k + 1, Qc{}, I0{});
-        pwait(I0{}, role_c);
-      } else {
-        lstage(cur, nxt, k + 1, Qc{}, I3{});
-        lwait(I0{}, role_c);
-      }
+      lstage(cur, nxt, k + 1, Qc{}, I3{});
+      lwait(I0{}, role_c);
       lreadA(Pc{}, I0{});
-      if constexpr (!PK) lreadB(Pc{}, I0{}, bf0);
+      lreadB(Pc{}, I0{}, bf0);
       if constexpr (SB && role == 1) lbias(cur, 0, bj0, bj1);
       DNA_BARRIER();
       lgkm0();
-      mm(0, 0, b0);
+      mm(0, 0, bf0);
       if constexpr (SB && role == 1) lstore(cur, 0, 0, bj0, bj1);
       if constexpr (GB && role == 1) lgstore(cur, 0, 0, gv);
       DNA_BARRIER();
       // phase 1: quadrant (0,1)
       if constexpr (GB && role == 1) lgload(cur, 0, 1, gv);
       lstage(cur, nxt, k + 1, Qc{}, I1{});
-      if constexpr (PK) {
-        lloadB(cur, nxt, k + 1, Qc{}, I1{});
-        pwait(I1{}, role_c);
-      } else {
-        lwait(I1{}, role_c);
-        lreadB(Pc{}, I1{}, bf1);
-      }
+      lwait(I1{}, role_c);
+      lreadB(Pc{}, I1{}, bf1);
       if constexpr (SB && role == 1) lbias(cur, 1, bj0, bj1);
       DNA_BARRIER();
       lgkm0();
-      mm(0, 1, b1);
+      mm(0, 1, bf1);
       if constexpr (SB && role == 1) lstore(cur, 0, 1, bj0, bj1);
       if constexpr (GB && role == 1) lgstore(cur, 0, 1, gv);
       if constexpr (!SB && !GB && role == 1) store_geglu_half(cur, 0);
@@ -1350,26 +1244,22 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       // phase 2: quadrant (1,1)
       if constexpr (GB && role == 1) lgload(cur, 1, 1, gv);
       lstage(cur, nxt, k + 2, Pc{}, I0{});
-      if constexpr (!PK) lwait(I2{}, role_c);  // PK: A_1 was retired by phase 1's wait
+      lwait(I2{}, role_c);
       lreadA(Pc{}, I1{});
       DNA_BARRIER();
       lgkm0();
-      mm(1, 1, b1);
+      mm(1, 1, bf1);
       if constexpr (SB && role == 1) lstore(cur, 1, 1, bj0, bj1);
       if constexpr (GB && role == 1) lgstore(cur, 1, 1, gv);
       DNA_BARRIER();
       // phase 3: quadrant (1,0)
       if constexpr (GB && role == 1) lgload(cur, 1, 0, gv);
-      if constexpr (PK) {
-        pwait(I3{}, role_c);
-      } else {
-        lstage(cur, nxt, k + 2, Pc{}, I2{});
-        lwait(I3{}, role_c);
-      }
+      lstage(cur, nxt, k + 2, Pc{}, I2{});
+      lwait(I3{}, role_c);
       if constexpr (SB && role == 1) lbias(cur, 0, bj0, bj1);
       DNA_BARRIER();
       if constexpr (SB && role == 1) lgkm0();
-      mm(1, 0, b0);
+      mm(1, 0, bf0);
       if constexpr (SB && role == 1) lstore(cur, 1, 0, bj0, bj1);
       if constexpr (GB && role == 1) lgstore(cur, 1, 0, gv);
       if constexpr (!SB && !GB && role == 1) store_geglu_half(cur, 1);
@@ -1382,16 +1272,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     using RF = std::integral_constant<int, 2>;
     // KT is even (launcher), so every unit starts on buffer parity 0
     LCur cur = lcur_at(0), nxt = lcur_at(nb > 1 ? 1 : 0);
-    if constexpr (PK) {
-      // prologue = the VMEM issues of "step -1" (see pk_wait): A_0(0), B_nq0(0), A_1(0),
-      // B_nq1(0), A_0(1); the wait retires A_0(0)
-      lstage(cur, nxt, 0, I0{}, I0{});
-      lloadB(cur, nxt, 0, I0{}, I0{});
-      lstage(cur, nxt, 0, I0{}, I1{});
-      lloadB(cur, nxt, 0, I0{}, I1{});
-      lstage(cur, nxt, 1, I1{}, I0{});
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(12));
-    } else {
     // prologue (as SCH 0): all four halves of step 0, A_0 / B_0 of step 1
     lstage(cur, nxt, 0, I0{}, I0{});
     lstage(cur, nxt, 0, I0{}, I2{});
@@ -1400,7 +1280,6 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     lstage(cur, nxt, 1, I1{}, I0{});
     lstage(cur, nxt, 1, I1{}, I2{});
     __builtin_amdgcn_s_waitcnt(waitcnt_imm(8));
-    }
     DNA_BARRIER();
     if (wr == 1) DNA_BARRIER();  // stagger: waves 4-7 one barrier behind
     lstep(I0{}, R0{}, ZY{}, 0, cur, nxt);
@@ -1974,15 +1853,6 @@ int launchp(Args& a, hipStream_t s, const char* name) {
   if (const char* e = getenv("DNA_GEMM_ORDER")) a.order = atoi(e);
   const char* ab = getenv("DNA_GEMM_ABL");
   const int abl = ab ? atoi(ab) : 0;
-  if constexpr (EPI == EPI_BF16) {
-    // packed weight (SCH 3) unless DNA_GEMM_PK=0 (A/B)
-    const char* pk = getenv("DNA_GEMM_PK");
-    if (a.Bp && abl == 0 && (a.K / BK) % 2 == 0 && !(pk && pk[0] == '0')) {
-      hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 3>), dim3(G), dim3(NTHR), 0, s, a);
-      DNA_LAUNCH_CHECK(name);
-      return DNA_OK;
-    }
-  }
   if (abl == 0 && gemm_sched() == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 1>), dim3(G), dim3(NTHR), 0, s, a);
   else if (abl == 0 && gemm_sched() == 2 && (a.K / BK) % 2 == 0)
     hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 2>), dim3(G), dim3(NTHR), 0, s, a);
@@ -2036,8 +1906,8 @@ inline Args base_args() {
 using namespace dna;
 using namespace dna::gemm;
 
-static int linear_fwd_impl(const void* x, const void* w, const void* wp, const float* bias, int M,
-                           int N, int K, void* y, void* stream) {
+extern "C" int dna_linear_fwd(const void* x, const void* w, const float* bias, int M, int N, int K,
+                              void* y, void* stream) {
   DNA_CHECK_ARG(x && w && y, "dna_linear_fwd: null pointer");
   DNA_CHECK_ARG(M >= 0 && N > 0 && K > 0, "dna_linear_fwd: bad shape");
   DNA_CHECK_ARG(K % BK == 0 && N % 8 == 0, "dna_linear_fwd: K %% 64 and N %% 8 required (K=%d N=%d)", K, N);
@@ -2045,7 +1915,6 @@ static int linear_fwd_impl(const void* x, const void* w, const void* wp, const f
   Args a = base_args();
   a.A = (const bf16*)x; a.lda = K;
   a.B = (const bf16*)w; a.ldb = K;
-  a.Bp = (const bf16*)wp;
   a.C = y; a.ldc = N; a.bias = bias;
   a.M = M; a.N = N; a.K = K; a.ksplit = K;
   if (persistent_enabled() && N <= BIAS_LDS / 4 && N % BN == 0 && K >= 2 * BK &&
@@ -2069,30 +1938,6 @@ static int linear_fwd_impl(const void* x, const void* w, const void* wp, const f
     }
   }
   return launch<true, true, EPI_BF16>(a, 1, as_stream(stream), "dna_linear_fwd");
-}
-
-extern "C" int dna_linear_fwd(const void* x, const void* w, const float* bias, int M, int N, int K,
-                              void* y, void* stream) {
-  return linear_fwd_impl(x, w, nullptr, bias, M, N, K, y, stream);
-}
-
-// as dna_linear_fwd, the persistent kernel reading the weight from its packed fragment copy
-// wp (dna_pack_frag_bf16 of w) straight into registers; w itself serves the other paths
-extern "C" int dna_linear_fwd_pk(const void* x, const void* w, const void* wp, const float* bias,
-                                 int M, int N, int K, void* y, void* stream) {
-  DNA_CHECK_ARG(wp, "dna_linear_fwd_pk: null packed weight");
-  return linear_fwd_impl(x, w, wp, bias, M, N, K, y, stream);
-}
-
-extern "C" int dna_pack_frag_bf16(const void* src, int R, int C, int trans, void* dst, void* stream) {
-  DNA_CHECK_ARG(src && dst, "dna_pack_frag_bf16: null pointer");
-  DNA_CHECK_ARG(R > 0 && C > 0 && R % 16 == 0 && C % 32 == 0,
-                "dna_pack_frag_bf16: R %% 16 and C %% 32 required (R=%d C=%d)", R, C);
-  const size_t n = (size_t)R * C / 8;
-  hipLaunchKernelGGL(pack_frag_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), (const bf16*)src, R, C, trans, (bf16*)dst);
-  DNA_LAUNCH_CHECK("dna_pack_frag_bf16");
-  return DNA_OK;
 }
 
 extern "C" int dna_linear_dgrad(const void* dy, const void* w, int M, int N, int K, void* dx,
@@ -2124,9 +1969,9 @@ extern "C" int dna_linear_wgrad(const void* dy, const void* x, int M, int N, int
   return launch<false, false, EPI_F32>(a, splits, as_stream(stream), "dna_linear_wgrad");
 }
 
-static int geglu_linear_fwd_impl(const void* x, const void* w, const void* wp, const float* bias,
-                                 int M, int F, int K, float p_drop, uint64_t seed, uint64_t offset,
-                                 void* g, void* out, void* stream) {
+extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* bias, int M, int F,
+                                    int K, float p_drop, uint64_t seed, uint64_t offset, void* g,
+                                    void* out, void* stream) {
   DNA_CHECK_ARG(x && w && g && out, "dna_geglu_linear_fwd: null pointer");
   DNA_CHECK_ARG(M >= 0 && K % BK == 0 && F % (BN / 2) == 0,
                 "dna_geglu_linear_fwd: K %% 64 and F %% 128 required (K=%d F=%d)", K, F);
@@ -2136,7 +1981,6 @@ static int geglu_linear_fwd_impl(const void* x, const void* w, const void* wp, c
   a.A = (const bf16*)x; a.lda = K;
   a.B = (const bf16*)w; a.ldb = K;
   a.C = g; a.ldc = 2 * F; a.bias = bias; a.aux = (bf16*)out;
-  a.Bp = (const bf16*)wp;
   a.M = M; a.N = F; a.K = K; a.ksplit = K; a.F = F;
   a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
   a.seed = seed; a.off = offset;
@@ -2160,19 +2004,6 @@ static int geglu_linear_fwd_impl(const void* x, const void* w, const void* wp, c
     }
   }
   return launch<true, true, EPI_GEGLU>(a, 1, as_stream(stream), "dna_geglu_linear_fwd");
-}
-
-extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* bias, int M, int F,
-                                    int K, float p_drop, uint64_t seed, uint64_t offset, void* g,
-                                    void* out, void* stream) {
-  return geglu_linear_fwd_impl(x, w, nullptr, bias, M, F, K, p_drop, seed, offset, g, out, stream);
-}
-
-extern "C" int dna_geglu_linear_fwd_pk(const void* x, const void* w, const void* wp, const float* bias,
-                                       int M, int F, int K, float p_drop, uint64_t seed,
-                                       uint64_t offset, void* g, void* out, void* stream) {
-  DNA_CHECK_ARG(wp, "dna_geglu_linear_fwd_pk: null packed weight");
-  return geglu_linear_fwd_impl(x, w, wp, bias, M, F, K, p_drop, seed, offset, g, out, stream);
 }
 
 extern "C" int dna_geglu_linear_dgrad(const void* dy, const void* w, const void* g, int M, int F,
