@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--L", type=int, default=131072)
     ap.add_argument("--N", type=int, default=16)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--ab", default="", help="ENV=V1,V2: time the backward under each value, interleaved")
     a = ap.parse_args()
     B, D, L, N = a.B, a.D, a.L, a.N
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -56,6 +57,15 @@ def main():
         o = selective_scan_fn(*ins[:5], D=ins[5], z=ins[6], delta_bias=ins[7], delta_softplus=True)
         o.backward(dout)
     t_fb = timeit(fb, a.iters)
+    if a.ab:
+        var, vals = a.ab.split("=")
+        res = {v: [] for v in vals.split(",")}
+        for _ in range(3):
+            for v in res:
+                os.environ[var] = v
+                res[v].append(timeit(fb, a.iters) - t_f)
+        os.environ.pop(var, None)
+        print("A/B bwd us:", {v: [round(x, 1) for x in ts] for v, ts in res.items()}, flush=True)
     s = 2
     fb_bytes = (4 * B * D * L + 2 * B * N * L) * s
     bb_bytes = (7 * B * D * L + 2 * B * N * L) * s + 2 * B * N * L * 4
