@@ -17,7 +17,6 @@
 // dB, dC (shared by all channels of a batch: fp32 atomics).
 // Everything in fp32; u/delta/z/B/C/out in fp32 or bf16.
 #include <math.h>
-#include <stdlib.h>
 
 #include "common.h"
 
@@ -768,240 +767,6 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
   }
 }
 
-// 8 consecutive positions of one channel in their storage type (16 B for bf16, 32 B for fp32),
-// loaded a channel ahead of their use; zero past `len`
-template <typename T>
-struct Raw8 {
-  static constexpr int NW = ITEMS * (int)sizeof(T) / 4;  // 32-bit words
-  uint32_t wd[NW];
-  __device__ __forceinline__ void load(const T* p, int pos, int len) {
-    if (pos + ITEMS <= len && (reinterpret_cast<uintptr_t>(p + pos) & 15) == 0) {
-#pragma unroll
-      for (int k = 0; k < NW / 4; ++k) {
-        const uint4 q = reinterpret_cast<const uint4*>(p + pos)[k];
-        wd[4 * k] = q.x; wd[4 * k + 1] = q.y; wd[4 * k + 2] = q.z; wd[4 * k + 3] = q.w;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) set(i, (pos + i < len) ? to_f32(p[pos + i]) : 0.f);
-    }
-  }
-  __device__ __forceinline__ void set(int i, float x) {
-    if constexpr (sizeof(T) == 2) {
-      const uint32_t h = (uint32_t)__builtin_bit_cast(unsigned short, (bf16)x);
-      wd[i / 2] = (i & 1) ? ((wd[i / 2] & 0xFFFFu) | (h << 16)) : ((wd[i / 2] & 0xFFFF0000u) | h);
-    } else {
-      wd[i] = __float_as_uint(x);
-    }
-  }
-  __device__ __forceinline__ float operator[](int i) const {
-    if constexpr (sizeof(T) == 2) return __uint_as_float((i & 1) ? (wd[i / 2] & 0xFFFF0000u) : (wd[i / 2] << 16));
-    else return __uint_as_float(wd[i]);
-  }
-  // element i for a wave-uniform runtime i: a select chain (a dynamic index goes to scratch)
-  __device__ __forceinline__ float pick(int i) const {
-    float r = (*this)[0];
-#pragma unroll
-    for (int k = 1; k < ITEMS; ++k) r = i == k ? (*this)[k] : r;
-    return r;
-  }
-};
-
-// Backward chunk kernel with the STATES split over the waves (N % CW == 0; default for N = 8, 16):
-// the block's 8 waves work on one channel at a time, wave w owning states n = w + CW*s, s < SPW.
-// Compared with chunk_bwd_kernel (one channel per wave, all N states, dB/dC accumulated with a
-// read-modify-write in LDS and a barrier after every state step):
-//  * dB[n, t] / dC[n, t] of a state get contributions from one wave only, so they accumulate in
-//    that wave's registers over all channels of the group and reach memory once per block
-//    (through LDS, as coalesced atomics) -- no LDS accumulator traffic in the state loop;
-//  * the per-position sums over states (dδ, du, y) are partials per wave, reduced through a
-//    double-buffered LDS image [dδ, du, y][wave][item][lane]: one barrier per channel, after which
-//    wave w finishes item w of every lane's 8 positions (lane*8 + w) from the inputs it already
-//    holds in registers -- a channel's u / δ / dout / z are loaded one channel ahead;
-//  * a wave's SPW states are independent chains, interleaved for ILP.
-template <typename T, int N>
-__global__ __launch_bounds__(CT) void chunk_bwd2_kernel(Args a, Chunked q) {
-  constexpr int SPW = N / CW;
-  static_assert(SPW >= 1 && N % CW == 0, "states split over the waves");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* Bs = reinterpret_cast<T*>(smem);                            // [N][CHUNK]
-  T* Cs = Bs + N * CHUNK;
-  float* red = reinterpret_cast<float*>(Cs + N * CHUNK);          // [2][3][CW][ITEMS][64]
-  float* wsm = red + 2 * 3 * CW * CHUNK;                          // [2][2][CW] dD / dbias partials
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
-  const int c = blockIdx.y, b = blockIdx.z;
-  const size_t nchN = (size_t)q.nch * N;
-  const float* hbuf = a.states + (size_t)a.batch * a.dim * nchN;
-  const int pos = c * CHUNK + lane * ITEMS;  // this lane's 8 positions
-  const int nchan = CW * q.k;
-  const int d0 = blockIdx.x * nchan;
-  Raw8<T> U, DR, GO, Z;  // the next channel's inputs
-  auto prefetch = [&](int j) {
-    const size_t off = (size_t)(b * a.dim + d0 + j) * a.len;
-    U.load((const T*)a.u + off, pos, a.len);
-    DR.load((const T*)a.delta + off, pos, a.len);
-    GO.load((const T*)a.dout + off, pos, a.len);
-    if (a.z) Z.load((const T*)a.z + off, pos, a.len);
-  };
-  prefetch(0);
-  stage<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
-  stage<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
-  __syncthreads();
-  float dBacc[SPW][ITEMS], dCacc[SPW][ITEMS];
-#pragma unroll
-  for (int s = 0; s < SPW; ++s)
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) dBacc[s][i] = dCacc[s][i] = 0.f;
-
-  // per-channel dD / ddelta_bias: the CW wave partials of channel j, summed in a fixed order
-  auto channel_sums = [&](int j) {
-    if (w == 0 && lane < 2) {
-      const float* sp = wsm + (j & 1) * 2 * CW + lane * CW;
-      float v = 0.f;
-#pragma unroll
-      for (int u = 0; u < CW; ++u) v += sp[u];
-      float* dst = lane == 0 ? a.dD : a.ddelta_bias;
-      if (dst) atomicAdd(dst + d0 + j, v);
-    }
-  };
-
-  for (int j = 0; j < nchan; ++j) {
-    const int d = d0 + j, ch = b * a.dim + d;
-    const size_t off = (size_t)ch * a.len;
-    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
-    const float Dd = a.D ? a.D[d] : 0.f;
-    const Raw8<T> u8 = U, dr8 = DR, go8 = GO, z8 = Z;
-    if (j + 1 < nchan) prefetch(j + 1);
-    float uu[ITEMS], dl[ITEMS], dy[ITEMS];
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      uu[i] = u8[i];
-      dl[i] = dr8[i];
-      dy[i] = a.z ? go8[i] * siluf(z8[i]) : go8[i];
-    }
-    prep_delta(dl, bias, a.softplus, pos, a.len);
-    float dlu[ITEMS], ddl[ITEMS], du[ITEMS], y[ITEMS], tl = 0.f;
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      dlu[i] = dl[i] * uu[i];
-      tl += dl[i];
-      ddl[i] = du[i] = y[i] = 0.f;
-    }
-#pragma unroll
-    for (int s = 0; s < SPW; ++s) {
-      const int n = w + CW * s;
-      const float An = a.A[d * N + n], An2 = An * LOG2E;
-      const float xc = a.states[(size_t)ch * nchN + (size_t)c * N + n];
-      const float hc = hbuf[(size_t)ch * nchN + (size_t)c * N + n];
-      float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
-      lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
-      lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
-      const float Pt = ex2(tl * An2);  // prod_i a_i, for both directions
-      float P = Pt, S = 0.f;
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        aa[i] = ex2(dl[i] * An2);
-        bb[i] = dlu[i] * Bv[i];
-        S = fmaf(aa[i], S, bb[i]);
-      }
-      scan_fwd(P, S, lane);
-      const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
-      const float xprev = fmaf(Pe, xc, Se);
-      float x = xprev;
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        x = fmaf(aa[i], x, bb[i]);
-        xs[i] = x;
-        y[i] = fmaf(Cv[i], x, y[i]);
-      }
-      float Pr = Pt, Sr = 0.f;
-#pragma unroll
-      for (int i = ITEMS - 1; i >= 0; --i) Sr = aa[i] * fmaf(Cv[i], dy[i], Sr);
-      scan_rev(Pr, Sr, lane);
-      const float Pn = shl1(Pr, 1.f), Sn = shl1(Sr, 0.f);
-      float h = fmaf(Pn, hc, Sn);
-      float dAn = 0.f;
-#pragma unroll
-      for (int i = ITEMS - 1; i >= 0; --i) {
-        const float g = fmaf(Cv[i], dy[i], h);
-        const float xm1 = i > 0 ? xs[i - 1] : xprev;
-        const float da = g * xm1 * aa[i];
-        ddl[i] = fmaf(da, An, ddl[i]);
-        dAn = fmaf(da, dl[i], dAn);
-        const float gb = g * dl[i];
-        ddl[i] = fmaf(g, Bv[i] * uu[i], ddl[i]);
-        du[i] = fmaf(gb, Bv[i], du[i]);
-        dBacc[s][i] = fmaf(gb, uu[i], dBacc[s][i]);
-        dCacc[s][i] = fmaf(dy[i], xs[i], dCacc[s][i]);
-        h = aa[i] * g;
-      }
-      const float dAs = wsum(dAn);
-      if (lane == 0) atomicAdd(a.dA + d * N + n, dAs);
-    }
-    // this wave's partials, item-major: [q][wave][i][lane] (64 consecutive floats per store)
-    float* R = red + (j & 1) * 3 * CW * CHUNK;
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      R[((0 * CW + w) * ITEMS + i) * 64 + lane] = ddl[i];
-      R[((1 * CW + w) * ITEMS + i) * 64 + lane] = du[i];
-      R[((2 * CW + w) * ITEMS + i) * 64 + lane] = y[i];
-    }
-    __syncthreads();
-    if (j > 0) channel_sums(j - 1);  // its wsm entries were written before this barrier
-    // wave w finishes item w of every lane: position lane*8 + w
-    {
-      float sddl = 0.f, sdu = 0.f, sy = 0.f;
-#pragma unroll
-      for (int v = 0; v < CW; ++v) {
-        sddl += R[((0 * CW + v) * ITEMS + w) * 64 + lane];
-        sdu += R[((1 * CW + v) * ITEMS + w) * 64 + lane];
-        sy += R[((2 * CW + v) * ITEMS + w) * 64 + lane];
-      }
-      const int p = pos + w;
-      const bool valid = p < a.len;
-      const float u_t = u8.pick(w), dr_t = dr8.pick(w), go_t = go8.pick(w), z_t = a.z ? z8.pick(w) : 0.f;
-      const float sz = a.z ? sigmoidf(z_t) : 1.f;
-      const float dy_t = a.z ? go_t * z_t * sz : go_t;
-      float g = sddl;
-      if (a.softplus) g *= sigmoidf(dr_t + bias);
-      const float dd = valid ? g : 0.f;
-      if (valid) {
-        ((T*)a.ddelta)[off + p] = from_f32<T>(dd);
-        ((T*)a.du)[off + p] = from_f32<T>(fmaf(Dd, dy_t, sdu));
-        if (a.z && a.dz) {
-          const float pre = fmaf(Dd, u_t, sy);
-          ((T*)a.dz)[off + p] = from_f32<T>(go_t * pre * sz * (1.f + z_t * (1.f - sz)));
-        }
-      }
-      const float dDp = wsum(dy_t * u_t), dbp = wsum(dd);
-      if (lane == 0) {
-        wsm[(j & 1) * 2 * CW + w] = dDp;
-        wsm[(j & 1) * 2 * CW + CW + w] = dbp;
-      }
-    }
-  }
-  __syncthreads();
-  channel_sums(nchan - 1);
-  // dB / dC of this wave's states: through LDS (the red image is free now), then coalesced atomics
-#pragma unroll
-  for (int mat = 0; mat < 2; ++mat) {
-#pragma unroll
-    for (int s = 0; s < SPW; ++s) {
-      const float* v = mat ? dCacc[s] : dBacc[s];
-      float* dst = red + (w + CW * s) * CHUNK + lane * ITEMS;
-      *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
-      *reinterpret_cast<f32x4*>(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
-    }
-    __syncthreads();
-    float* dM = (mat ? a.dC : a.dB) + (size_t)b * N * a.len;
-    for (int e = tid; e < N * CHUNK; e += CT) {
-      const int n = e / CHUNK, p = c * CHUNK + (e - n * CHUNK);
-      if (p < a.len) atomicAdd(dM + (size_t)n * a.len + p, red[e]);
-    }
-    __syncthreads();
-  }
-}
-
 inline Chunked plan_chunks(int batch, int dim, int len) {
   Chunked q;
   q.nch = (len + CHUNK - 1) / CHUNK;
@@ -1096,23 +861,11 @@ extern "C" int dna_selective_scan_bwd(const void* u, const void* delta, const fl
     using T = decltype(t);
     constexpr int NS = decltype(n)::value;
     if (chunked) {
-      hipLaunchKernelGGL((sum_bwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
-      hipLaunchKernelGGL((carry_kernel<NS>), dim3((batch * dim * NS + 255) / 256), dim3(256), 0, s, a, q, 1);
-      // states split over the waves for N >= 8 (DNA_SCAN_BWD=1: the one-channel-per-wave kernel)
-      const char* sel = getenv("DNA_SCAN_BWD");
-      // (fp32 B/C at N = 16 leave no room for the double-buffered partials in the 160 KiB LDS)
-      constexpr size_t bytes2 = (size_t)2 * NS * CHUNK * sizeof(T) + (size_t)(2 * 3 * CW * CHUNK + 4 * CW) * sizeof(float);
-      if constexpr (NS % CW == 0 && bytes2 <= 163840) {
-        if (!(sel && sel[0] == '1')) {
-          const size_t bytes = bytes2;
-          allow_lds(chunk_bwd2_kernel<T, NS>, bytes);
-          hipLaunchKernelGGL((chunk_bwd2_kernel<T, NS>), cgrid, dim3(CT), bytes, s, a, q);
-          return;
-        }
-      }
       constexpr int R = CW > NS ? CW / NS : 1;
       const size_t bytes = (size_t)2 * NS * CHUNK * (R * sizeof(float) + sizeof(T));
       allow_lds(chunk_bwd_kernel<T, NS>, bytes);
+      hipLaunchKernelGGL((sum_bwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
+      hipLaunchKernelGGL((carry_kernel<NS>), dim3((batch * dim * NS + 255) / 256), dim3(256), 0, s, a, q, 1);
       hipLaunchKernelGGL((chunk_bwd_kernel<T, NS>), cgrid, dim3(CT), bytes, s, a, q);
     } else {
       hipLaunchKernelGGL((bwd_kernel<T, NS>), dim3((batch * dim + WPB - 1) / WPB), dim3(64 * WPB),

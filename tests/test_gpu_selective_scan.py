@@ -68,35 +68,3 @@ def test_selective_scan_bf16(d):
                             z=z.to(DEV).bfloat16(), delta_bias=bias.to(DEV), delta_softplus=True)
     assert out.dtype == torch.bfloat16 and _rel(out.float().cpu(), ref.float()) < 3e-2
 
-
-@pytest.mark.parametrize("dtype,n,use_z", [(torch.bfloat16, 16, True), (torch.float32, 8, True),
-                                           (torch.bfloat16, 8, False)])
-def test_scan_bwd_state_split_kernel_matches_channel_kernel(dtype, n, use_z, monkeypatch):
-    """The backward chunk kernel with the states split over the waves (chunk_bwd2_kernel, the
-    default for d_state 8 / 16) against the one-channel-per-wave kernel (DNA_SCAN_BWD=1) and the
-    float64 oracle, ragged length (the last chunk partly past L), 3 channel groups."""
-    from dna_amd.mamba import selective_scan_fn
-    b, d, l = 2, 24, 1500
-    u, delta, A, B, C, D, z, bias = _inputs(b, d, l, n, seed=5 + n, dtype=dtype)
-    z = z if use_z else None
-    dout = torch.randn(b, d, l, generator=torch.Generator().manual_seed(3)).to(dtype)
-    grads = {}
-    for sel in ("0", "1"):
-        monkeypatch.setenv("DNA_SCAN_BWD", sel)
-        ins = [t.to(DEV).requires_grad_(True) if t is not None else None
-               for t in (u, delta, A, B, C, D, z, bias)]
-        out = selective_scan_fn(*ins[:5], D=ins[5], z=ins[6], delta_bias=ins[7], delta_softplus=True)
-        out.backward(dout.to(DEV))
-        grads[sel] = [t.grad.float().cpu() if t is not None else None for t in ins]
-    ref_in = [t.double().requires_grad_(True) if t is not None else None
-              for t in (u, delta, A, B, C, D, z, bias)]
-    ref = selective_scan_ref(*ref_in[:5], D=ref_in[5], z=ref_in[6], delta_bias=ref_in[7],
-                             delta_softplus=True)
-    ref.backward(dout.double())
-    tol = 1e-3 if dtype == torch.float32 else 3e-2
-    for k, name in enumerate(("u", "delta", "A", "B", "C", "D", "z", "bias")):
-        if grads["0"][k] is None:
-            continue
-        assert _rel(grads["0"][k], ref_in[k].grad) < tol, name
-        # the two kernels sum in different orders: equal to fp32 / bf16 rounding
-        assert _rel(grads["0"][k], grads["1"][k]) < (1e-4 if dtype == torch.float32 else 1e-2), name
