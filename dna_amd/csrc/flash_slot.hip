@@ -18,7 +18,10 @@
 // 2D+16 bytes: row reads by 16 lanes of consecutive rows are conflict-free); MFMA
 // v_mfma_f32_16x16x32_{bf16,f16}; P / dS pass from the accumulator layout to an A operand
 // through a per-wave LDS image; the column-direction operands (V, dO, Q, K) come from
-// ds_read_b64_tr_b16 transposed reads of the row-major tiles.
+// ds_read_b64_tr_b16 transposed reads of the row-major tiles. A matrix bias is staged through LDS
+// one 64 x 64 tile per (query block, key block) with 16-B loads (stage_bias).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace dna {
@@ -116,9 +119,68 @@ __device__ __forceinline__ float bias_v(const Args& a, long long base, int q, in
     return 0.f;
   } else {
     if (q >= a.S || k >= a.S) return 0.f;
-    const long long off = base + (BT == 2 ? (long long)q * a.sq : 0) + k;
+    const long long off = base + (BT >= 2 ? (long long)q * a.sq : 0) + k;
     return a.bias_f32 ? reinterpret_cast<const float*>(a.bias)[off]
                       : Mf<T>::val(reinterpret_cast<const unsigned short*>(a.bias)[off]);
+  }
+}
+
+// Matrix bias staged through LDS (BT == 3: a [b?, H?, S, S] bias whose base and strides keep every
+// row 16-B aligned): the 64 x 64 tile of the (query block, key block) pair is read with 16-B loads,
+// converted to fp32 and kept at row stride BLD = 68 floats (rows 4 apart sit 16 banks apart, so
+// every score read -- 16 consecutive columns x 4 row groups -- is conflict-free). TR stores it
+// [key][query] for the dK/dV kernel, whose lanes walk queries. Out-of-range entries are 0.
+constexpr int BLD = 68;
+constexpr int BIAS_TILE = BR * BLD * 4;  // bytes
+template <typename T, bool TR>
+__device__ __forceinline__ void stage_bias(float* t, const Args& a, long long base, int q0, int k0,
+                                           int tid) {
+  auto put = [&](int qq, int kk, const float (&v)[8], int n) {
+    if constexpr (TR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (e < n) t[(kk + e) * BLD + qq] = v[e];
+    } else {
+      *reinterpret_cast<f32x4*>(t + qq * BLD + kk) = f32x4{v[0], v[1], v[2], v[3]};
+      if (n == 8) *reinterpret_cast<f32x4*>(t + qq * BLD + kk + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  };
+  if (a.bias_f32) {
+    const float* B = reinterpret_cast<const float*>(a.bias);
+    for (int c = tid; c < BR * 16; c += NT) {  // 16 chunks of 4 per row
+      const int qq = c >> 4, kk = (c & 15) * 4, q = q0 + qq, k = k0 + kk;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (q < a.S) {
+        const float* p = B + base + (long long)q * a.sq + k;
+        if (k + 3 < a.S) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+          v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = k + e < a.S ? p[e] : 0.f;
+        }
+      }
+      put(qq, kk, v, 4);
+    }
+  } else {
+    const unsigned short* B = reinterpret_cast<const unsigned short*>(a.bias);
+    for (int c = tid; c < BR * 8; c += NT) {  // 8 chunks of 8 per row
+      const int qq = c >> 3, kk = (c & 7) * 8, q = q0 + qq, k = k0 + kk;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (q < a.S) {
+        const unsigned short* p = B + base + (long long)q * a.sq + k;
+        if (k + 7 < a.S) {
+          const uint4 x = *reinterpret_cast<const uint4*>(p);
+          const unsigned short* h = reinterpret_cast<const unsigned short*>(&x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = Mf<T>::val(h[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = k + e < a.S ? Mf<T>::val(p[e]) : 0.f;
+        }
+      }
+      put(qq, kk, v, 8);
+    }
   }
 }
 
@@ -139,11 +201,12 @@ template <typename T, int D, int BT>
 __global__ __launch_bounds__(NT) void fwd_kernel(Args a) {
   using V8 = typename Mf<T>::v8;
   constexpr int KK = D / 32, NTL = D / 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BR * rs<D>() + 4 * 16 * PRS];
+  __shared__ __attribute__((aligned(16))) char smem[2 * BR * rs<D>() + 4 * 16 * PRS + (BT == 3 ? BIAS_TILE : 0)];
   char* Kt = smem;
   char* Vt = smem + BR * rs<D>();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   char* Pw = smem + 2 * BR * rs<D>() + w * 16 * PRS;
+  float* btile = reinterpret_cast<float*>(smem + 2 * BR * rs<D>() + 4 * 16 * PRS);
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
   const int q0 = blockIdx.x * BR;
   const long long HD = (long long)a.H * D, ld = 3 * HD;
@@ -176,6 +239,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(Args a) {
     __syncthreads();
     load_tile<D>(Kt, qg + HD, ld, k0, a.S, tid);
     load_tile<D>(Vt, qg + 2 * HD, ld, k0, a.S, tid);
+    if constexpr (BT == 3) stage_bias<T, false>(btile, a, bbase, q0, k0, tid);
     __syncthreads();
     f32x4 s[4];
 #pragma unroll
@@ -195,7 +259,8 @@ __global__ __launch_bounds__(NT) void fwd_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = qrow + r;
-        float x = s[j][r] * sl2 + bias_v<T, BT>(a, bbase, q, k) * LOG2E;
+        const float bv = BT == 3 ? btile[(q - q0) * BLD + (k - k0)] : bias_v<T, BT>(a, bbase, q, k);
+        float x = s[j][r] * sl2 + bv * LOG2E;
         if (k >= a.S || (a.causal && k > q)) x = -INFINITY;
         s[j][r] = x;
         mx[r] = fmaxf(mx[r], x);
@@ -282,7 +347,8 @@ template <typename T, int D, int BT>
 __global__ __launch_bounds__(NT) void dkdv_kernel(Args a) {
   using V8 = typename Mf<T>::v8;
   constexpr int KK = D / 32, NTL = D / 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BR * rs<D>() + 8 * 16 * PRS + 2 * BR * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * BR * rs<D>() + 8 * 16 * PRS + 2 * BR * 4 + (BT == 3 ? BIAS_TILE : 0)];
+  float* btile = reinterpret_cast<float*>(smem + 2 * BR * rs<D>() + 8 * 16 * PRS + 2 * BR * 4);
   char* Qt = smem;
   char* Gt = smem + BR * rs<D>();  // dO tile
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -323,6 +389,7 @@ __global__ __launch_bounds__(NT) void dkdv_kernel(Args a) {
     __syncthreads();
     load_tile<D>(Qt, qg, ld, q0, a.S, tid);
     load_tile<D>(Gt, gg, HD, q0, a.S, tid);
+    if constexpr (BT == 3) stage_bias<T, true>(btile, a, bbase, q0, k0, tid);
     if (tid < BR) {
       const int q = q0 + tid;
       lse_t[tid] = q < a.S ? a.lse[(long long)bh * a.Sr + q] * LOG2E : INFINITY;
@@ -349,7 +416,8 @@ __global__ __launch_bounds__(NT) void dkdv_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int k = krow + r;
-        float p = exp2f(s[j][r] * sl2 + bias_v<T, BT>(a, bbase, q, k) * LOG2E - lq);
+        const float bv = BT == 3 ? btile[(k - k0) * BLD + ql] : bias_v<T, BT>(a, bbase, q, k);
+        float p = exp2f(s[j][r] * sl2 + bv * LOG2E - lq);
         if (a.causal && k > q) p = 0.f;
         const float ds = p * (dp[j][r] - dq) * a.scale;
         const int off = (4 * (lane >> 4) + r) * PRS + ql * 2;
@@ -399,11 +467,12 @@ template <typename T, int D, int BT>
 __global__ __launch_bounds__(NT) void dq_kernel(Args a) {
   using V8 = typename Mf<T>::v8;
   constexpr int KK = D / 32, NTL = D / 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BR * rs<D>() + 4 * 16 * PRS];
+  __shared__ __attribute__((aligned(16))) char smem[2 * BR * rs<D>() + 4 * 16 * PRS + (BT == 3 ? BIAS_TILE : 0)];
   char* Kt = smem;
   char* Vt = smem + BR * rs<D>();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   char* Sw = smem + 2 * BR * rs<D>() + w * 16 * PRS;
+  float* btile = reinterpret_cast<float*>(smem + 2 * BR * rs<D>() + 4 * 16 * PRS);
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
   const int q0 = blockIdx.x * BR;
   const long long HD = (long long)a.H * D, ld = 3 * HD;
@@ -445,6 +514,7 @@ __global__ __launch_bounds__(NT) void dq_kernel(Args a) {
     __syncthreads();
     load_tile<D>(Kt, qg + HD, ld, k0, a.S, tid);
     load_tile<D>(Vt, qg + 2 * HD, ld, k0, a.S, tid);
+    if constexpr (BT == 3) stage_bias<T, false>(btile, a, bbase, q0, k0, tid);
     __syncthreads();
     f32x4 s[4], dp[4];
 #pragma unroll
@@ -465,7 +535,8 @@ __global__ __launch_bounds__(NT) void dq_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = qrow + r;
-        float p = exp2f(s[j][r] * sl2 + bias_v<T, BT>(a, bbase, q, k) * LOG2E - lq[r]);
+        const float bv = BT == 3 ? btile[(q - q0) * BLD + kl] : bias_v<T, BT>(a, bbase, q, k);
+        float p = exp2f(s[j][r] * sl2 + bv * LOG2E - lq[r]);
         if (k >= a.S || (a.causal && k > q)) p = 0.f;
         *reinterpret_cast<unsigned short*>(Sw + (4 * (lane >> 4) + r) * PRS + kl * 2) =
             Mf<T>::bits(p * (dp[j][r] - dq_[r]) * a.scale);
@@ -502,9 +573,19 @@ __global__ __launch_bounds__(NT) void dq_kernel(Args a) {
 template <typename T, int D>
 int run(bool bwd, const Args& a, int bias_type, hipStream_t s) {
   const dim3 grid((a.S + BR - 1) / BR, a.B * a.H);
+  // a matrix bias whose rows all start 16-B aligned is staged tile by tile through LDS (BT 3);
+  // DNA_FLASH_BIAS_DIRECT=1 keeps the per-score global reads (A/B)
+  if (bias_type == 2) {
+    const long long vec = a.bias_f32 ? 4 : 8;
+    const char* e = getenv("DNA_FLASH_BIAS_DIRECT");
+    if (((uintptr_t)a.bias & 15) == 0 && a.sb % vec == 0 && a.sh % vec == 0 && a.sq % vec == 0 &&
+        !(e && e[0] == '1'))
+      bias_type = 3;
+  }
   if (!bwd) {
     if (bias_type == 0) hipLaunchKernelGGL((fwd_kernel<T, D, 0>), grid, dim3(NT), 0, s, a);
     else if (bias_type == 1) hipLaunchKernelGGL((fwd_kernel<T, D, 1>), grid, dim3(NT), 0, s, a);
+    else if (bias_type == 3) hipLaunchKernelGGL((fwd_kernel<T, D, 3>), grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((fwd_kernel<T, D, 2>), grid, dim3(NT), 0, s, a);
     return DNA_OK;
   }
@@ -516,6 +597,9 @@ int run(bool bwd, const Args& a, int bias_type, hipStream_t s) {
   } else if (bias_type == 1) {
     hipLaunchKernelGGL((dkdv_kernel<T, D, 1>), grid, dim3(NT), 0, s, a);
     hipLaunchKernelGGL((dq_kernel<T, D, 1>), grid, dim3(NT), 0, s, a);
+  } else if (bias_type == 3) {
+    hipLaunchKernelGGL((dkdv_kernel<T, D, 3>), grid, dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((dq_kernel<T, D, 3>), grid, dim3(NT), 0, s, a);
   } else {
     hipLaunchKernelGGL((dkdv_kernel<T, D, 2>), grid, dim3(NT), 0, s, a);
     hipLaunchKernelGGL((dq_kernel<T, D, 2>), grid, dim3(NT), 0, s, a);
