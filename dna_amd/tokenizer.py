@@ -144,6 +144,16 @@ class CharacterTokenizer:
         return [self.bos_token_id, self.eos_token_id, self.unk_token_id, self.pad_token_id,
                 self.cls_token_id, self.mask_token_id]
 
+    def complement_map(self):
+        """{id: id of the complementary base} over the whole vocabulary (A<->T, C<->G, either
+        case when both are characters; every other id maps to itself) -- the `complement_map` a
+        Caduceus rcps=True model takes (RCPSEmbedding / RCPSLMHead, reference
+        src/models/caduceus/modeling_rcps.py:18-64, :206-243)."""
+        pairs = {"A": "T", "T": "A", "C": "G", "G": "C", "a": "t", "t": "a", "c": "g", "g": "c"}
+        v = self._vocab_str_to_int
+        return {i: v.get(pairs.get(s, s), i) if s in pairs else i
+                for s, i in sorted(v.items(), key=lambda kv: kv[1])}
+
     def encode_raw(self, text):
         b = np.frombuffer(text.encode("latin-1", errors="replace"), dtype=np.uint8)
         return self._lut[b].tolist()

@@ -25,6 +25,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dna_amd.caduceus import CaduceusForMaskedLM  # noqa: E402
 from dna_amd.functional import OpTimer  # noqa: E402
+from dna_amd.tokenizer import CharacterTokenizer  # noqa: E402
 from dna_amd.trainer import ModuleTrainer  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0
@@ -44,6 +45,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--rcps", action="store_true",
+                    help="RC-equivariant variant (RCPS layers, 2*d_model hidden channels)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -61,8 +64,9 @@ def main():
             dist.init_process_group(backend)
     torch.manual_seed(0)
     n_state = 16
+    cm = CharacterTokenizer("ACGTN", a.L + 2).complement_map() if a.rcps else None
     m = CaduceusForMaskedLM(d_model=a.d_model, n_layer=a.layers, vocab_size=12,
-                            ssm_cfg={"d_state": n_state})
+                            ssm_cfg={"d_state": n_state}, rcps=a.rcps, complement_map=cm)
     loss_fn = lambda model, batch: model(batch[0], labels=batch[1])[0]
     tr = ModuleTrainer(m, torch.device("cuda", local), loss_fn, lr=8e-3, weight_decay=0.1,
                        max_grad_norm=1.0, wire_dtype=a.wire)
@@ -127,7 +131,7 @@ def main():
             "config": {"workload": "Caduceus bi-Mamba MLM (BASELINE configs[4])",
                        "d_model": a.d_model, "n_layer": a.layers, "d_state": n_state,
                        "seq_len": a.L, "per_gpu_batch": a.B, "parallelism": f"dp{world}",
-                       "grad_wire": a.wire},
+                       "grad_wire": a.wire, "rcps": a.rcps},
             "final_loss": round(float(loss.item()), 4),
             "hip_kernel_share": round(sum(total.values()) / (el * 1e3), 4),
             "roofline": roof, "kernels": kernels}

@@ -1,5 +1,5 @@
-"""CPU: Caduceus MLM (rcps=False) structure -- reference parameter names, tied head, vocab
-padding, unsupported options raise. GPU parity vs the float64 oracle: tests/test_gpu_caduceus.py."""
+"""CPU: Caduceus MLM structure (rcps=False and the RCPS variant) -- reference parameter names,
+tied head, vocab padding, unsupported options raise; the RCPS oracle's RC equivariance. GPU parity vs the float64 oracle: tests/test_gpu_caduceus.py."""
 import pytest
 import torch
 
@@ -18,8 +18,6 @@ def test_caduceus_structure():
         assert k in keys, k
     m2 = m.caduceus.backbone.layers[0].mixer
     assert m2.mamba_rev.in_proj.weight is m2.mamba_fwd.in_proj.weight
-    with pytest.raises(NotImplementedError):
-        CaduceusForMaskedLM(d_model=64, n_layer=1, vocab_size=12, rcps=True)
     with pytest.raises(TypeError):
         CaduceusForMaskedLM(d_model=64, n_layer=1, vocab_size=12, not_a_key=1)
     with pytest.raises(RuntimeError):  # no CPU fallback
@@ -52,3 +50,92 @@ def test_caduceus_oracle_c_scan_equals_python_scan():
     assert ga.keys() == gb.keys() and len(ga) > 10
     for k in ga:
         assert torch.allclose(ga[k], gb[k], rtol=1e-9, atol=1e-12), k
+
+
+CM = {0: 0, 1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 10, 8: 9, 9: 8, 10: 7, 11: 11}  # A<->T, C<->G
+
+
+def _rcps_sd(m):
+    """float64 leaves of the model's state_dict with the tied tensors sharing one leaf."""
+    sd = {k: (v.detach().double().clone().requires_grad_(True) if v.is_floating_point() else v)
+          for k, v in m.state_dict().items()}
+    sd["lm_head.lm_head.weight"] = sd["caduceus.backbone.embeddings.word_embeddings.embedding.weight"]
+    for i in range(m.config["n_layer"]):
+        p = f"caduceus.backbone.layers.{i}.mixer.submodule."
+        for k in ("in_proj.weight", "out_proj.weight"):
+            sd[p + "mamba_rev." + k] = sd[p + "mamba_fwd." + k]
+    return sd
+
+
+def test_caduceus_rcps_structure():
+    """rcps=True: reference parameter / buffer names (modeling_rcps.py), the complement map padded
+    with identity ids to the padded vocabulary, head tied to the embedding, config errors."""
+    from dna_amd.caduceus import CaduceusForMaskedLM
+    for fused in (True, False):
+        m = CaduceusForMaskedLM(d_model=16, n_layer=2, vocab_size=12, rcps=True, complement_map=CM,
+                                fused_add_norm=fused, ssm_cfg={"d_state": 8})
+        emb = m.caduceus.backbone.embeddings.word_embeddings
+        assert m.lm_head.weight is emb.weight and emb.weight.shape == (16, 16)
+        assert emb.complement_map.tolist() == [CM[i] for i in range(12)] + [12, 13, 14, 15]
+        assert torch.equal(m.lm_head.complement_map, emb.complement_map)
+        keys = set(m.state_dict())
+        norm = "norm." if fused else "norm.submodule."
+        for k in ("caduceus.backbone.embeddings.word_embeddings.embedding.weight",
+                  "caduceus.backbone.embeddings.word_embeddings.complement_map",
+                  "caduceus.backbone.layers.1.mixer.submodule.mamba_fwd.A_log",
+                  "caduceus.backbone.layers.0.mixer.submodule.mamba_rev.conv1d.weight",
+                  f"caduceus.backbone.layers.0.{norm}weight", f"caduceus.backbone.{'norm_f.' if fused else 'norm_f.submodule.'}weight",
+                  "lm_head.lm_head.weight", "lm_head.complement_map"):
+            assert k in keys, k
+    with pytest.raises(ValueError):
+        CaduceusForMaskedLM(d_model=16, n_layer=1, vocab_size=12, rcps=True)   # no complement map
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_caduceus_rcps_oracle_is_rc_equivariant(fused):
+    """The float64 RCPS restatement is reverse-complement equivariant:
+    logits(rc(x))[t, v] == logits(x)[L-1-t, comp(v)] -- the property RCPS is built for, here
+    checked on the oracle the GPU parity test compares against."""
+    from dna_amd.caduceus import CaduceusForMaskedLM
+    from oracle import caduceus_ref as CR
+    torch.manual_seed(5)
+    m = CaduceusForMaskedLM(d_model=16, n_layer=2, vocab_size=12, rcps=True, complement_map=CM,
+                            fused_add_norm=fused, ssm_cfg={"d_state": 8})
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+    sd = _rcps_sd(m)
+    cm = sd["lm_head.complement_map"]
+    ids = torch.randint(4, 12, (2, 24), generator=torch.Generator().manual_seed(3))
+    dt_rank = m.caduceus.backbone.layers[0].mixer.submodule.mamba_fwd.dt_rank
+    a = CR.mlm_logits(sd, ids, 2, 8, 4, dt_rank, rcps=True, fused_add_norm=fused).detach()
+    b = CR.mlm_logits(sd, cm[ids.flip(-1)], 2, 8, 4, dt_rank, rcps=True, fused_add_norm=fused).detach()
+    assert torch.allclose(b, a.flip(1)[..., cm], rtol=1e-10, atol=1e-12)
+    assert (a - a.flip(1)[..., cm]).abs().max() > 1e-3   # not trivially symmetric
+
+
+def test_weighted_cross_entropy():
+    """modeling_caduceus.py:267-275: CE weighted by loss_weights renormalised over non-ignored
+    tokens; uniform weights == the plain mean CE; the caller's weights are left untouched."""
+    from dna_amd.caduceus import weighted_cross_entropy
+    g = torch.Generator().manual_seed(0)
+    logits = torch.randn(2, 7, 12, generator=g)
+    y = torch.randint(0, 12, (2, 7), generator=g)
+    y[0, :3] = -100
+    w = torch.ones(2, 7)
+    plain = torch.nn.functional.cross_entropy(logits.view(-1, 12), y.view(-1), ignore_index=-100)
+    assert torch.allclose(weighted_cross_entropy(logits, y, w), plain)
+    assert torch.equal(w, torch.ones(2, 7))
+    w = torch.rand(2, 7, generator=g)
+    ce = torch.nn.functional.cross_entropy(logits.view(-1, 12), y.view(-1), ignore_index=-100,
+                                           reduction="none")
+    keep = (y.view(-1) != -100).double()
+    ref = (ce.double() * w.view(-1).double() * keep).sum() / (w.view(-1).double() * keep).sum()
+    assert torch.allclose(weighted_cross_entropy(logits, y, w).double(), ref, rtol=1e-6)
+
+
+def test_char_tokenizer_complement_map():
+    from dna_amd.tokenizer import CharacterTokenizer
+    assert CharacterTokenizer("ACGTN", 10).complement_map() == CM
+    cm = CharacterTokenizer("ACGTNacgt", 10).complement_map()
+    assert cm[7] == 10 and cm[11] == 11 and cm[12] == 15 and cm[13] == 14

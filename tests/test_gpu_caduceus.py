@@ -1,4 +1,4 @@
-"""GPU: Caduceus MLM (rcps=False) logits and every gradient vs the float64 oracle
+"""GPU: Caduceus MLM (rcps=False and RCPS) logits and every gradient vs the float64 oracle
 (oracle/caduceus_ref.py; parity unpinned: mamba_ssm absent). fp32, tolerances fwd 1e-4, grads 2e-3."""
 import pytest
 import torch
@@ -73,3 +73,53 @@ def test_hip_rmsnorm_module(d, dtype):
         assert (yb.float() - yr.float().bfloat16().float()).abs().max() <= 2 ** -7 * yr.abs().max()
         yb.backward(dy.bfloat16())
         assert _rel(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("fused,rms", [(True, True), (False, True), (True, False)])
+def test_caduceus_rcps_vs_oracle(fused, rms):
+    """rcps=True (RCPSEmbedding / RCPSMambaBlock / RCPSLMHead) on the HIP mixers and norms vs the
+    float64 RCPS restatement: logits, every parameter gradient, and RC equivariance of the GPU
+    model itself (logits(rc(x))[t, v] == logits(x)[L-1-t, comp(v)])."""
+    from dna_amd.caduceus import CaduceusForMaskedLM
+    from test_caduceus import CM, _rcps_sd
+    torch.manual_seed(11)
+    m = CaduceusForMaskedLM(d_model=64, n_layer=2, vocab_size=12, rms_norm=rms, rcps=True,
+                            complement_map=CM, fused_add_norm=fused, ssm_cfg={"d_state": 16})
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(torch.randn_like(p) * 0.02)
+    sd = _rcps_sd(m)
+    m = m.to(DEV)
+    ids = torch.randint(0, 12, (2, 300), generator=torch.Generator().manual_seed(3))
+    dt_rank = m.caduceus.backbone.layers[0].mixer.submodule.mamba_fwd.dt_rank
+    ref = CR.mlm_logits(sd, ids, 2, 16, 4, dt_rank, rms_norm=rms, rcps=True, fused_add_norm=fused)
+    _, logits = m(ids.to(DEV))
+    assert _rel(logits, ref) < 1e-4
+    g = torch.randn(ref.shape, generator=torch.Generator().manual_seed(4), dtype=torch.float64)
+    ref.backward(g)
+    logits.backward(g.float().to(DEV))
+    for n, p in m.named_parameters():
+        assert _rel(p.grad, sd[n].grad) < 2e-3, n
+    cm = m.lm_head.complement_map
+    with torch.no_grad():
+        ids_d = ids.to(DEV)
+        _, a = m(ids_d)
+        _, b = m(cm[ids_d.flip(-1)])
+    assert _rel(b, a.flip(1)[..., cm]) < 1e-5
+
+
+def test_caduceus_loss_weights():
+    """forward(..., loss_weights=) == weighted_cross_entropy of the returned logits; all-ones
+    weights == the unweighted loss."""
+    from dna_amd.caduceus import CaduceusForMaskedLM, weighted_cross_entropy
+    torch.manual_seed(2)
+    m = CaduceusForMaskedLM(d_model=64, n_layer=1, vocab_size=12, ssm_cfg={"d_state": 16}).to(DEV)
+    ids = torch.randint(0, 12, (2, 64), device=DEV)
+    labels = ids.clone()
+    labels[:, ::3] = -100
+    w = torch.rand(2, 64, device=DEV)
+    loss, logits = m(ids, labels, loss_weights=w)
+    assert torch.allclose(loss, weighted_cross_entropy(logits, labels, w))
+    l1, _ = m(ids, labels, loss_weights=torch.ones(2, 64, device=DEV))
+    l0, _ = m(ids, labels)
+    assert torch.allclose(l1, l0, rtol=1e-5)
