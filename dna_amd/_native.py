@@ -68,6 +68,11 @@ _SIGS = {
     "dna_linear_dgrad_f32": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_linear_wgrad_f32_splits": (_i, [_i, _i, _i]),
     "dna_linear_wgrad_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "dna_gemm_strided_splits": (_i, [_i, _i, _i, _i]),
+    "dna_gemm_bf16_strided": (_i, [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64,
+                                   _i, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "dna_gemm_f32_strided": (_i, [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64,
+                                  _vp, _i, _i, _i, _i, _i, _vp]),
     "dna_linear_wgrad_p": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_geglu_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
     "dna_geglu_linear_dgrad": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),

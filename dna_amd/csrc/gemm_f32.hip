@@ -30,7 +30,9 @@ struct Args {
   const float* B; long long sbk, sbn;  // B(k, n) = B[k * sbk + n * sbn]
   float* C; long long ldc, slice;      // C[m * ldc + n] (+ blockIdx.z * slice)
   const float* bias;                   // [N] or null
-  int M, N, K, kchunk;                 // kchunk: k range per blockIdx.z
+  int M, N, K, kchunk;                 // kchunk: k range per split
+  long long saz, sbz;                  // batch steps of A / B (dna_gemm_f32_strided)
+  int splits;                          // blockIdx.z = batch * splits + split
 };
 
 // Loads of one 128 x 16 operand tile into 8 registers per thread, then into the LDS image
@@ -97,7 +99,10 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(Args a) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kb = blockIdx.z * a.kchunk;
+  const int zb = blockIdx.z / a.splits, sp = blockIdx.z - zb * a.splits;
+  const float* A = a.A + zb * a.saz;
+  const float* B = a.B + zb * a.sbz;
+  const int kb = sp * a.kchunk;
   const int ke = min(a.K, kb + a.kchunk);
   const int nk = (ke - kb + BK - 1) / BK;
 
@@ -110,8 +115,8 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(Args a) {
   Tile<AKC, VA> ta;
   Tile<BKC, VB> tb;
   if (nk > 0) {
-    ta.load(a.A, a.sam, a.sak, m0, a.M, kb, ke, t);
-    tb.load(a.B, a.sbn, a.sbk, n0, a.N, kb, ke, t);
+    ta.load(A, a.sam, a.sak, m0, a.M, kb, ke, t);
+    tb.load(B, a.sbn, a.sbk, n0, a.N, kb, ke, t);
     ta.store(smem[0][0], t);
     tb.store(smem[0][1], t);
   }
@@ -120,8 +125,8 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(Args a) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {  // next tile into registers while this one computes
-      ta.load(a.A, a.sam, a.sak, m0, a.M, kb + (kt + 1) * BK, ke, t);
-      tb.load(a.B, a.sbn, a.sbk, n0, a.N, kb + (kt + 1) * BK, ke, t);
+      ta.load(A, a.sam, a.sak, m0, a.M, kb + (kt + 1) * BK, ke, t);
+      tb.load(B, a.sbn, a.sbk, n0, a.N, kb + (kt + 1) * BK, ke, t);
     }
     const float* ia = smem[cur][0] + wm * 64 + li;
     const float* ib = smem[cur][1] + wn * 64 + li;
@@ -164,13 +169,15 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(Args a) {
 }
 
 template <bool AKC, bool BKC>
-int launch(const Args& a, int splits, hipStream_t st, const char* name) {
-  // float4 paths need the contiguous stride 1, the other stride a multiple of 4 and 16-B bases
+int launch(Args a, int splits, hipStream_t st, const char* name, int batch = 1) {
+  a.splits = splits;
+  // float4 paths need the contiguous stride 1, the other stride (and the batch step) a
+  // multiple of 4 and 16-B bases
   const bool va = (AKC ? a.sak == 1 && a.sam % 4 == 0 : a.sam == 1 && a.sak % 4 == 0) &&
-                  ((uintptr_t)a.A & 15) == 0;
+                  a.saz % 4 == 0 && ((uintptr_t)a.A & 15) == 0;
   const bool vb = (BKC ? a.sbk == 1 && a.sbn % 4 == 0 : a.sbn == 1 && a.sbk % 4 == 0) &&
-                  ((uintptr_t)a.B & 15) == 0;
-  const dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
+                  a.sbz % 4 == 0 && ((uintptr_t)a.B & 15) == 0;
+  const dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch * splits);
   if (va && vb) hipLaunchKernelGGL((gemm_f32_kernel<AKC, BKC, true, true>), grid, dim3(NT), 0, st, a);
   else if (va) hipLaunchKernelGGL((gemm_f32_kernel<AKC, BKC, true, false>), grid, dim3(NT), 0, st, a);
   else if (vb) hipLaunchKernelGGL((gemm_f32_kernel<AKC, BKC, false, true>), grid, dim3(NT), 0, st, a);
@@ -232,4 +239,31 @@ extern "C" int dna_linear_wgrad_f32(const float* dy, const float* x, int T, int 
   a.kchunk = ((T + splits - 1) / splits + BK - 1) / BK * BK;
   if (T == 0) a.kchunk = BK;  // every slice computes zeros
   return launch<false, false>(a, splits, as_stream(stream), "dna_linear_wgrad_f32");
+}
+
+// C[z][m][n] = sum_k A(m, k) B(k, n) over a batch with split-K slices (z = batch * splits +
+// split; C + z * scz): the fp32 form of dna_gemm_bf16_strided (gemm_strided.hip), for the Mamba
+// projections outside autocast. A needs a unit stride along k or m, B along k or n.
+extern "C" int dna_gemm_f32_strided(const float* A, long long sam, long long sak, long long saz,
+                                    const float* B, long long sbk, long long sbn, long long sbz,
+                                    float* C, long long ldc, long long scz, const float* bias_n,
+                                    int M, int N, int K, int batch, int splits, void* stream) {
+  DNA_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && splits >= 1 && splits <= 65535 / batch,
+                "dna_gemm_f32_strided: bad shape");
+  if (M == 0 || N == 0) return DNA_OK;
+  DNA_CHECK_ARG(A && B && C, "dna_gemm_f32_strided: null pointer");
+  DNA_CHECK_ARG(sak == 1 || sam == 1, "dna_gemm_f32_strided: A needs a unit stride along k or m");
+  DNA_CHECK_ARG(sbk == 1 || sbn == 1, "dna_gemm_f32_strided: B needs a unit stride along k or n");
+  Args a{};
+  a.A = A; a.sam = sam; a.sak = sak; a.saz = saz;
+  a.B = B; a.sbk = sbk; a.sbn = sbn; a.sbz = sbz;
+  a.C = C; a.ldc = ldc; a.slice = scz; a.bias = bias_n;
+  a.M = M; a.N = N; a.K = K;
+  a.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  if (a.kchunk == 0) a.kchunk = BK;
+  hipStream_t st = as_stream(stream);
+  if (sak == 1 && sbk == 1) return launch<true, true>(a, splits, st, "dna_gemm_f32_strided", batch);
+  if (sak == 1) return launch<true, false>(a, splits, st, "dna_gemm_f32_strided", batch);
+  if (sbk == 1) return launch<false, true>(a, splits, st, "dna_gemm_f32_strided", batch);
+  return launch<false, false>(a, splits, st, "dna_gemm_f32_strided", batch);
 }

@@ -143,6 +143,22 @@ class EmbeddingLN(torch.autograd.Function):
         return None, dE, dtt, dg, db, None, None, None, None, None, None
 
 
+def strided_gemm(A, sa, B, sb, C, sc, M, Nc, K, batch, splits=1, out_f32=None, bias_n=None):
+    """C[z][m][n] = sum_k A(m, k) B(k, n) (+ bias_n[n], fp32) on dna_gemm_bf16_strided /
+    dna_gemm_f32_strided (z = batch * splits + split). sa = (sam, sak, saz), sb = (sbk, sbn, sbz),
+    sc = (ldc, scz); strides in elements."""
+    bn = None if bias_n is None else bias_n.data_ptr()
+    if A.dtype == torch.bfloat16:
+        assert B.dtype == torch.bfloat16
+        f32 = C.dtype == torch.float32 if out_f32 is None else out_f32
+        N.call("dna_gemm_bf16_strided", A.data_ptr(), *sa, B.data_ptr(), *sb, C.data_ptr(), *sc,
+               int(f32), None, bn, M, Nc, K, batch, splits, N.stream_ptr())
+    else:
+        assert A.dtype == B.dtype == C.dtype == torch.float32
+        N.call("dna_gemm_f32_strided", A.data_ptr(), *sa, B.data_ptr(), *sb, C.data_ptr(), *sc,
+               bn, M, Nc, K, batch, splits, N.stream_ptr())
+
+
 # ----------------------------------------------------------------------------------- fused LN
 class FusedLayerNorm(torch.autograd.Function):
     """LN(dropout(act(x + bias)) + residual) -> (y fp32|None, y_bf16|None).

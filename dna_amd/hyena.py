@@ -16,6 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native as N
+from . import functional as DF
 from .functional import Linear as _LinearFn
 from .functional import _dt, _gpu, _p, _timed
 
@@ -307,48 +308,62 @@ class ExponentialModulation(_OptimModule):
         return x * (torch.exp(-t * self.deltas.abs()) + self.shift)
 
 
-class _ChunkedLinear(torch.autograd.Function):
-    """y[L, N] = x[L, K] . w^T + b as c chunk products; dW and db reduced in fp32 over the chunks
-    and rounded once (as one GEMM with fp32 accumulation would), x / w / b in one dtype."""
+class _FilterLinear(torch.autograd.Function):
+    """y[L, N] = x[L, K] . w[N, K]^T + b for the implicit filter MLP on the strided MFMA GEMM
+    (dna_gemm_bf16_strided / dna_gemm_f32_strided): the weight gradient's L-long contraction runs
+    as fp32 split-K slices summed once by dna_sum_slices_accum (rounded once, as one GEMM with fp32
+    accumulation would), the bias gradient as an fp32 column sum. x / w / b in one dtype."""
 
     @staticmethod
-    def forward(ctx, x, w, b, c):
+    def forward(ctx, x, w, b):
+        _gpu(x, w, b)
         L, K = x.shape
-        N = w.shape[0]
-        xc = x.view(c, L // c, K)
-        wt = w.t().unsqueeze(0).expand(c, K, N)
-        y = torch.baddbmm(b.view(1, 1, N), xc, wt) if b is not None else torch.bmm(xc, wt)
+        Nn = w.shape[0]
+        x = x.contiguous()
+        w = w.contiguous()
+        y = torch.empty(L, Nn, device=x.device, dtype=x.dtype)
+        bf = None if b is None else b.float().contiguous()
+        with _timed("filter_linear", (L * (K + Nn)) * x.element_size(), "byte"):
+            DF.strided_gemm(x, (K, 1, 0), w, (1, K, 0), y, (Nn, 0), L, Nn, K, 1, bias_n=bf)
         ctx.save_for_backward(x, w)
-        ctx.c, ctx.has_b = c, b is not None
-        return y.view(L, N)
+        ctx.has_b = b is not None
+        return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        c = ctx.c
         L, K = x.shape
-        N = w.shape[0]
-        dy = dy.contiguous()
-        dx = dy @ w if ctx.needs_input_grad[0] else None
-        dw = torch.bmm(dy.view(c, L // c, N).transpose(1, 2), x.view(c, L // c, K),
-                       out_dtype=torch.float32).sum(0).to(w.dtype)
+        Nn = w.shape[0]
+        dy = dy.contiguous().to(x.dtype)
+        dx = None
+        if ctx.needs_input_grad[0]:  # dx[L, K] = dy[L, N] . w[N, K]
+            dx = torch.empty(L, K, device=x.device, dtype=x.dtype)
+            DF.strided_gemm(dy, (Nn, 1, 0), w, (K, 1, 0), dx, (K, 0), L, K, Nn, 1)
+        s = int(N.lib().dna_gemm_strided_splits(Nn, K, L, 1))
+        part = torch.empty(s, Nn, K, device=x.device, dtype=torch.float32)
+        if x.dtype == torch.bfloat16:  # dW[N, K] = sum_l dy[l, n] x[l, k]
+            DF.strided_gemm(dy, (1, Nn, 0), x, (K, 1, 0), part, (K, Nn * K), Nn, K, L, 1, s,
+                            out_f32=True)
+        else:
+            DF.strided_gemm(dy, (1, Nn, 0), x, (K, 1, 0), part, (K, Nn * K), Nn, K, L, 1, s)
+        dw = torch.zeros(Nn, K, device=x.device, dtype=torch.float32)
+        N.call("dna_sum_slices_accum", part.data_ptr(), s, Nn * K, dw.data_ptr(), N.stream_ptr())
         db = dy.float().sum(0).to(dy.dtype) if ctx.has_b else None
-        return dx, dw, db, None
+        return dx, dw.to(w.dtype), db
 
 
-def _split_k_linear(x, lin, rows_per_chunk=512):
-    """nn.Linear over the L positions of the implicit filter MLP ([1, L, K] -> [1, L, N], K and N
-    64-256). As one GEMM its weight gradient is a 64 x 64 (or 256 x 64) output reduced over all
-    L = 65,536 positions, which hipBLASLt ran as one or four workgroups (≈210 us per call, 12 % of
-    the config-D step). Here the product runs batched over L / 512 chunks and the weight gradient
-    as a batched GEMM over the chunks with fp32 partials summed in fp32: split-K with every CU
-    busy. Same dtype flow as nn.Linear: under autocast x, W and b are cast to the autocast dtype
-    and the output is in it (bias added inside the product, as addmm does); the gradients are
-    rounded once. Short or odd lengths and CPU tensors keep the plain linear."""
-    L = x.shape[-2]
-    if not x.is_cuda or os.environ.get("DNA_HYENA_FILTER_SPLITK", "1") == "0" or L < 8 * rows_per_chunk \
-            or L % rows_per_chunk or x.dim() != 3 or x.shape[0] != 1:
+def _split_k_linear(x, lin):
+    """nn.Linear over the L positions of the implicit filter MLP ([1, L, K] -> [1, L, N], K 3-5
+    and N 64-256) on the strided MFMA GEMM (`_FilterLinear`). As one library GEMM its weight
+    gradient is a 64 x 64 (or 256 x 64) output reduced over all L = 65,536 positions, which
+    hipBLASLt ran as one or four workgroups (~210 us per call, 12 % of the config-D step); here the
+    contraction is split over the CUs. Same dtype flow as nn.Linear: under autocast x, W and b are
+    cast to the autocast dtype and the output is in it (bias added in the product's epilogue, in
+    fp32, as addmm does); the gradients are rounded once. CPU tensors keep the plain linear
+    (parity tests of the module on the CPU)."""
+    if not x.is_cuda or x.dim() != 3 or x.shape[0] != 1:
         return lin(x)
+    L = x.shape[-2]
     w, b = lin.weight, lin.bias
     if torch.is_autocast_enabled(x.device.type):
         dt = torch.get_autocast_dtype(x.device.type)
@@ -356,8 +371,10 @@ def _split_k_linear(x, lin, rows_per_chunk=512):
     else:
         b = b.to(x.dtype) if b is not None else None
         w = w.to(x.dtype)
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        raise NotImplementedError(f"implicit filter MLP in {x.dtype}")
     with torch.autocast(x.device.type, enabled=False):
-        y = _ChunkedLinear.apply(x.reshape(L, -1), w, b, L // rows_per_chunk)
+        y = _FilterLinear.apply(x.reshape(L, -1), w, b)
     return y.reshape(1, L, -1)
 
 

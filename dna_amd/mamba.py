@@ -9,7 +9,8 @@ delta_softplus. Forward and backward run dna_amd/csrc/selective_scan.hip; no CPU
 
 Around it: `Mamba` (mamba_ssm.modules.mamba_simple.Mamba 1.x, restated: same parameters, names
 and forward math on its non-fused path) with the depthwise causal conv1d + SiLU on the HIP
-kernel of dna_amd/csrc/causal_conv.hip, and `BiMambaWrapper` (the reference's own wrapper,
+kernel of dna_amd/csrc/causal_conv.hip, x_proj / dt_proj channel-major on the strided MFMA GEMM
+(dna_amd/csrc/gemm_strided.hip, `ChannelLinear`), and `BiMambaWrapper` (the reference's own wrapper,
 modeling_caduceus.py:68-121: forward + flipped reverse Mamba, tied in/out projections, "add" or
 "ew_multiply").
 """
@@ -20,7 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native as N
-from .functional import _dt, _gpu, _p, _timed
+from .functional import _dt, _gpu, _p, _timed, strided_gemm as _strided_gemm
 
 
 class SelectiveScan(torch.autograd.Function):
@@ -136,6 +137,68 @@ class CausalConv1d(torch.autograd.Function):
         return dx, s[:, :K].reshape(wshape).to(wdtype), db, None
 
 
+class ChannelLinear(torch.autograd.Function):
+    """y[b, M, L] = W[M, K] . x[b, K, L] with x channel-major (unit position stride, any channel /
+    batch stride): the x_proj and dt_proj products of mamba_ssm Mamba.forward (`x_proj(rearrange(x,
+    "b d l -> (b l) d"))`, `dt_proj.weight @ dt.t()`) computed without transposing x, so B / C /
+    delta come out in the [b, ·, L] layout the scan reads. Forward and backward on
+    dna_gemm_bf16_strided (bf16, under autocast) or dna_gemm_f32_strided (fp32); dW's contraction
+    over b and L runs as fp32 split-K slices summed by dna_sum_slices_accum."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        _gpu(x, weight)
+        b, K, L = x.shape
+        M = weight.shape[0]
+        assert weight.shape[1] == K
+        if torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+        else:
+            dt = torch.promote_types(x.dtype, weight.dtype)
+        if dt not in (torch.bfloat16, torch.float32):
+            raise NotImplementedError(f"ChannelLinear: {dt}")
+        xin = x.to(dt)
+        if xin.stride(2) != 1:
+            xin = xin.contiguous()
+        w = weight.detach().to(dt).contiguous()
+        y = torch.empty(b, M, L, device=x.device, dtype=dt)
+        with _timed("mamba_proj", (b * K * L + b * M * L) * xin.element_size(), "byte"):
+            _strided_gemm(w, (K, 1, 0), xin, (xin.stride(1), 1, xin.stride(0)), y, (L, M * L),
+                          M, L, K, b)
+        ctx.save_for_backward(xin, w)
+        ctx.cfg = (x.dtype, weight.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xin, w = ctx.saved_tensors
+        xdt, wdt = ctx.cfg
+        b, K, L = xin.shape
+        M = w.shape[0]
+        dy = dy.to(xin.dtype)
+        if dy.stride(2) != 1:
+            dy = dy.contiguous()
+        dx = dw = None
+        es = xin.element_size()
+        if ctx.needs_input_grad[0]:  # dx[b, K, L] = W^T[K, M] . dy[b, M, L]
+            dx = torch.empty(b, K, L, device=xin.device, dtype=xin.dtype)
+            with _timed("mamba_proj", (b * M * L + b * K * L) * es, "byte"):
+                _strided_gemm(w, (1, K, 0), dy, (dy.stride(1), 1, dy.stride(0)), dx, (L, K * L),
+                              K, L, M, b)
+        if ctx.needs_input_grad[1]:  # dW[M, K] = sum_b dy[b] . x[b]^T (contraction over L)
+            s = int(N.lib().dna_gemm_strided_splits(M, K, L, b))
+            part = torch.empty(b * s, M, K, device=xin.device, dtype=torch.float32)
+            with _timed("mamba_proj", (b * M * L + b * K * L) * es, "byte"):
+                _strided_gemm(dy, (dy.stride(1), 1, dy.stride(0)), xin,
+                              (1, xin.stride(1), xin.stride(0)), part, (K, M * K), M, K, L, b, s,
+                              out_f32=True)
+            dw = torch.zeros(M, K, device=xin.device, dtype=torch.float32)
+            N.call("dna_sum_slices_accum", part.data_ptr(), b * s, M * K, dw.data_ptr(),
+                   N.stream_ptr())
+            dw = dw.to(wdt)
+        return (None if dx is None else dx.to(xdt)), dw
+
+
 class Mamba(nn.Module):
     """mamba_ssm.modules.mamba_simple.Mamba (1.x) as Caduceus builds it (BiMambaWrapper,
     modeling_caduceus.py:88-91): same constructor, parameter names/shapes and initialisation;
@@ -195,12 +258,15 @@ class Mamba(nn.Module):
         A = -torch.exp(self.A_log.float())
         x, z = xz.chunk(2, dim=1)
         x = CausalConv1d.apply(x.contiguous(), self.conv1d.weight, self.conv1d.bias, True)
-        x_dbl = self.x_proj(x.transpose(1, 2).reshape(batch * seqlen, self.d_inner))
-        dt, Bm, Cm = torch.split(x_dbl, [self.dt_rank, self.d_state, self.d_state], dim=-1)
-        dt = (self.dt_proj.weight @ dt.t()).reshape(self.d_inner, batch, seqlen).permute(1, 0, 2)
-        Bm = Bm.reshape(batch, seqlen, self.d_state).transpose(1, 2).contiguous()
-        Cm = Cm.reshape(batch, seqlen, self.d_state).transpose(1, 2).contiguous()
-        y = selective_scan_fn(x, dt.contiguous(), A, Bm, Cm, self.D.float(), z=z.contiguous(),
+        # x_proj and dt_proj channel-major on the strided MFMA GEMM (ChannelLinear): x_dbl
+        # [b, R + 2N, L] = x_proj.weight . x, delta [b, E, L] = dt_proj.weight . x_dbl[:, :R]
+        if self.x_proj.bias is not None:
+            raise NotImplementedError("Mamba: x_proj with a bias (mamba_ssm builds it bias-free)")
+        x_dbl = ChannelLinear.apply(x, self.x_proj.weight)
+        R, Ns = self.dt_rank, self.d_state
+        dt = ChannelLinear.apply(x_dbl[:, :R], self.dt_proj.weight)
+        Bm, Cm = x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
+        y = selective_scan_fn(x, dt, A, Bm, Cm, self.D.float(), z=z.contiguous(),
                               delta_bias=self.dt_proj.bias.float(), delta_softplus=True)
         return self.out_proj(y.transpose(1, 2))
 

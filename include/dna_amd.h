@@ -219,6 +219,27 @@ int dna_linear_dgrad_f32(const float* dy, const float* w, int M, int N, int K, f
 int dna_linear_wgrad_f32_splits(int T, int N, int K);
 int dna_linear_wgrad_f32(const float* dy, const float* x, int T, int N, int K, int splits,
                          float* partials, void* stream);
+
+/* Strided batched GEMM for the Mamba mixer's skinny projections, computed channel-major so no
+ * operand is transposed in memory (replaces the x_proj / dt_proj nn.Linear forward and backward
+ * of mamba_ssm Mamba.forward as Caduceus builds it, modeling_caduceus.py:88-91):
+ *   C[z][m][n] = sum_k A(m, k) B(k, n),  z = b * splits + s (k slice s of the contraction),
+ *   A(m, k) = A[b*saz + m*sam + k*sak] (sak == 1 or sam == 1),
+ *   B(k, n) = B[b*sbz + k*sbk + n*sbn] (sbk == 1 or sbn == 1),
+ *   C + z*scz, row stride ldc; bf16 in, fp32 accumulate, bf16 or fp32 (out_f32) out;
+ *   bias_m[M] / bias_n[N] optional (may be null).
+ * Weight gradients: splits from dna_gemm_strided_splits, fp32 slices summed over z by
+ * dna_sum_slices_accum. csrc/gemm_strided.hip (bf16, MFMA 16x16x32), csrc/gemm_f32.hip (fp32). */
+int dna_gemm_strided_splits(int M, int N, int K, int batch);
+int dna_gemm_bf16_strided(const void* A, long long sam, long long sak, long long saz,
+                          const void* B, long long sbk, long long sbn, long long sbz,
+                          void* C, long long ldc, long long scz, int out_f32,
+                          const float* bias_m, const float* bias_n, int M, int N, int K,
+                          int batch, int splits, void* stream);
+int dna_gemm_f32_strided(const float* A, long long sam, long long sak, long long saz,
+                         const float* B, long long sbk, long long sbn, long long sbz,
+                         float* C, long long ldc, long long scz, const float* bias_n,
+                         int M, int N, int K, int batch, int splits, void* stream);
 /* dst[cols][rows] = src[rows][cols] (bf16; rows, cols % 8 == 0): the transposed weight copy kept
  * beside the bf16 weights, so the data gradient dx = dy . w runs as
  * dna_linear_fwd(dy, w^T, NULL, M, K, N, dx) on both-operands-K-major MFMA tiles (replaces the
