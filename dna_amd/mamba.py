@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native as N
+from . import functional as DF
 from .functional import _dt, _gpu, _p, _timed, strided_gemm as _strided_gemm
 
 
@@ -199,6 +200,131 @@ class ChannelLinear(torch.autograd.Function):
         return (None if dx is None else dx.to(xdt)), dw
 
 
+def _wgrad_tokens(dy, sa, x, sb, M, Nn, T, batch, part=None, row0=0, rows_total=None):
+    """fp32 split-K slices of dW[m][n] = sum_{b, t} A(m, t) B(t, n) (the Mamba projections' weight
+    gradients: contraction over every token) on the strided MFMA GEMM. Returns (part, splits);
+    slices are [z][rows_total][Nn], this call filling rows row0 .. row0 + M."""
+    s = int(N.lib().dna_gemm_strided_splits(M, Nn, T, batch))
+    rt = M if rows_total is None else rows_total
+    if part is None:
+        part = torch.empty(batch * s, rt, Nn, device=dy.device, dtype=torch.float32)
+    assert part.shape[0] == batch * s
+    DF.strided_gemm(dy, sa, x, sb, part[:, row0:], (Nn, rt * Nn), M, Nn, T, batch, s, out_f32=True)
+    return part, s
+
+
+def _sum_parts(part, shape, dtype):
+    out = torch.zeros(shape, device=part.device, dtype=torch.float32)
+    N.call("dna_sum_slices_accum", part.data_ptr(), part.shape[0], out.numel(), out.data_ptr(),
+           N.stream_ptr())
+    return out.to(dtype)
+
+
+class InProj(torch.autograd.Function):
+    """in_proj of mamba_ssm Mamba.forward, channel-major as the reference computes it
+    (`in_proj.weight @ rearrange(hidden, "b l d -> d (b l)")`), returning x and z ([b, E, L] each)
+    as two outputs so the backward takes dx and dz apart (no cat of the two halves). The forward
+    and the data gradient are the K = d_model / E products hipBLASLt runs at ~1.2 PF/s; the weight
+    gradient -- a contraction over all b*L tokens into a [2E, d] output, which hipBLASLt ran on
+    256x32 tiles at 0.17 PF/s -- runs as fp32 split-K slices on the strided MFMA GEMM."""
+
+    @staticmethod
+    def forward(ctx, h, weight):
+        _gpu(h, weight)
+        b, L, d = h.shape
+        E2 = weight.shape[0]
+        if torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+        else:
+            dt = torch.promote_types(h.dtype, weight.dtype)
+        h2 = h.reshape(b * L, d).to(dt).contiguous()
+        w = weight.detach().to(dt)
+        with torch.autocast("cuda", enabled=False):
+            xz = (w @ h2.t()).reshape(E2, b, L).permute(1, 0, 2)
+        ctx.save_for_backward(h2, w)
+        ctx.cfg = (b, L, h.dtype, weight.dtype)
+        x, z = xz.chunk(2, dim=1)
+        return x, z
+
+    @staticmethod
+    def backward(ctx, dx, dz):
+        h2, w = ctx.saved_tensors
+        b, L, hdt, wdt = ctx.cfg
+        E2, d = w.shape
+        E = E2 // 2
+        T = b * L
+        dt = h2.dtype
+        halves = []
+        for i, g in enumerate((dx, dz)):
+            if g is not None:  # [b, E, L] -> [E, T] (token index t = b * L + l)
+                halves.append((i, g.to(dt).permute(1, 0, 2).reshape(E, T).contiguous()))
+        dh = dw = None
+        with torch.autocast("cuda", enabled=False):
+            if ctx.needs_input_grad[0]:
+                dh = torch.zeros(T, d, device=h2.device, dtype=dt) if not halves else None
+                for i, g in halves:
+                    wi = w[i * E:(i + 1) * E]
+                    dh = g.t() @ wi if dh is None else torch.addmm(dh, g.t(), wi)
+                dh = dh.reshape(b, L, d).to(hdt)
+            if ctx.needs_input_grad[1]:
+                part, s = None, 0
+                if not halves:
+                    dw = torch.zeros_like(w, dtype=wdt)
+                else:
+                    s = int(N.lib().dna_gemm_strided_splits(E, d, T, 1))
+                    part = torch.zeros(s, E2, d, device=h2.device, dtype=torch.float32)
+                    for i, g in halves:  # dW[c][j] = sum_t g[c][t] h[t][j]
+                        _wgrad_tokens(g, (T, 1, 0), h2, (d, 1, 0), E, d, T, 1, part, i * E, E2)
+                    dw = _sum_parts(part, (E2, d), wdt)
+        return dh, dw
+
+
+class OutProj(torch.autograd.Function):
+    """out_proj of mamba_ssm Mamba.forward on the scan output y [b, E, L] (channel-major):
+    out [b, L, d] = y^T . W^T (+ bias). Forward and data gradient on hipBLASLt (transposed-operand
+    GEMMs at ~1.2 PF/s); the weight gradient (contraction over all b*L tokens into [d, E]) as fp32
+    split-K slices on the strided MFMA GEMM, reading y where it lies."""
+
+    @staticmethod
+    def forward(ctx, y, weight, bias):
+        _gpu(y, weight)
+        b, E, L = y.shape
+        if torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+        else:
+            dt = torch.promote_types(y.dtype, weight.dtype)
+        yc = y.to(dt)
+        if yc.stride(2) != 1 or yc.stride(1) != L:
+            yc = yc.contiguous()
+        w = weight.detach().to(dt)
+        bb = None if bias is None else bias.detach().to(dt)
+        with torch.autocast("cuda", enabled=False):
+            out = F.linear(yc.transpose(1, 2), w, bb)
+        ctx.save_for_backward(yc, w)
+        ctx.cfg = (y.dtype, weight.dtype, None if bias is None else bias.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        yc, w = ctx.saved_tensors
+        ydt, wdt, bdt = ctx.cfg
+        b, E, L = yc.shape
+        d = w.shape[0]
+        dt = yc.dtype
+        dout = dout.to(dt).contiguous()
+        dy = dw = db = None
+        with torch.autocast("cuda", enabled=False):
+            if ctx.needs_input_grad[0]:
+                dy = (dout @ w).transpose(1, 2).to(ydt)   # [b, E, L] view
+            if ctx.needs_input_grad[1]:  # dW[o][e] = sum_{b,l} dout[b][l][o] y[b][e][l]
+                part, _ = _wgrad_tokens(dout, (1, d, L * d), yc, (1, yc.stride(1), yc.stride(0)),
+                                        d, E, L, b)
+                dw = _sum_parts(part, (d, E), wdt)
+            if bdt is not None and ctx.needs_input_grad[2]:
+                db = dout.float().sum((0, 1)).to(bdt)
+        return dy, dw, db
+
+
 class Mamba(nn.Module):
     """mamba_ssm.modules.mamba_simple.Mamba (1.x) as Caduceus builds it (BiMambaWrapper,
     modeling_caduceus.py:88-91): same constructor, parameter names/shapes and initialisation;
@@ -251,12 +377,11 @@ class Mamba(nn.Module):
             raise NotImplementedError("Mamba: inference_params (recurrent decoding)")
         batch, seqlen, _ = hidden_states.shape
         # in_proj computed channel-major, as the reference does (W @ x^T -> [b, 2E, l])
-        xz = (self.in_proj.weight @ hidden_states.reshape(-1, self.d_model).t()).reshape(
-            2 * self.d_inner, batch, seqlen).permute(1, 0, 2)
+        x, z = InProj.apply(hidden_states, self.in_proj.weight)
         if self.in_proj.bias is not None:
-            xz = xz + self.in_proj.bias.to(xz.dtype)[:, None]
+            bx, bz = self.in_proj.bias.chunk(2)
+            x, z = x + bx.to(x.dtype)[:, None], z + bz.to(z.dtype)[:, None]
         A = -torch.exp(self.A_log.float())
-        x, z = xz.chunk(2, dim=1)
         x = CausalConv1d.apply(x.contiguous(), self.conv1d.weight, self.conv1d.bias, True)
         # x_proj and dt_proj channel-major on the strided MFMA GEMM (ChannelLinear): x_dbl
         # [b, R + 2N, L] = x_proj.weight . x, delta [b, E, L] = dt_proj.weight . x_dbl[:, :R]
@@ -268,7 +393,7 @@ class Mamba(nn.Module):
         Bm, Cm = x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
         y = selective_scan_fn(x, dt, A, Bm, Cm, self.D.float(), z=z.contiguous(),
                               delta_bias=self.dt_proj.bias.float(), delta_softplus=True)
-        return self.out_proj(y.transpose(1, 2))
+        return OutProj.apply(y, self.out_proj.weight, self.out_proj.bias)
 
 
 class BiMambaWrapper(nn.Module):
