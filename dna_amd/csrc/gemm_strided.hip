@@ -23,7 +23,7 @@
 // operand contiguous along k (AKC / BKC) is staged into a [row][k] image (80-B rows: the
 // ds_read_b128 fragment reads are bank-conflict free); one contiguous along m / n into a [k][row]
 // image (272-B rows) read with ds_read_b64_tr_b16. The product is issued swapped (C^T = B^T A^T),
-// so a lane holds 4 consecutive n of one m: 8-B bf16 / 16-B fp32 stores.
+// so a lane holds 4 consecutive n of one m; a permlane16 exchange widens that to 8 (16-B stores).
 #include "common.h"
 
 namespace dna {
@@ -157,35 +157,67 @@ __global__ __launch_bounds__(NT) void sgemm_kernel(Args a) {
     __syncthreads();
   }
 
-  // swapped product: lane holds n = 4 * (lane >> 4) + r of column m = lane & 15 of each tile
+  // swapped product: lane holds n = 4 * (lane >> 4) + r of column m = lane & 15 of each tile.
+  // Tiles j, j + 1 are exchanged with v_permlane16_swap so a lane holds 8 consecutive n of its m
+  // (columns {0, 16, 8, 24}[lane >> 4] .. + 7 of the pair's 32): one 16-B bf16 store (two fp32)
+  // per lane, 64 contiguous bytes per row and instruction.
   const long long zc = (long long)z * a.scz;
+  const int cg = lane >> 4;
+  const int colq = ((cg & 1) << 4) + ((cg & 2) << 2);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-    if (m >= a.M) continue;
-    const float bm = a.bias_m ? a.bias_m[m] : 0.f;
+    const float bm = (a.bias_m && m < a.M) ? a.bias_m[m] : 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-      if (n >= a.N) continue;
-      f32x4 v = acc[i][j];
+    for (int jp = 0; jp < 2; ++jp) {
+      f32x4 v[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += bm + ((a.bias_n && n + r < a.N) ? a.bias_n[n + r] : 0.f);
-      const long long off = zc + (long long)m * a.ldc + n;
+      for (int h = 0; h < 2; ++h) {
+        const int nt = n0 + wn * 64 + (2 * jp + h) * 16 + 4 * cg;  // this tile's 4 columns
+        v[h] = acc[i][2 * jp + h];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[h][r] += bm + ((a.bias_n && nt + r < a.N) ? a.bias_n[nt + r] : 0.f);
+      }
+      const int n = n0 + wn * 64 + jp * 32 + colq;  // first of this lane's 8 columns
+      float o[8];
       if constexpr (F32) {
-        float* C = reinterpret_cast<float*>(a.C) + off;
-        if (a.vc && n + 4 <= a.N) *reinterpret_cast<f32x4*>(C) = v;
-        else
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < a.N) C[r] = v[r];
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v[0][r]),
+                                                           __builtin_bit_cast(unsigned, v[1][r]), false, false);
+          o[r] = __builtin_bit_cast(float, (unsigned)sw[0]);
+          o[4 + r] = __builtin_bit_cast(float, (unsigned)sw[1]);
+        }
       } else {
-        bf16* C = reinterpret_cast<bf16*>(a.C) + off;
-        if (a.vc && n + 4 <= a.N) *reinterpret_cast<bf16x4*>(C) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        else
+        typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+        const u32x2_t h0 = __builtin_bit_cast(u32x2_t, bf16x4{(bf16)v[0][0], (bf16)v[0][1], (bf16)v[0][2], (bf16)v[0][3]});
+        const u32x2_t h1 = __builtin_bit_cast(u32x2_t, bf16x4{(bf16)v[1][0], (bf16)v[1][1], (bf16)v[1][2], (bf16)v[1][3]});
+        const auto sx = __builtin_amdgcn_permlane16_swap(h0[0], h1[0], false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(h0[1], h1[1], false, false);
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+        const bf16x8 hb = __builtin_bit_cast(bf16x8, u32x4_t{(unsigned)sx[0], (unsigned)sy[0], (unsigned)sx[1], (unsigned)sy[1]});
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < a.N) C[r] = (bf16)v[r];
+        for (int e = 0; e < 8; ++e) o[e] = (float)hb[e];  // exact: already bf16 values
+        if (m < a.M && n < a.N) {
+          bf16* C = reinterpret_cast<bf16*>(a.C) + zc + (long long)m * a.ldc + n;
+          if (a.vc && n + 8 <= a.N) *reinterpret_cast<bf16x8*>(C) = hb;
+          else
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (n + e < a.N) C[e] = hb[e];
+        }
+        continue;
+      }
+      if (m < a.M && n < a.N) {
+        float* C = reinterpret_cast<float*>(a.C) + zc + (long long)m * a.ldc + n;
+        if (a.vc && n + 8 <= a.N) {
+          *reinterpret_cast<f32x4*>(C) = f32x4{o[0], o[1], o[2], o[3]};
+          *reinterpret_cast<f32x4*>(C + 4) = f32x4{o[4], o[5], o[6], o[7]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < a.N) C[e] = o[e];
+        }
       }
     }
   }
@@ -233,7 +265,7 @@ extern "C" int dna_gemm_bf16_strided(const void* A, long long sam, long long sak
   };
   a.va = al(A, akc ? sam : sak, saz);
   a.vb = al(B, bkc ? sbn : sbk, sbz);
-  a.vc = ((uintptr_t)C & (out_f32 ? 15 : 7)) == 0 && ldc % 4 == 0 && scz % 4 == 0;
+  a.vc = ((uintptr_t)C & 15) == 0 && ldc % 8 == 0 && scz % 8 == 0;
   const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * splits);
   DNA_CHECK_ARG(grid.y <= 65535, "dna_gemm_bf16_strided: M too large");
   hipStream_t st = as_stream(stream);

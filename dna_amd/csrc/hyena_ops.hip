@@ -206,75 +206,153 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // duc for this tile's positions plus the K-1 after it (0 at t >= L: cropped conv outputs).
-  // All the lane's d(x_g) / d(v x) loads (NQ (channel, row) items, order <= 4) are issued first.
-  constexpr int NQ = (CPW * RD + 63) / 64;
-  T lx[NQ][ORD - 1 > 0 ? ORD - 1 : 1], lv[NQ];
+  // A lane takes (channel jj of the wave's 8, chunk of 8 positions): its d(x_g) / d(v x) loads are
+  // 16-B vectors of the channel-major rows (when L % 8 == 0: every row 16-B aligned), all issued
+  // before the conv recompute; rows past the duc tile (RD) or past L are dropped / zero.
+  constexpr int NCH = (RD + 7) / 8;                 // position chunks per channel
+  constexpr int NQ = (CPW * NCH + 63) / 64;         // items per lane
+  constexpr int NX = ORD - 1 > 0 ? ORD - 1 : 1;
+  const bool vec = (a.L & 7) == 0;
+  bf16x8 lxv[NQ][NX], lvv[NQ];
+  float4 lxf[NQ][NX][2], lvf[NQ][2];
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
     const int q = lane + 64 * n;
-    const int jj = q / RD, rr = q - jj * RD;
-    const int c = c0 + wv * CPW + jj, t = t0 + rr;
-    const bool ok = q < CPW * RD && t < a.L;
-    lv[n] = ok ? ((const T*)a.dvx)[((size_t)b * a.d + c) * a.L + t] : T(0.f);
+    const int jj = q / NCH, pc = q - jj * NCH;
+    const int c = c0 + wv * CPW + jj, t = t0 + 8 * pc;
+    const bool okq = q < CPW * NCH;
+    const size_t ov = ((size_t)b * a.d + c) * a.L + t;
+    if constexpr (sizeof(T) == 2) {
+      lvv[n] = bf16x8{};
 #pragma unroll
-    for (int g = 0; g < ORD - 1; ++g)
-      lx[n][g] = ok ? ((const T*)a.dxs)[((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t] : T(0.f);
+      for (int g = 0; g < NX; ++g) lxv[n][g] = bf16x8{};
+      if (okq && vec && t + 8 <= a.L) {
+        lvv[n] = *reinterpret_cast<const bf16x8*>((const bf16*)a.dvx + ov);
+#pragma unroll
+        for (int g = 0; g < ORD - 1; ++g)
+          lxv[n][g] = *reinterpret_cast<const bf16x8*>(
+              (const bf16*)a.dxs + ((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t);
+      } else if (okq) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (t + i >= a.L) break;
+          lvv[n][i] = ((const bf16*)a.dvx)[ov + i];
+#pragma unroll
+          for (int g = 0; g < ORD - 1; ++g)
+            lxv[n][g][i] = ((const bf16*)a.dxs)[((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t + i];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        lvf[n][h] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int g = 0; g < NX; ++g) lxf[n][g][h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (okq && vec && t + 8 <= a.L) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          lvf[n][h] = *reinterpret_cast<const float4*>((const float*)a.dvx + ov + 4 * h);
+#pragma unroll
+          for (int g = 0; g < ORD - 1; ++g)
+            lxf[n][g][h] = *reinterpret_cast<const float4*>(
+                (const float*)a.dxs + ((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t + 4 * h);
+        }
+      } else if (okq) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (t + i >= a.L) break;
+          reinterpret_cast<float*>(&lvf[n][0])[i] = ((const float*)a.dvx)[ov + i];
+#pragma unroll
+          for (int g = 0; g < ORD - 1; ++g)
+            reinterpret_cast<float*>(&lxf[n][g][0])[i] =
+                ((const float*)a.dxs)[((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t + i];
+        }
+      }
+    }
   }
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
     const int q = lane + 64 * n;
-    if (q >= CPW * RD) break;
-    const int jj = q / RD, rr = q - jj * RD;
+    if (q >= CPW * NCH) break;
+    const int jj = q / NCH, pc = q - jj * NCH;
     const int j = wv * CPW + jj, c = c0 + j;
-    const int t = t0 + rr;
-    float conv_last = 0.f, conv_v = 0.f;
-    if (t < a.L) {
-      // recompute the conv outputs of groups order-1 and order at t (u rows rr .. rr + K - 1)
+    // the two recomputed conv outputs (groups order-1, order) need u rows rr .. rr + K - 1
+    const int chl = (ORD - 1) * a.d + c, chv = ORD * a.d + c;
+    float wl[K], wvv[K];
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int g = ORD - 1 + e;
-        const int ch = g * a.d + c;
-        const float* tl = us + g * RU * LW;
-        float acc = a.bias[ch];
+    for (int k = 0; k < K; ++k) { wl[k] = a.w[chl * K + k]; wvv[k] = a.w[chv * K + k]; }
+    const float bl = a.bias[chl], bv = a.bias[chv];
+    const float* tl_l = us + (ORD - 1) * RU * LW;
+    const float* tl_v = us + ORD * RU * LW;
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc = fmaf(a.w[ch * K + k], tl[(rr + k) * LW + j], acc);
-        if (e == 0) conv_last = acc; else conv_v = acc;
+    for (int i = 0; i < 8; ++i) {
+      const int rr = 8 * pc + i;
+      if (rr >= RD) break;
+      const int t = t0 + rr;
+      float conv_last = 0.f, conv_v = 0.f;
+      if (t < a.L) {
+        conv_last = bl;
+        conv_v = bv;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          conv_last = fmaf(wl[k], tl_l[(rr + k) * LW + j], conv_last);
+          conv_v = fmaf(wvv[k], tl_v[(rr + k) * LW + j], conv_v);
+        }
       }
-    }
-    const float dvx = to_f32(lv[n]);
-    for (int g = 0; g < G; ++g) {
-      float v;
-      if (g < ORD - 1) v = to_f32(lx[n][g < ORD - 1 ? g : 0]);
-      else v = g == ORD - 1 ? dvx * conv_v : dvx * conv_last;
-      ds[(g * RD + rr) * LW + j] = v;
+      float dvx, xg[NX];
+      if constexpr (sizeof(T) == 2) {
+        dvx = (float)lvv[n][i];
+#pragma unroll
+        for (int g = 0; g < NX; ++g) xg[g] = (float)lxv[n][g][i];
+      } else {
+        dvx = reinterpret_cast<const float*>(&lvf[n][0])[i];
+#pragma unroll
+        for (int g = 0; g < NX; ++g) xg[g] = reinterpret_cast<const float*>(&lxf[n][g][0])[i];
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float v;
+        if (g < ORD - 1) v = xg[g < NX ? g : 0];
+        else v = g == ORD - 1 ? dvx * conv_v : dvx * conv_last;
+        ds[(g * RD + rr) * LW + j] = v;
+      }
     }
   }
   __syncthreads();
-  // du (token-major): lane = (row in 4, channel pair in 16); 4 waves x 4 rows per pass
+  // du (token-major): lane = (row in 16, 8-channel chunk in 4): one 16-B (bf16) / 2 x 16-B
+  // (fp32) store per lane and row; 4 waves x 16 rows per pass
   T* du = (T*)a.du + (size_t)b * a.L * C;
-  const int cp = 2 * (lane & 15), rsub = lane >> 4;
+  const int cc8 = 8 * (lane & 3), rsub = lane >> 2;
   for (int g = 0; g < G; ++g) {
-    const int ch = g * a.d + c0 + cp;
-    float w0[K], w1[K];
+    const int ch = g * a.d + c0 + cc8;
+    float w8[8][K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) { w0[k] = a.w[ch * K + k]; w1[k] = a.w[(ch + 1) * K + k]; }
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int k = 0; k < K; ++k) w8[e][k] = a.w[(ch + e) * K + k];
     const float* dl = ds + g * RD * LW;
-    for (int r = wv * 4 + rsub; r < TP; r += 16) {
+    for (int r = wv * 16 + rsub; r < TP; r += 64) {
       const int t = t0 + r;
       if (t >= a.L) break;
-      float a0 = 0.f, a1 = 0.f;
+      float acc[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = 0.f;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const float* src = dl + (r + K - 1 - k) * LW + cp;
-        a0 = fmaf(w0[k], src[0], a0);
-        a1 = fmaf(w1[k], src[1], a1);
+        const float* src = dl + (r + K - 1 - k) * LW + cc8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(w8[e][k], src[e], acc[e]);
       }
       T* o = du + (size_t)t * C + ch;
       if constexpr (sizeof(T) == 2) {
-        const bf16x2 v = {cvt<T>(a0), cvt<T>(a1)};
-        *reinterpret_cast<bf16x2*>(o) = v;
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)acc[e];
+        *reinterpret_cast<bf16x8*>(o) = v;
       } else {
-        *reinterpret_cast<float2*>(o) = make_float2(a0, a1);
+        *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
       }
     }
   }

@@ -139,3 +139,31 @@ def test_char_tokenizer_complement_map():
     assert CharacterTokenizer("ACGTN", 10).complement_map() == CM
     cm = CharacterTokenizer("ACGTNacgt", 10).complement_map()
     assert cm[7] == 10 and cm[11] == 11 and cm[12] == 15 and cm[13] == 14
+
+
+def test_rcps_modules_equivariance_cpu():
+    """Each RCPS building block on the CPU with plain torch submodules: RCPSEmbedding, RCPSWrapper
+    and RCPSAddNormWrapper commute with the reverse complement (flip over length and channels),
+    and RCPSLMHead maps it to the complemented, position-reversed logits -- the algebra the
+    whole-model equivariance tests rest on (modeling_rcps.py)."""
+    from dna_amd.caduceus import (RCPSAddNormWrapper, RCPSEmbedding, RCPSLMHead, RCPSWrapper,
+                                  _complement_tensor)
+    torch.manual_seed(0)
+    rc = lambda h: torch.flip(h, dims=[-2, -1])  # noqa: E731
+    cm = _complement_tensor(CM)
+    ids = torch.randint(0, 12, (2, 9))
+    emb = RCPSEmbedding(12, 6, CM)
+    e = emb(ids)
+    assert e.shape == (2, 9, 12)
+    assert torch.allclose(emb(cm[ids.flip(-1)]), rc(e))
+    h = torch.randn(2, 9, 12, dtype=torch.float64)
+    wrap = RCPSWrapper(torch.nn.Linear(6, 6).double())
+    assert torch.allclose(wrap(rc(h)), rc(wrap(h)))
+    an = RCPSAddNormWrapper(torch.nn.LayerNorm(6).double())
+    res = torch.randn_like(h)
+    y0, r0 = an(h, residual=res, prenorm=True)
+    y1, r1 = an(rc(h), residual=rc(res), prenorm=True)
+    assert torch.allclose(y1, rc(y0)) and torch.allclose(r1, rc(r0))
+    head = RCPSLMHead(6, 12, CM).double()
+    lg = head(h)
+    assert torch.allclose(head(rc(h)), lg.flip(1)[..., cm])

@@ -150,7 +150,8 @@ def test_hyena_operator_fwd_bwd_vs_oracle(d_model, L, order, bi, emb_dim):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
-@pytest.mark.parametrize("B,L,d,order,K", [(2, 1000, 64, 2, 3), (1, 4096, 128, 3, 4), (3, 64, 64, 2, 2)])
+@pytest.mark.parametrize("B,L,d,order,K", [(2, 1000, 64, 2, 3), (1, 4096, 128, 3, 4), (3, 64, 64, 2, 2),
+                                            (1, 1003, 64, 2, 3)])
 def test_hyena_fused_kernels_vs_torch(dtype, tol, B, L, d, order, K):
     """ShortConvSplit / GateOut (fused HIP kernels) fwd + bwd against the same math in torch
     fp32 (the reference's conv1d / split / gate, hyena.py:421-507) on identical inputs."""
