@@ -181,12 +181,15 @@ __global__ __launch_bounds__(NT) void sgemm_kernel(Args a) {
       const int n = n0 + wn * 64 + jp * 32 + colq;  // first of this lane's 8 columns
       float o[8];
       if constexpr (F32) {
+        // whole-vector bit casts (a bit cast of a single vector element lvalue compiled to
+        // element 0 for every r: ROCm 7.2 clang, caught by test_strided_gemm_vs_torch)
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+        const u32x4_t a0 = __builtin_bit_cast(u32x4_t, v[0]), a1 = __builtin_bit_cast(u32x4_t, v[1]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v[0][r]),
-                                                           __builtin_bit_cast(unsigned, v[1][r]), false, false);
-          o[r] = __builtin_bit_cast(float, (unsigned)sw[0]);
-          o[4 + r] = __builtin_bit_cast(float, (unsigned)sw[1]);
+          const auto sw = __builtin_amdgcn_permlane16_swap(a0[r], a1[r], false, false);
+          o[r] = __uint_as_float((unsigned)sw[0]);
+          o[4 + r] = __uint_as_float((unsigned)sw[1]);
         }
       } else {
         typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
