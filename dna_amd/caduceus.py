@@ -26,6 +26,7 @@ import torch.nn.functional as F
 
 from . import functional as DF
 from .hyena_lm import _LN_COLS, LayerNorm
+from .hyena import HipLinear, hip_linear
 from .mamba import BiMambaWrapper
 
 _TORCH_NORM = os.environ.get("DNA_CADUCEUS_TORCH_NORM", "0") == "1"  # A/B switch: torch norms
@@ -189,7 +190,7 @@ class RCPSLMHead(nn.Module):
         super().__init__()
         self.register_buffer("complement_map", _complement_tensor(complement_map))
         self.true_dim = true_dim
-        self.lm_head = nn.Linear(true_dim, vocab_size, bias=False)
+        self.lm_head = HipLinear(true_dim, vocab_size, bias=False)
 
     @property
     def weight(self):
@@ -202,9 +203,9 @@ class RCPSLMHead(nn.Module):
         c = x.shape[-1]
         if c != 2 * self.true_dim:
             raise ValueError(f"RCPSLMHead: input has {c} channels, expected 2 * {self.true_dim}")
-        fwd = F.linear(x[..., :c // 2], self.weight, self.lm_head.bias)
-        rc = F.linear(torch.flip(x[..., c // 2:], dims=[-1]), self.weight[self.complement_map, :],
-                      self.lm_head.bias)
+        fwd = hip_linear(x[..., :c // 2], self.weight, self.lm_head.bias)
+        rc = hip_linear(torch.flip(x[..., c // 2:], dims=[-1]), self.weight[self.complement_map, :],
+                        self.lm_head.bias)
         return fwd + rc
 
 
@@ -332,7 +333,7 @@ class CaduceusForMaskedLM(nn.Module):
         if cfg["rcps"]:
             self.lm_head = RCPSLMHead(cfg["d_model"], cfg["vocab_size"], cfg["complement_map"])
         else:
-            self.lm_head = nn.Linear(cfg["d_model"], cfg["vocab_size"], bias=False)
+            self.lm_head = HipLinear(cfg["d_model"], cfg["vocab_size"], bias=False)
         ic = cfg["initializer_cfg"] or {}
         self.apply(lambda m: _init_weights(m, cfg["n_layer"], **ic))
         emb = self.caduceus.backbone.embeddings.word_embeddings

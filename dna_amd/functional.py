@@ -159,6 +159,69 @@ def strided_gemm(A, sa, B, sb, C, sc, M, Nc, K, batch, splits=1, out_f32=None, b
                bn, M, Nc, K, batch, splits, N.stream_ptr())
 
 
+class StridedLinear(torch.autograd.Function):
+    """y[L, N] = x[L, K] . w[N, K]^T + b on the strided MFMA GEMM (dna_gemm_bf16_strided /
+    dna_gemm_f32_strided) for skinny projections over many tokens (the HyenaDNA implicit-filter
+    MLP, the char-vocabulary LM heads): the weight gradient's L-long contraction runs as fp32
+    split-K slices summed once by dna_sum_slices_accum (rounded once, as one GEMM with fp32
+    accumulation would), the bias gradient as an fp32 column sum. x / w / b in one dtype."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        _gpu(x, w, b)
+        L, K = x.shape
+        Nn = w.shape[0]
+        x = x.contiguous()
+        w = w.contiguous()
+        y = torch.empty(L, Nn, device=x.device, dtype=x.dtype)
+        bf = None if b is None else b.float().contiguous()
+        with _timed("strided_linear", (L * (K + Nn)) * x.element_size(), "byte"):
+            strided_gemm(x, (K, 1, 0), w, (1, K, 0), y, (Nn, 0), L, Nn, K, 1, bias_n=bf)
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        L, K = x.shape
+        Nn = w.shape[0]
+        dy = dy.contiguous().to(x.dtype)
+        dx = None
+        if ctx.needs_input_grad[0]:  # dx[L, K] = dy[L, N] . w[N, K]
+            dx = torch.empty(L, K, device=x.device, dtype=x.dtype)
+            strided_gemm(dy, (Nn, 1, 0), w, (K, 1, 0), dx, (K, 0), L, K, Nn, 1)
+        s = int(N.lib().dna_gemm_strided_splits(Nn, K, L, 1))
+        part = torch.empty(s, Nn, K, device=x.device, dtype=torch.float32)
+        if x.dtype == torch.bfloat16:  # dW[N, K] = sum_l dy[l, n] x[l, k]
+            strided_gemm(dy, (1, Nn, 0), x, (K, 1, 0), part, (K, Nn * K), Nn, K, L, 1, s,
+                            out_f32=True)
+        else:
+            strided_gemm(dy, (1, Nn, 0), x, (K, 1, 0), part, (K, Nn * K), Nn, K, L, 1, s)
+        dw = torch.zeros(Nn, K, device=x.device, dtype=torch.float32)
+        N.call("dna_sum_slices_accum", part.data_ptr(), s, Nn * K, dw.data_ptr(), N.stream_ptr())
+        db = dy.float().sum(0).to(dy.dtype) if ctx.has_b else None
+        return dx, dw.to(w.dtype), db
+
+
+def strided_linear(x, weight, bias=None):
+    """F.linear(x, weight, bias) with nn.Linear's dtype flow (under autocast x, W and b in the
+    autocast dtype, output in it, bias added inside the product) on StridedLinear; x [..., K]."""
+    w, b = weight, bias
+    if torch.is_autocast_enabled(x.device.type):
+        dt = torch.get_autocast_dtype(x.device.type)
+        x, w, b = x.to(dt), w.to(dt), (b.to(dt) if b is not None else None)
+    else:
+        b = b.to(x.dtype) if b is not None else None
+        w = w.to(x.dtype)
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        raise NotImplementedError(f"strided_linear in {x.dtype}")
+    lead = x.shape[:-1]
+    with torch.autocast(x.device.type, enabled=False):
+        y = StridedLinear.apply(x.reshape(-1, x.shape[-1]), w, b)
+    return y.reshape(*lead, w.shape[0])
+
+
 # ----------------------------------------------------------------------------------- fused LN
 class FusedLayerNorm(torch.autograd.Function):
     """LN(dropout(act(x + bias)) + residual) -> (y fp32|None, y_bf16|None).

@@ -23,25 +23,34 @@ from .functional import _dt, _gpu, _p, _timed
 _TORCH_LINEAR = os.environ.get("DNA_HYENA_TORCH_LINEAR", "0") == "1"  # A/B switch: torch Linear
 
 
+def hip_linear(x, weight, bias=None):
+    """F.linear(x, weight, bias) with autocast nn.Linear's dtype flow on hand-written kernels:
+    under CUDA bf16 autocast with K % 64 == 0 and N % 256 == 0 the persistent MFMA GEMM
+    (`dna_linear_fwd`, dgrad on a transposed bf16 weight copy, fp32 split-K weight gradient);
+    every other CUDA case -- fp32, skinny or ragged N such as a 16-token character vocabulary --
+    the strided MFMA GEMM (`functional.strided_linear`). CPU tensors (module-level CPU tests)
+    and DNA_HYENA_TORCH_LINEAR=1 (A/B) keep torch's linear."""
+    K, Nout = weight.shape[1], weight.shape[0]
+    if _TORCH_LINEAR or not x.is_cuda:
+        return F.linear(x, weight, bias)
+    if (K % 64 or Nout % 256 or not torch.is_autocast_enabled("cuda")
+            or torch.get_autocast_dtype("cuda") != torch.bfloat16):
+        return DF.strided_linear(x, weight, bias)
+    w_lp = weight.to(torch.bfloat16)
+    y = _LinearFn.apply(x.reshape(-1, K).to(torch.bfloat16), weight, w_lp, bias,
+                        w_lp.t().contiguous())
+    return y.view(*x.shape[:-1], Nout)
+
+
 class HipLinear(nn.Linear):
-    """nn.Linear (same parameters / state_dict) whose bf16-autocast forward and data gradient run
-    on the persistent MFMA GEMM (`dna_linear_fwd`, dgrad on a transposed bf16 weight copy) and
-    whose weight gradient is the fp32 split-K GEMM of functional.Linear -- the projections of the
-    Hyena operator (in_proj / out_proj, hyena.py:311-509) and of the HyenaDNA Block's Mlp
-    (fc1 / fc2). The reference runs them as autocast nn.Linear (bf16 GEMM of the bf16-cast input
-    and weight, bf16 output, fp32 weight / bias gradients): same operands, same output dtype.
-    Outside CUDA bf16 autocast, or for shapes the kernel does not take (K % 64, N % 256),
-    it is torch's Linear."""
+    """nn.Linear (same parameters / state_dict) running `hip_linear`: the projections of the
+    Hyena operator (in_proj / out_proj, hyena.py:311-509), the HyenaDNA Block's Mlp (fc1 / fc2)
+    and the LM heads. The reference runs them as autocast nn.Linear (bf16 GEMM of the bf16-cast
+    input and weight, bf16 output, fp32 weight / bias gradients): same operands, same output
+    dtype."""
 
     def forward(self, x):
-        if (_TORCH_LINEAR or not x.is_cuda or self.in_features % 64 or self.out_features % 256
-                or not torch.is_autocast_enabled("cuda")
-                or torch.get_autocast_dtype("cuda") != torch.bfloat16):
-            return super().forward(x)
-        w_lp = self.weight.to(torch.bfloat16)
-        y = _LinearFn.apply(x.reshape(-1, self.in_features).to(torch.bfloat16), self.weight, w_lp,
-                            self.bias, w_lp.t().contiguous())
-        return y.view(*x.shape[:-1], self.out_features)
+        return hip_linear(x, self.weight, self.bias)
 
 
 def _bytes_per_elem(t):
@@ -308,74 +317,16 @@ class ExponentialModulation(_OptimModule):
         return x * (torch.exp(-t * self.deltas.abs()) + self.shift)
 
 
-class _FilterLinear(torch.autograd.Function):
-    """y[L, N] = x[L, K] . w[N, K]^T + b for the implicit filter MLP on the strided MFMA GEMM
-    (dna_gemm_bf16_strided / dna_gemm_f32_strided): the weight gradient's L-long contraction runs
-    as fp32 split-K slices summed once by dna_sum_slices_accum (rounded once, as one GEMM with fp32
-    accumulation would), the bias gradient as an fp32 column sum. x / w / b in one dtype."""
-
-    @staticmethod
-    def forward(ctx, x, w, b):
-        _gpu(x, w, b)
-        L, K = x.shape
-        Nn = w.shape[0]
-        x = x.contiguous()
-        w = w.contiguous()
-        y = torch.empty(L, Nn, device=x.device, dtype=x.dtype)
-        bf = None if b is None else b.float().contiguous()
-        with _timed("filter_linear", (L * (K + Nn)) * x.element_size(), "byte"):
-            DF.strided_gemm(x, (K, 1, 0), w, (1, K, 0), y, (Nn, 0), L, Nn, K, 1, bias_n=bf)
-        ctx.save_for_backward(x, w)
-        ctx.has_b = b is not None
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, w = ctx.saved_tensors
-        L, K = x.shape
-        Nn = w.shape[0]
-        dy = dy.contiguous().to(x.dtype)
-        dx = None
-        if ctx.needs_input_grad[0]:  # dx[L, K] = dy[L, N] . w[N, K]
-            dx = torch.empty(L, K, device=x.device, dtype=x.dtype)
-            DF.strided_gemm(dy, (Nn, 1, 0), w, (K, 1, 0), dx, (K, 0), L, K, Nn, 1)
-        s = int(N.lib().dna_gemm_strided_splits(Nn, K, L, 1))
-        part = torch.empty(s, Nn, K, device=x.device, dtype=torch.float32)
-        if x.dtype == torch.bfloat16:  # dW[N, K] = sum_l dy[l, n] x[l, k]
-            DF.strided_gemm(dy, (1, Nn, 0), x, (K, 1, 0), part, (K, Nn * K), Nn, K, L, 1, s,
-                            out_f32=True)
-        else:
-            DF.strided_gemm(dy, (1, Nn, 0), x, (K, 1, 0), part, (K, Nn * K), Nn, K, L, 1, s)
-        dw = torch.zeros(Nn, K, device=x.device, dtype=torch.float32)
-        N.call("dna_sum_slices_accum", part.data_ptr(), s, Nn * K, dw.data_ptr(), N.stream_ptr())
-        db = dy.float().sum(0).to(dy.dtype) if ctx.has_b else None
-        return dx, dw.to(w.dtype), db
-
-
 def _split_k_linear(x, lin):
     """nn.Linear over the L positions of the implicit filter MLP ([1, L, K] -> [1, L, N], K 3-5
-    and N 64-256) on the strided MFMA GEMM (`_FilterLinear`). As one library GEMM its weight
-    gradient is a 64 x 64 (or 256 x 64) output reduced over all L = 65,536 positions, which
-    hipBLASLt ran as one or four workgroups (~210 us per call, 12 % of the config-D step); here the
-    contraction is split over the CUs. Same dtype flow as nn.Linear: under autocast x, W and b are
-    cast to the autocast dtype and the output is in it (bias added in the product's epilogue, in
-    fp32, as addmm does); the gradients are rounded once. CPU tensors keep the plain linear
-    (parity tests of the module on the CPU)."""
+    and N 64-256) on the strided MFMA GEMM (`functional.strided_linear`). As one library GEMM
+    its weight gradient is a 64 x 64 (or 256 x 64) output reduced over all L = 65,536 positions,
+    which hipBLASLt ran as one or four workgroups (~210 us per call, 12 % of the config-D step);
+    here the contraction is split over the CUs. CPU tensors keep the plain linear (parity tests of
+    the module on the CPU)."""
     if not x.is_cuda or x.dim() != 3 or x.shape[0] != 1:
         return lin(x)
-    L = x.shape[-2]
-    w, b = lin.weight, lin.bias
-    if torch.is_autocast_enabled(x.device.type):
-        dt = torch.get_autocast_dtype(x.device.type)
-        x, w, b = x.to(dt), w.to(dt), (b.to(dt) if b is not None else None)
-    else:
-        b = b.to(x.dtype) if b is not None else None
-        w = w.to(x.dtype)
-    if x.dtype not in (torch.bfloat16, torch.float32):
-        raise NotImplementedError(f"implicit filter MLP in {x.dtype}")
-    with torch.autocast(x.device.type, enabled=False):
-        y = _FilterLinear.apply(x.reshape(L, -1), w, b)
-    return y.reshape(1, L, -1)
+    return DF.strided_linear(x, lin.weight, lin.bias)
 
 
 class HyenaFilter(_OptimModule):

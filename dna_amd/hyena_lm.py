@@ -183,7 +183,7 @@ class BertLMHeadModel(nn.Module):
         if vocab_size % pad_vocab_size_multiple:
             vocab_size += pad_vocab_size_multiple - vocab_size % pad_vocab_size_multiple
         self.backbone = LMBackbone(d_model, n_layer, d_inner, vocab_size, **kwargs)
-        self.lm_head = nn.Linear(d_model, vocab_size, bias=False)
+        self.lm_head = HipLinear(d_model, vocab_size, bias=False)
         self.apply(partial(_init_weights, n_layer=n_layer,
                            **(kwargs.get("initializer_cfg") or {})))
         self.lm_head.weight = self.backbone.embeddings.word_embeddings.weight

@@ -281,9 +281,10 @@ class InProj(torch.autograd.Function):
 
 class OutProj(torch.autograd.Function):
     """out_proj of mamba_ssm Mamba.forward on the scan output y [b, E, L] (channel-major):
-    out [b, L, d] = y^T . W^T (+ bias). Forward and data gradient on hipBLASLt (transposed-operand
-    GEMMs at ~1.2 PF/s); the weight gradient (contraction over all b*L tokens into [d, E]) as fp32
-    split-K slices on the strided MFMA GEMM, reading y where it lies."""
+    out [b, L, d] = y^T . W^T (+ bias). Forward on hipBLASLt (a transposed-operand GEMM at
+    ~1.2 PF/s); the data gradient straight into the channel-major [b, E, L] layout the scan's
+    backward reads (token-major, it cost a 268-MB transpose copy per call) and the weight gradient
+    (contraction over all b*L tokens into [d, E], fp32 split-K slices) on the strided MFMA GEMM."""
 
     @staticmethod
     def forward(ctx, y, weight, bias):
@@ -314,8 +315,10 @@ class OutProj(torch.autograd.Function):
         dout = dout.to(dt).contiguous()
         dy = dw = db = None
         with torch.autocast("cuda", enabled=False):
-            if ctx.needs_input_grad[0]:
-                dy = (dout @ w).transpose(1, 2).to(ydt)   # [b, E, L] view
+            if ctx.needs_input_grad[0]:  # dy[b][e][l] = sum_o W[o][e] dout[b][l][o], channel-major
+                dy = torch.empty(b, E, L, device=dout.device, dtype=dt)
+                DF.strided_gemm(w, (1, E, 0), dout, (1, d, L * d), dy, (L, E * L), E, L, d, b)
+                dy = dy.to(ydt)
             if ctx.needs_input_grad[1]:  # dW[o][e] = sum_{b,l} dout[b][l][o] y[b][e][l]
                 part, _ = _wgrad_tokens(dout, (1, d, L * d), yc, (1, yc.stride(1), yc.stride(0)),
                                         d, E, L, b)
