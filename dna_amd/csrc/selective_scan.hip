@@ -673,9 +673,9 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
       ddl[i] = 0.f; du[i] = Dd * dy[i]; y[i] = 0.f; dDacc = fmaf(dy[i], uu[i], dDacc);
       dlu[i] = dl[i] * uu[i]; tl += dl[i];
     }
-#pragma unroll 1
-    for (int st = 0; st < N; ++st) {
-      const int n = (st + w) % N;
+    // one state's share of the backward (its dB / dC accumulator row is this wave's alone in the
+    // current step)
+    auto state = [&](const int n) __attribute__((always_inline)) {
       float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
       lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
       lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
@@ -723,7 +723,23 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
       }
       const float dAs = wsum(dAn);
       if (lane == n) dAl = dAs;
-      __syncthreads();
+    };
+    if constexpr (R == 1 && N / 2 >= CW) {
+      // two states per step (wave w: states 2((st + w) mod N/2) and + 1, still one writer per
+      // accumulator row): half the barriers, and the two states' scans interleave
+#pragma unroll 1
+      for (int st = 0; st < N / 2; ++st) {
+        const int n0 = 2 * ((st + w) % (N / 2));
+        state(n0);
+        state(n0 + 1);
+        __syncthreads();
+      }
+    } else {
+#pragma unroll 1
+      for (int st = 0; st < N; ++st) {
+        state((st + w) % N);
+        __syncthreads();
+      }
     }
     float dd[ITEMS], dbacc = 0.f;
 #pragma unroll

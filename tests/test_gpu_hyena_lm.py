@@ -194,3 +194,28 @@ def test_implicit_filter_split_k_linear_matches_linear():
         assert (y1 - y0).abs().max().item() <= 1e-5 * y0.abs().max().item() + 1e-6
         for a, b in zip(g1, g0):
             assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("autocast", [True, False])
+def test_config_d_model_has_no_library_gemm(autocast, monkeypatch):
+    """Config D's model (HyenaDNA LM: Hyena in/out projections, Block MLP, implicit-filter MLP, LM
+    head) runs forward and backward with every torch GEMM entry point banned -- under bf16
+    autocast (persistent MFMA GEMM + strided MFMA GEMM) and in fp32 (strided fp32 MFMA GEMM):
+    no hipBLASLt / rocBLAS call is left in the HyenaDNA path."""
+    from test_gpu_model import _ban_library_gemm
+    torch.manual_seed(3)
+    L = 1024
+    m = _config_d_model(2, L).to(DEV)
+    ids = torch.randint(7, 11, (1, L), device=DEV)
+    mask = torch.ones(1, L, dtype=torch.bool, device=DEV)
+    with monkeypatch.context() as mp:
+        _ban_library_gemm(mp)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            (out, _) = m((ids, mask))
+        logits = out.logits[0]
+        loss = torch.nn.functional.cross_entropy(logits.float().reshape(-1, logits.shape[-1]),
+                                                 ids.reshape(-1))
+        loss.backward()
+    assert torch.isfinite(loss)
+    grads = [p.grad for p in m.parameters() if p.grad is not None]
+    assert len(grads) > 10 and all(torch.isfinite(g).all() for g in grads)
