@@ -8,8 +8,9 @@
 // Backward (act = SiLU recomputed from x): g = dout * silu'(pre),
 //   dx[t] = sum_k w[k] g[t + K-1-k]  (g = 0 past L),  dw[k] = sum_t g[t] x[t + k - (K-1)],
 //   dbias = sum_t g[t]  -- dw/dbias as one partial row per block, summed by dna_colsum_f32.
-// A block = 256 threads x 4 positions = 1024 positions of one (b, c) row; the K-1 halo comes
-// from LDS. HBM-bound (reads x, writes out; bwd reads x, dout, writes dx).
+// Element path: a block = 256 threads x 4 positions = 1024 positions of one (b, c) row, the K-1
+// halo from LDS. 16-B path (L % 8 == 0, aligned rows; the Caduceus shapes): 8 positions per lane,
+// halos by lane shuffles (below). HBM-bound (reads x, writes out; bwd reads x, dout, writes dx).
 #include "common.h"
 
 namespace dna {
@@ -127,6 +128,190 @@ __global__ __launch_bounds__(256) void bwd_kernel(const T* __restrict__ x, size_
   }
 }
 
+// ---- vectorised forms (rows 16-B aligned, L % 8 == 0): a lane owns 8 consecutive positions
+// (one 16-B bf16 / two 16-B fp32 loads per tensor, the same for the stores), the K-1 halo comes
+// from the neighbouring lane by a shuffle and, at a wave's edge, from a direct load; no LDS, no
+// block barrier in the forward. Block = 4 waves x 64 lanes x 8 = 2048 positions of one row.
+constexpr int VPL = 8;
+constexpr int VSEG = 256 * VPL;
+
+template <typename T>
+__device__ __forceinline__ void ld8v(const T* p, float (&v)[VPL]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 q = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) v[i] = (float)q[i];
+  } else {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[i] = a[i]; v[4 + i] = b[i]; }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8v(T* p, const float (&v)[VPL]) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 q;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) q[i] = (bf16)v[i];
+    *reinterpret_cast<bf16x8*>(p) = q;
+  } else {
+    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+template <typename T, int K>
+__global__ __launch_bounds__(256) void fwd_vec_kernel(const T* __restrict__ x, size_t x_bstride,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ bias, int C, int L,
+                                                      int silu, T* __restrict__ out) {
+  const int c = blockIdx.y, b = blockIdx.z, lane = threadIdx.x & 63;
+  const int t0 = blockIdx.x * VSEG + threadIdx.x * VPL;
+  const T* row = x + (size_t)b * x_bstride + (size_t)c * L;
+  float v[VPL];
+  if (t0 < L) ld8v(row + t0, v);
+  else {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) v[i] = 0.f;
+  }
+  // h[k] = x[t0 - (K-1) + k], k < K-1: the previous lane's last K-1 (0 before the row)
+  float h[K > 1 ? K - 1 : 1];
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k) {
+    h[k] = __shfl_up(v[VPL - (K - 1) + k], 1, 64);
+    if (lane == 0) {
+      const int t = t0 - (K - 1) + k;
+      h[k] = (t >= 0 && t < L) ? to_f32(row[t]) : 0.f;
+    }
+  }
+  if (t0 >= L) return;
+  float wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wk[k] = w[c * K + k];
+  const float bc = bias ? bias[c] : 0.f;
+  float o[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    float acc = bc;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int q = j + k - (K - 1);  // x index relative to t0
+      acc = fmaf(wk[k], q < 0 ? h[q + K - 1] : v[q], acc);
+    }
+    if (silu) acc *= sigm(acc);
+    o[j] = acc;
+  }
+  st8v(out + ((size_t)b * C + c) * L + t0, o);
+}
+
+template <typename T, int K>
+__global__ __launch_bounds__(256) void bwd_vec_kernel(const T* __restrict__ x, size_t x_bstride,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ bias,
+                                                      const T* __restrict__ dout, int C, int L,
+                                                      int silu, T* __restrict__ dx,
+                                                      size_t dx_bstride, float* __restrict__ part) {
+  __shared__ float red[4][MAXK + 1];
+  const int c = blockIdx.y, b = blockIdx.z, lane = threadIdx.x & 63;
+  const int t0 = blockIdx.x * VSEG + threadIdx.x * VPL;
+  const bool live = t0 < L;
+  const T* row = x + (size_t)b * x_bstride + (size_t)c * L;
+  const T* drow = dout + ((size_t)b * C + c) * L;
+  float xv[VPL], dv[VPL];
+  if (live) { ld8v(row + t0, xv); ld8v(drow + t0, dv); }
+  else {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) xv[i] = dv[i] = 0.f;
+  }
+  float wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wk[k] = w[c * K + k];
+  const float bc = bias ? bias[c] : 0.f;
+  // x halo before t0 (previous lane / direct load at the wave's edge)
+  float xh[K > 1 ? K - 1 : 1];
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k) {
+    xh[k] = __shfl_up(xv[VPL - (K - 1) + k], 1, 64);
+    if (lane == 0) {
+      const int t = t0 - (K - 1) + k;
+      xh[k] = (t >= 0 && t < L) ? to_f32(row[t]) : 0.f;
+    }
+  }
+  auto xat = [&](int q) { return q < 0 ? xh[q + K - 1] : xv[q]; };  // x[t0 + q], q in [-(K-1), 8)
+  // g = dout * silu'(pre) on the lane's 8 positions
+  float g[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    float gj = dv[j];
+    if (silu) {
+      float pre = bc;
+#pragma unroll
+      for (int k = 0; k < K; ++k) pre = fmaf(wk[k], xat(j + k - (K - 1)), pre);
+      const float s = sigm(pre);
+      gj *= s * fmaf(pre, 1.f - s, 1.f);
+    }
+    g[j] = (t0 + j < L) ? gj : 0.f;
+  }
+  // g halo after the lane: the next lane's first K-1; lane 63 computes them itself
+  float gh[K > 1 ? K - 1 : 1];
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k) gh[k] = __shfl_down(g[k], 1, 64);
+  if (lane == 63) {
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) {
+      const int t = t0 + VPL + k;
+      float gk = 0.f;
+      if (t < L) {
+        gk = to_f32(drow[t]);
+        if (silu) {
+          float pre = bc;
+#pragma unroll
+          for (int kk = 0; kk < K; ++kk) {
+            const int q = VPL + k + kk - (K - 1);  // relative to t0
+            const float xq = q < VPL ? xat(q) : to_f32(row[t0 + q]);
+            pre = fmaf(wk[kk], xq, pre);
+          }
+          const float s = sigm(pre);
+          gk *= s * fmaf(pre, 1.f - s, 1.f);
+        }
+      }
+      gh[k] = gk;
+    }
+  }
+  float sw[K + 1];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) sw[k] = 0.f;
+  if (live) {
+    float o[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int q = j + K - 1 - k;  // g index relative to t0
+        acc = fmaf(wk[k], q < VPL ? g[q] : gh[q - VPL], acc);
+      }
+      o[j] = acc;
+#pragma unroll
+      for (int k = 0; k < K; ++k) sw[k] = fmaf(g[j], xat(j + k - (K - 1)), sw[k]);
+      sw[K] += g[j];
+    }
+    st8v(dx + (size_t)b * dx_bstride + (size_t)c * L + t0, o);
+  }
+#pragma unroll
+  for (int k = 0; k <= K; ++k) sw[k] = wave_sum(sw[k]);
+  const int wv = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k <= K; ++k) red[wv][k] = sw[k];
+  }
+  __syncthreads();
+  if (threadIdx.x <= K) {
+    const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    part[((size_t)b * gridDim.x + blockIdx.x) * C * (K + 1) + (size_t)c * (K + 1) + threadIdx.x] = s;
+  }
+}
+
 template <typename F>
 int dispatch(int dtype, int K, F&& f) {
   if (dtype != DNA_F32 && dtype != DNA_BF16) return -1;
@@ -145,23 +330,37 @@ int dispatch(int dtype, int K, F&& f) {
 using namespace dna;
 using namespace dna::cconv;
 
+// the 16-B path: every row start 16-B aligned (L and the batch stride multiples of 8 elements)
+static bool conv_vec_ok(const void* p, size_t bstride, int L) {
+  return ((uintptr_t)p & 15) == 0 && L % 8 == 0 && bstride % 8 == 0;
+}
+
 extern "C" int dna_causal_conv1d_fwd(const void* x, size_t x_bstride, int dtype, const float* w,
                                      const float* bias, int B, int C, int L, int K, int silu,
                                      void* out, void* stream) {
   DNA_CHECK_ARG(x && w && out && B > 0 && C > 0 && L > 0, "dna_causal_conv1d_fwd: bad args");
-  const dim3 grid((L + SEG - 1) / SEG, C, B);
+  const bool vec = conv_vec_ok(x, x_bstride, L) && conv_vec_ok(out, (size_t)C * L, L);
+  const dim3 grid(vec ? (L + VSEG - 1) / VSEG : (L + SEG - 1) / SEG, C, B);
   hipStream_t s = as_stream(stream);
   const int st = dispatch(dtype, K, [&](auto t, auto kk) {
     using T = decltype(t);
-    hipLaunchKernelGGL((fwd_kernel<T, decltype(kk)::value>), grid, dim3(256), 0, s, (const T*)x,
-                       x_bstride, w, bias, C, L, silu, (T*)out);
+    if (vec)
+      hipLaunchKernelGGL((fwd_vec_kernel<T, decltype(kk)::value>), grid, dim3(256), 0, s, (const T*)x,
+                         x_bstride, w, bias, C, L, silu, (T*)out);
+    else
+      hipLaunchKernelGGL((fwd_kernel<T, decltype(kk)::value>), grid, dim3(256), 0, s, (const T*)x,
+                         x_bstride, w, bias, C, L, silu, (T*)out);
   });
   DNA_CHECK_ARG(st == 0, "dna_causal_conv1d_fwd: kernel size %d / dtype %d unsupported (2..4; f32/bf16)", K, dtype);
   DNA_LAUNCH_CHECK("dna_causal_conv1d_fwd");
   return DNA_OK;
 }
 
-extern "C" size_t dna_causal_conv1d_part_rows(int B, int L) { return (size_t)B * ((L + SEG - 1) / SEG); }
+// partial rows of the backward's dw / dbias: one per (batch, block); the 16-B path (L % 8 == 0)
+// uses 2048-position blocks, the element path 1024
+extern "C" size_t dna_causal_conv1d_part_rows(int B, int L) {
+  return (size_t)B * (L % 8 == 0 ? (L + VSEG - 1) / VSEG : (L + SEG - 1) / SEG);
+}
 
 extern "C" int dna_causal_conv1d_bwd(const void* x, size_t x_bstride, int dtype, const float* w,
                                      const float* bias, const void* dout, int B, int C, int L,
@@ -169,12 +368,21 @@ extern "C" int dna_causal_conv1d_bwd(const void* x, size_t x_bstride, int dtype,
                                      void* stream) {
   DNA_CHECK_ARG(x && w && dout && dx && part && B > 0 && C > 0 && L > 0,
                 "dna_causal_conv1d_bwd: bad args");
-  const dim3 grid((L + SEG - 1) / SEG, C, B);
+  // the partial-row count must match dna_causal_conv1d_part_rows (it depends on L only): a
+  // misaligned pointer with L % 8 == 0 takes the element kernel on 2048-position blocks' rows
+  const bool vec = L % 8 == 0 && conv_vec_ok(x, x_bstride, L) && conv_vec_ok(dout, (size_t)C * L, L) &&
+                   conv_vec_ok(dx, dx_bstride, L);
+  DNA_CHECK_ARG(vec || L % 8 != 0, "dna_causal_conv1d_bwd: L %% 8 == 0 needs 16-B aligned rows");
+  const dim3 grid(vec ? (L + VSEG - 1) / VSEG : (L + SEG - 1) / SEG, C, B);
   hipStream_t s = as_stream(stream);
   const int st = dispatch(dtype, K, [&](auto t, auto kk) {
     using T = decltype(t);
-    hipLaunchKernelGGL((bwd_kernel<T, decltype(kk)::value>), grid, dim3(256), 0, s, (const T*)x,
-                       x_bstride, w, bias, (const T*)dout, C, L, silu, (T*)dx, dx_bstride, part);
+    if (vec)
+      hipLaunchKernelGGL((bwd_vec_kernel<T, decltype(kk)::value>), grid, dim3(256), 0, s, (const T*)x,
+                         x_bstride, w, bias, (const T*)dout, C, L, silu, (T*)dx, dx_bstride, part);
+    else
+      hipLaunchKernelGGL((bwd_kernel<T, decltype(kk)::value>), grid, dim3(256), 0, s, (const T*)x,
+                         x_bstride, w, bias, (const T*)dout, C, L, silu, (T*)dx, dx_bstride, part);
   });
   DNA_CHECK_ARG(st == 0, "dna_causal_conv1d_bwd: kernel size %d / dtype %d unsupported (2..4; f32/bf16)", K, dtype);
   DNA_LAUNCH_CHECK("dna_causal_conv1d_bwd");
