@@ -57,6 +57,7 @@ _SIGS = {
     "dna_embed_grad_segsum_workspace": (_sz, [_i, _i]),
     "dna_embed_grad_segsum": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "dna_sum_slices_accum": (_i, [_vp, _i, _sz, _vp, _vp]),
+    "dna_sum_slices": (_i, [_vp, _i, _sz, _vp, _vp]),
     "dna_geglu_fwd": (_i, [_vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_geglu_bwd": (_i, [_vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),

@@ -13,19 +13,21 @@
 namespace dna {
 namespace gacc {
 
+// accum: out += sum (gradient accumulation); else out = sum (no zero fill needed first). The
+// slices are added in slice order either way (deterministic).
 __global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict__ parts, int s,
                                                          size_t n, float* __restrict__ out,
-                                                         int vec) {
+                                                         int vec, int accum) {
   const size_t n4 = vec ? n / 4 : 0;  // 16-B path when every slice starts 16-B aligned
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
-    f32x4 acc = reinterpret_cast<const f32x4*>(out)[i];
+    f32x4 acc = accum ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < s; ++k) acc += reinterpret_cast<const f32x4*>(parts + (size_t)k * n)[i];
     reinterpret_cast<f32x4*>(out)[i] = acc;
   }
   for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
-    float acc = out[i];
+    float acc = accum ? out[i] : 0.f;
     for (int k = 0; k < s; ++k) acc += parts[(size_t)k * n + i];
     out[i] = acc;
   }
@@ -185,8 +187,20 @@ extern "C" int dna_sum_slices_accum(const float* parts, int s, size_t n, float* 
   size_t blocks = ((vec ? n / 4 : n) + 255) / 256;
   int nb = (int)(blocks < 4096 ? (blocks ? blocks : 1) : 4096);
   hipLaunchKernelGGL(gacc::sum_slices_kernel, dim3(nb), dim3(256), 0, as_stream(stream), parts, s,
-                     n, out, vec);
+                     n, out, vec, 1);
   DNA_LAUNCH_CHECK("dna_sum_slices_accum");
+  return DNA_OK;
+}
+
+extern "C" int dna_sum_slices(const float* parts, int s, size_t n, float* out, void* stream) {
+  DNA_CHECK_ARG(parts && out && s >= 1, "dna_sum_slices: bad args");
+  if (n == 0) return DNA_OK;
+  const int vec = (((uintptr_t)parts | (uintptr_t)out) & 15) == 0 && n % 4 == 0;
+  size_t blocks = ((vec ? n / 4 : n) + 255) / 256;
+  int nb = (int)(blocks < 4096 ? (blocks ? blocks : 1) : 4096);
+  hipLaunchKernelGGL(gacc::sum_slices_kernel, dim3(nb), dim3(256), 0, as_stream(stream), parts, s,
+                     n, out, vec, 0);
+  DNA_LAUNCH_CHECK("dna_sum_slices");
   return DNA_OK;
 }
 

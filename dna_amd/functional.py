@@ -198,8 +198,8 @@ class StridedLinear(torch.autograd.Function):
                             out_f32=True)
         else:
             strided_gemm(dy, (1, Nn, 0), x, (K, 1, 0), part, (K, Nn * K), Nn, K, L, 1, s)
-        dw = torch.zeros(Nn, K, device=x.device, dtype=torch.float32)
-        N.call("dna_sum_slices_accum", part.data_ptr(), s, Nn * K, dw.data_ptr(), N.stream_ptr())
+        dw = torch.empty(Nn, K, device=x.device, dtype=torch.float32)
+        N.call("dna_sum_slices", part.data_ptr(), s, Nn * K, dw.data_ptr(), N.stream_ptr())
         db = dy.float().sum(0).to(dy.dtype) if ctx.has_b else None
         return dx, dw.to(w.dtype), db
 

@@ -193,10 +193,7 @@ class ChannelLinear(torch.autograd.Function):
                 _strided_gemm(dy, (dy.stride(1), 1, dy.stride(0)), xin,
                               (1, xin.stride(1), xin.stride(0)), part, (K, M * K), M, K, L, b, s,
                               out_f32=True)
-            dw = torch.zeros(M, K, device=xin.device, dtype=torch.float32)
-            N.call("dna_sum_slices_accum", part.data_ptr(), b * s, M * K, dw.data_ptr(),
-                   N.stream_ptr())
-            dw = dw.to(wdt)
+            dw = _sum_parts(part, (M, K), wdt)
         return (None if dx is None else dx.to(xdt)), dw
 
 
@@ -214,8 +211,8 @@ def _wgrad_tokens(dy, sa, x, sb, M, Nn, T, batch, part=None, row0=0, rows_total=
 
 
 def _sum_parts(part, shape, dtype):
-    out = torch.zeros(shape, device=part.device, dtype=torch.float32)
-    N.call("dna_sum_slices_accum", part.data_ptr(), part.shape[0], out.numel(), out.data_ptr(),
+    out = torch.empty(shape, device=part.device, dtype=torch.float32)
+    N.call("dna_sum_slices", part.data_ptr(), part.shape[0], out.numel(), out.data_ptr(),
            N.stream_ptr())
     return out.to(dtype)
 
@@ -272,7 +269,10 @@ class InProj(torch.autograd.Function):
                     dw = torch.zeros_like(w, dtype=wdt)
                 else:
                     s = int(N.lib().dna_gemm_strided_splits(E, d, T, 1))
-                    part = torch.zeros(s, E2, d, device=h2.device, dtype=torch.float32)
+                    # both halves written in full when dx and dz are both there; else the
+                    # missing half's rows must read as zero
+                    alloc = torch.empty if len(halves) == 2 else torch.zeros
+                    part = alloc(s, E2, d, device=h2.device, dtype=torch.float32)
                     for i, g in halves:  # dW[c][j] = sum_t g[c][t] h[t][j]
                         _wgrad_tokens(g, (T, 1, 0), h2, (d, 1, 0), E, d, T, 1, part, i * E, E2)
                     dw = _sum_parts(part, (E2, d), wdt)

@@ -181,6 +181,9 @@ int dna_colsum_f32(const float* part, int rows, int cols, float* out, int accumu
  * into the flat fp32 gradient buffer (16-byte loads when the buffers are 16-byte aligned and
  * n % 4 == 0, element-wise otherwise). */
 int dna_sum_slices_accum(const float* parts, int s, size_t n, float* out, void* stream);
+/* out = sum_k parts[k] (same slice order; no zero fill of `out` needed): the weight gradients of
+ * the strided GEMM's split-K slices (mamba.InProj / OutProj / ChannelLinear, StridedLinear). */
+int dna_sum_slices(const float* parts, int s, size_t n, float* out, void* stream);
 
 /* ------------------------------------------------------------------ GeGLU (+ dropout)
  * a = dropout( gelu_erf(g[:, :inter]) * g[:, inter:] )   (bert_layers.py:292-296)
