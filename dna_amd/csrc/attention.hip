@@ -335,8 +335,10 @@ __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballo
 // key offset (within a 32-key half, lane half hh excluded) of accumulator register r
 __device__ __forceinline__ constexpr int aoff(int r) { return (r & 3) + 8 * (r >> 2); }
 
-template <int NQB>
-__global__ __launch_bounds__(256, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_bf16_kernel(const bf16* __restrict__ qkv,
+// NW waves per workgroup: 4 (two workgroups per CU) or 8 (one workgroup covers 512 queries, so
+// at S = 512 each (b, h)'s K/V tiles stream from HBM once instead of once per 256 queries)
+template <int NQB, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_bf16_kernel(const bf16* __restrict__ qkv,
                                                            const uint8_t* __restrict__ key_valid,
                                                            const float* __restrict__ slopes,
                                                            int S, int H, float c,
@@ -348,7 +350,8 @@ __global__ __launch_bounds__(256, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_b
   float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);  // [2][64] pad bias (log2 units)
 
   int qblk, h, b;
-  constexpr int QPB = 4 * 32 * NQB;  // queries per workgroup
+  constexpr int QPB = NW * 32 * NQB;  // queries per workgroup
+  constexpr int NTH = 64 * NW, TPI = 512 / NTH;  // threads; 16-B tile chunks per thread
   decode_block((S + QPB - 1) / QPB, H, qblk, h, b);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: branches stay uniform
@@ -376,10 +379,10 @@ __global__ __launch_bounds__(256, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_b
   }
 
   // per-lane LDS element offsets (tile buffer, kh and s add immediates)
-  int so[2];
+  int so[TPI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int cidx = tid + i * 256;
+  for (int i = 0; i < TPI; ++i) {
+    const int cidx = tid + i * NTH;
     so[i] = swz(cidx >> 3, (cidx & 7) * 8);
   }
   int kro[4];
@@ -397,8 +400,8 @@ __global__ __launch_bounds__(256, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_b
 
   auto load_tile = [&](int kt, TileRegs& t, float& bias) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int cidx = tid + i * 256;
+    for (int i = 0; i < TPI; ++i) {
+      const int cidx = tid + i * NTH;
       const bf16* src = base + (size_t)(kt * BK + (cidx >> 3)) * ld + h * D + (cidx & 7) * 8;
       t.k[i] = *reinterpret_cast<const bf16x8*>(src + H * D);
       t.v[i] = *reinterpret_cast<const bf16x8*>(src + 2 * H * D);
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(256, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_b
   };
   auto store_tile = [&](int buf, const TileRegs& t, float bias) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < TPI; ++i) {
       *reinterpret_cast<bf16x8*>(Ks + buf * BK * D + so[i]) = t.k[i];
       *reinterpret_cast<bf16x8*>(Vs + buf * BK * D + so[i]) = t.v[i];
     }
@@ -1987,6 +1990,10 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
       } else if (forced == 3) {  // one 32-query block per wave, 3 waves per SIMD (A/B)
         dim3 grid(((seqlen + 127) / 128) * heads * batch);
         hipLaunchKernelGGL((fwd2_bf16_kernel<1>), grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
+                           key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+      } else if (forced == 8) {  // eight waves, 512 queries per workgroup (A/B)
+        dim3 grid(((seqlen + 511) / 512) * heads * batch);
+        hipLaunchKernelGGL((fwd2_bf16_kernel<2, 8>), grid, dim3(512), FWD_LDS, s, (const bf16*)qkv,
                            key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
       } else {
         dim3 grid(((seqlen + BQ2 - 1) / BQ2) * heads * batch);

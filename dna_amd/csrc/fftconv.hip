@@ -121,7 +121,7 @@ __host__ __device__ __forceinline__ int seq_stride(int logM, bool col) {
   return (1 << logM) + ((1 << logM) >> 4) + (col ? 1 : 0);
 }
 
-template <int R, int LOGR, bool INV>
+template <int R, int LOGR, bool INV, int NT = NTH>  // NT threads, PPT points each
 __device__ __forceinline__ void stockham_pass(cf* buf, int G, int logM, int S, int logNs, const cf* twM) {
   constexpr int IPT = PPT / R;  // butterflies per thread
   const int M = 1 << logM;
@@ -132,7 +132,7 @@ __device__ __forceinline__ void stockham_pass(cf* buf, int G, int logM, int S, i
   cf x[IPT][R];
 #pragma unroll
   for (int it = 0; it < IPT; ++it) {
-    const int w = threadIdx.x + it * NTH;
+    const int w = threadIdx.x + it * NT;
     if (w < items) {
       const int g = w >> lognbf, j = w & ((1 << lognbf) - 1);
       const int k = j & (Ns - 1);
@@ -152,7 +152,7 @@ __device__ __forceinline__ void stockham_pass(cf* buf, int G, int logM, int S, i
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < IPT; ++it) {
-    const int w = threadIdx.x + it * NTH;
+    const int w = threadIdx.x + it * NT;
     if (w < items) {
       const int g = w >> lognbf, j = w & ((1 << lognbf) - 1);
       const int k = j & (Ns - 1);
@@ -164,16 +164,16 @@ __device__ __forceinline__ void stockham_pass(cf* buf, int G, int logM, int S, i
   __syncthreads();
 }
 
-template <bool INV>
+template <bool INV, int NT = NTH>
 __device__ __forceinline__ void fft_lds(cf* buf, int G, int logM, int S, const cf* twM) {
   int logNs = 0, left = logM;
   while (left >= 3) {
-    stockham_pass<8, 3, INV>(buf, G, logM, S, logNs, twM);
+    stockham_pass<8, 3, INV, NT>(buf, G, logM, S, logNs, twM);
     logNs += 3;
     left -= 3;
   }
-  if (left == 2) stockham_pass<4, 2, INV>(buf, G, logM, S, logNs, twM);
-  else if (left == 1) stockham_pass<2, 1, INV>(buf, G, logM, S, logNs, twM);
+  if (left == 2) stockham_pass<4, 2, INV, NT>(buf, G, logM, S, logNs, twM);
+  else if (left == 1) stockham_pass<2, 1, INV, NT>(buf, G, logM, S, logNs, twM);
 }
 
 // LDS twiddle table tw[m] = W_M^m, m < M.
@@ -366,6 +366,100 @@ __global__ FFT_BOUNDS void row_kernel(cf* __restrict__ ws, const cf* __restrict_
   }
   fft_lds<true>(buf, rw, g.logM2, S, tw);
   for (int e = threadIdx.x; e < rw * M2; e += NTH) base[e] = buf[lds_at(e >> g.logM2, e & (M2 - 1), S)];
+}
+
+// ---------------------------------------------------------------- B, backward: both gradients
+// One row block of channel d, the channel's BP pairs in turn: FFT-M2 of the dy column output ->
+// Z_dy, then (DU) Z_dy * conj(K_d), inverse FFT-M2, stored in place (the du column pass reads it),
+// and (DK) conj(Z_u) * Z_dy summed over the pairs in registers (each thread owns the same PPT
+// points every pair), inverse FFT-M2 of the sum -> pk[d]. Replaces ROW_SPEC + the dk spectrum
+// pass + ROW_INV + ROW_INV_MULCONJ: Z_dy never goes to memory, the products see the same fp32
+// values in the same order (bit-identical to the four-pass form).
+// 256-thread blocks (8 rows of 512 at N = 2^17): the PPT-point sum stays in registers (32 VGPRs
+// beside the Stockham pass's 32) without spilling, 3 waves per SIMD.
+constexpr int RB_NT = 256, RB_LOG_PTS = LOG_PTS - 1;
+__host__ __device__ __forceinline__ int log_rowbwd_group(const Geo& g) {
+  return (RB_LOG_PTS - g.logM2) < g.logM1 ? (RB_LOG_PTS - g.logM2) : g.logM1;
+}
+template <int LN, bool DK, bool DU>
+__global__ __launch_bounds__(RB_NT, 3) void row_bwd_kernel(cf* __restrict__ zy, const cf* __restrict__ zu,
+                                                           const cf* __restrict__ kspec, int BP, Geo g_,
+                                                           cf* __restrict__ pk) {
+  const Geo g = fixed<LN>(g_);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int M2 = 1 << g.logM2;
+  const int lrw = log_rowbwd_group(g), rw = 1 << lrw;
+  const int S = seq_stride(g.logM2, false);
+  cf* buf = reinterpret_cast<cf*>(smem);  // [rw][S] padded
+  cf* tw = buf + rw * S;
+  const int k10 = blockIdx.x * rw;
+  const int d = blockIdx.y;
+  const size_t roff = (size_t)k10 * M2;
+  make_table(tw, g.logM2);
+  cf acc[PPT];
+#pragma unroll
+  for (int it = 0; it < PPT; ++it) acc[it] = make_float2(0.f, 0.f);
+  const cf* ks = kspec + ((size_t)d << g.logN) + roff;
+  for (int bp = 0; bp < BP; ++bp) {
+    const int p = d * BP + bp;
+    cf* base = zy + ((size_t)p << g.logN) + roff;
+    {
+      cf v[PPT];
+#pragma unroll
+      for (int it = 0; it < PPT; ++it) {
+        const int e = threadIdx.x + it * RB_NT;
+        if (e < rw * M2) v[it] = base[e];
+      }
+      if (bp > 0) __syncthreads();  // the previous pair's reads / stores of buf are done
+#pragma unroll
+      for (int it = 0; it < PPT; ++it) {
+        const int e = threadIdx.x + it * RB_NT;
+        if (e < rw * M2) buf[lds_at(e >> g.logM2, e & (M2 - 1), S)] = v[it];
+      }
+    }
+    __syncthreads();
+    fft_lds<false, RB_NT>(buf, rw, g.logM2, S, tw);
+    const cf* zup = zu + ((size_t)p << g.logN) + roff;
+#pragma unroll 1
+    for (int c0 = 0; c0 < PPT; c0 += 8) {  // 8 spectrum loads per operand in flight
+      cf uv[8], kv[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int e = threadIdx.x + (c0 + it) * RB_NT;
+        if (e < rw * M2) {
+          if (DK) uv[it] = zup[e];
+          if (DU) kv[it] = ks[e];
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int e = threadIdx.x + (c0 + it) * RB_NT;
+        const int a = lds_at(e >> g.logM2, e & (M2 - 1), S);
+        if (e < rw * M2) {
+          const cf z = buf[a];
+          if (DK) acc[c0 + it] = cadd(acc[c0 + it], cmul(cconj(uv[it]), z));
+          if (DU) buf[a] = cmul(z, cconj(kv[it]));
+        }
+      }
+    }
+    if (DU) {
+      __syncthreads();
+      fft_lds<true, RB_NT>(buf, rw, g.logM2, S, tw);
+      for (int e = threadIdx.x; e < rw * M2; e += RB_NT) base[e] = buf[lds_at(e >> g.logM2, e & (M2 - 1), S)];
+    }
+  }
+  if (DK) {
+    __syncthreads();  // the last pair's reads / stores of buf are done
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * RB_NT;
+      if (e < rw * M2) buf[lds_at(e >> g.logM2, e & (M2 - 1), S)] = acc[it];
+    }
+    __syncthreads();
+    fft_lds<true, RB_NT>(buf, rw, g.logM2, S, tw);
+    cf* out = pk + ((size_t)d << g.logN) + roff;
+    for (int e = threadIdx.x; e < rw * M2; e += RB_NT) out[e] = buf[lds_at(e >> g.logM2, e & (M2 - 1), S)];
+  }
 }
 
 // ---------------------------------------------------------------- C: inverse column FFT over k1
@@ -596,6 +690,22 @@ void launch_row(cf* ws, const cf* kspec, Pairing pr, const Geo& g, int P, hipStr
 #undef L_
 }
 
+template <bool DK, bool DU>
+void launch_row_bwd(cf* zy, const cf* zu, const cf* kspec, int BP, int D, const Geo& g, cf* pk,
+                    hipStream_t s) {
+#define L_(LN)                                                                                   \
+  {                                                                                              \
+    auto k = row_bwd_kernel<LN, DK, DU>;                                                         \
+    const size_t lds = ((size_t)(1 << log_rowbwd_group(g)) * seq_stride(g.logM2, false) +        \
+                        (1u << g.logM2)) * sizeof(cf);                                           \
+    allow_lds(k, lds);                                                                           \
+    hipLaunchKernelGGL(k, dim3(1 << (g.logM1 - log_rowbwd_group(g)), D), dim3(RB_NT), lds, s, zy, \
+                       zu, kspec, BP, g, pk);                                                    \
+  }
+  DNA_FFT_DISPATCH(L_)
+#undef L_
+}
+
 template <typename T, int MODE>
 void launch_col_inv(const cf* ws, Pairing pr, const Geo& g, int off, void* y, float* outf, float scale,
                     int P, hipStream_t s) {
@@ -725,19 +835,29 @@ static void bwd_impl(const void* dy, const void* u, const cf* kspec, const cf* u
   }
   const cf* zuc = uspec ? uspec : zu;
   launch_col_fwd<T>(dy, pr, g, 0, zy, P, s);
-  launch_row<ROW_SPEC>(zy, nullptr, pr, g, P, s);
-  if (dk) {
-    const int bx = (int)((N + NTH - 1) / NTH) < 512 ? (int)((N + NTH - 1) / NTH) : 512;
-    hipLaunchKernelGGL(dkspec_kernel, dim3(bx, D), dim3(NTH), 0, s, zuc, (const cf*)zy, BP,
-                       g.logN, pk);
-    Pairing one{D, 1, 0};  // BP = 0: row index is the channel
-    launch_row<ROW_INV>(pk, nullptr, one, g, D, s);
-    launch_col_inv<float, OUT_REAL>(pk, one, g, 0, nullptr, dk, 1.f / (float)N, D, s);
-  }
-  if (du) {
-    // du~ = IFFT(DY * conj(K')) with the bias tap in K'; du = du~[pb : pb + L]  (zy consumed in place)
-    launch_row<ROW_INV_MULCONJ>(zy, kspec, pr, g, P, s);
-    launch_col_inv<T, OUT_PAIR>(zy, pr, g, pb, du, nullptr, 1.f, P, s);
+  static const bool split = getenv("DNA_FFT_BWD_SPLIT") && atoi(getenv("DNA_FFT_BWD_SPLIT")) == 1;
+  Pairing one{D, 1, 0};  // BP = 0: row index is the channel
+  if (!split) {
+    // one row pass for both gradients (row_bwd_kernel): zy -> du column input in place, pk
+    if (dk && du) launch_row_bwd<true, true>(zy, zuc, kspec, BP, D, g, pk, s);
+    else if (dk) launch_row_bwd<true, false>(zy, zuc, kspec, BP, D, g, pk, s);
+    else if (du) launch_row_bwd<false, true>(zy, zuc, kspec, BP, D, g, pk, s);
+    if (dk) launch_col_inv<float, OUT_REAL>(pk, one, g, 0, nullptr, dk, 1.f / (float)N, D, s);
+    if (du) launch_col_inv<T, OUT_PAIR>(zy, pr, g, pb, du, nullptr, 1.f, P, s);
+  } else {  // DNA_FFT_BWD_SPLIT=1 (A/B): the four-pass form
+    launch_row<ROW_SPEC>(zy, nullptr, pr, g, P, s);
+    if (dk) {
+      const int bx = (int)((N + NTH - 1) / NTH) < 512 ? (int)((N + NTH - 1) / NTH) : 512;
+      hipLaunchKernelGGL(dkspec_kernel, dim3(bx, D), dim3(NTH), 0, s, zuc, (const cf*)zy, BP,
+                         g.logN, pk);
+      launch_row<ROW_INV>(pk, nullptr, one, g, D, s);
+      launch_col_inv<float, OUT_REAL>(pk, one, g, 0, nullptr, dk, 1.f / (float)N, D, s);
+    }
+    if (du) {
+      // du~ = IFFT(DY * conj(K')) with the bias tap in K'; du = du~[pb : pb + L]  (zy consumed in place)
+      launch_row<ROW_INV_MULCONJ>(zy, kspec, pr, g, P, s);
+      launch_col_inv<T, OUT_PAIR>(zy, pr, g, pb, du, nullptr, 1.f, P, s);
+    }
   }
   if (dbias) {
     // partials live after the dk spectra in the workspace

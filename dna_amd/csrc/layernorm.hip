@@ -85,6 +85,7 @@ struct FwdArgs {
   uint64_t seed, off; const float* res; const float* gamma; const float* beta;
   int rows, cols; float eps; float* y; bf16* yb; float* mean; float* rstd;
   int rms;  // RMSNorm: no mean subtraction, no beta, mean[] not written
+  float* sum;  // pre-norm residual stream (x + residual, fp32) of dna_add_ln_fwd, or null
 };
 
 template <typename TX, int NV, bool VEC>
@@ -117,6 +118,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] += r[k];
   }
+  if (a.sum) store_row<float, NV, VEC>(a.sum + ro, lane, v);
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) s += v[k];
@@ -148,6 +150,7 @@ struct BwdArgs {
   const float* mean; const float* rstd; int rows, cols; float* dres; void* dx;
   float* part;  // [gridDim.x][3][cols]: dgamma, dbeta, dbias
   int rms;      // RMSNorm backward: mean taken as 0, no mean-gradient term
+  const float* dsum;  // dna_add_ln_bwd: gradient of the pre-norm sum output, added to the LN's
 };
 
 template <int NV, bool VEC>
@@ -225,6 +228,12 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
     const float c1 = a.rms ? 0.f : wave_sum(s1) * inv_cols, c2 = wave_sum(s2) * inv_cols;
 #pragma unroll
     for (int k = 0; k < NV; ++k) g[k] = rs * (g[k] - c1 - v[k] * c2);  // d(pre-LN sum)
+    if (a.dsum) {  // the sum's other consumers (the residual stream): total gradient of the sum
+      float t[NV];
+      load_row<float, NV, VEC>(a.dsum + ro, lane, t);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) g[k] += t[k];
+    }
     if (a.dres) store_row<float, NV, VEC>(a.dres + ro, lane, g);
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -436,7 +445,7 @@ extern "C" int dna_ln_fwd(const void* x, int x_dtype, const float* bias, int act
   DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_ln_fwd: bad dtype");
   if (rows == 0) return DNA_OK;
   FwdArgs a{x, bias, act, p_drop, dropout_threshold(p_drop), 1.f / (1.f - p_drop), seed, offset,
-            residual, gamma, beta, rows, cols, eps, y, (bf16*)y_bf16, mean, rstd, 0};
+            residual, gamma, beta, rows, cols, eps, y, (bf16*)y_bf16, mean, rstd, 0, nullptr};
   hipStream_t s = as_stream(stream);
   dim3 grid((rows + WAVES - 1) / WAVES);
   int st = dispatch_cols(cols, [&](auto nv, auto vec) {
@@ -467,7 +476,7 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
   const int nb = bwd_blocks(rows);
   BwdArgs a{dy, (const bf16*)dy_bf16, x, bias, act, p_drop, dropout_threshold(p_drop),
             1.f / (1.f - p_drop), seed, offset, residual, gamma, mean, rstd, rows, cols,
-            dresidual, dx, (float*)workspace, 0};
+            dresidual, dx, (float*)workspace, 0, nullptr};
   hipStream_t s = as_stream(stream);
   const size_t lds = (size_t)WAVES * 3 * cols * sizeof(float);
   int st = dispatch_cols(cols, [&](auto nv, auto vec) {
@@ -482,6 +491,69 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
   hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
                      (const float*)workspace, nb, cols, dgamma, dbeta, dbias);
   DNA_LAUNCH_CHECK("dna_ln_bwd");
+  return DNA_OK;
+}
+
+// Pre-norm residual add + LayerNorm (HyenaDNA / flash_attn Block with residual_in_fp32:
+// residual = dropout(x) + residual; y = LN(residual), reference long_conv_lm.py:231-267 through
+// flash_attn.modules.block.Block.forward): sum = x + residual (fp32, written), y = LN(sum) (fp32
+// and / or bf16). The backward takes the gradient of `sum` from its other consumers (dsum: the
+// next Block's residual add) and adds it to the LN's input gradient in the same pass: dres =
+// total (fp32), dx = total in x's dtype -- the add node, its gradient accumulation and the cast
+// of the mixer-output gradient are gone.
+extern "C" int dna_add_ln_fwd(const void* x, int x_dtype, const float* residual, const float* gamma,
+                              const float* beta, int rows, int cols, float eps, float* sum, float* y,
+                              void* y_bf16, float* mean, float* rstd, void* stream) {
+  DNA_CHECK_ARG(x && residual && gamma && beta && sum && mean && rstd, "dna_add_ln_fwd: null pointer");
+  DNA_CHECK_ARG(y || y_bf16, "dna_add_ln_fwd: no output");
+  DNA_CHECK_ARG(rows >= 0, "dna_add_ln_fwd: bad rows");
+  DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_add_ln_fwd: bad dtype");
+  if (rows == 0) return DNA_OK;
+  FwdArgs a{x, nullptr, 0, 0.f, 0u, 1.f, 0, 0, residual, gamma, beta, rows, cols, eps, y,
+            (bf16*)y_bf16, mean, rstd, 0, sum};
+  hipStream_t s = as_stream(stream);
+  dim3 grid((rows + WAVES - 1) / WAVES);
+  int st = dispatch_cols(cols, [&](auto nv, auto vec) {
+    constexpr int NV = decltype(nv)::value;
+    constexpr bool VEC = decltype(vec)::value;
+    if (x_dtype == DNA_BF16)
+      hipLaunchKernelGGL((fwd_kernel<bf16, NV, VEC>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((fwd_kernel<float, NV, VEC>), grid, dim3(256), 0, s, a);
+  });
+  if (st) return st;
+  DNA_LAUNCH_CHECK("dna_add_ln_fwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_add_ln_bwd(const float* dy, const void* dy_bf16, const float* dsum, const void* x,
+                              int x_dtype, const float* residual, const float* gamma,
+                              const float* mean, const float* rstd, int rows, int cols,
+                              float* dresidual, void* dx, float* dgamma, float* dbeta,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  DNA_CHECK_ARG(x && residual && gamma && mean && rstd && dx && dresidual, "dna_add_ln_bwd: null pointer");
+  DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_add_ln_bwd: bad dtype");
+  if (rows == 0) return DNA_OK;
+  DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
+                "dna_add_ln_bwd: workspace too small (%zu < %zu)", workspace_bytes,
+                dna_ln_bwd_workspace(rows, cols));
+  const int nb = bwd_blocks(rows);
+  BwdArgs a{dy, (const bf16*)dy_bf16, x, nullptr, 0, 0.f, 0u, 1.f, 0, 0, residual, gamma, mean,
+            rstd, rows, cols, dresidual, dx, (float*)workspace, 0, dsum};
+  hipStream_t s = as_stream(stream);
+  const size_t lds = (size_t)WAVES * 3 * cols * sizeof(float);
+  int st = dispatch_cols(cols, [&](auto nv, auto vec) {
+    constexpr int NV = decltype(nv)::value;
+    constexpr bool VEC = decltype(vec)::value;
+    if (x_dtype == DNA_BF16)
+      hipLaunchKernelGGL((bwd_kernel<bf16, NV, VEC>), dim3(nb), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((bwd_kernel<float, NV, VEC>), dim3(nb), dim3(256), lds, s, a);
+  });
+  if (st) return st;
+  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
+                     (const float*)workspace, nb, cols, dgamma, dbeta, (float*)nullptr);
+  DNA_LAUNCH_CHECK("dna_add_ln_bwd");
   return DNA_OK;
 }
 

@@ -277,6 +277,57 @@ class FusedLayerNorm(torch.autograd.Function):
         return dx, dbias, dres, dg, db, None, None, None, None, None, None, None
 
 
+class AddLayerNorm(torch.autograd.Function):
+    """Pre-norm residual add + LN: (x, residual fp32) -> (sum = x + residual fp32, LN(sum) fp32
+    or bf16) in one pass (dna_add_ln_fwd). The flash_attn Block's `residual = dropout(x) +
+    residual; norm(residual)` with residual_in_fp32 and dropout p = 0 (HyenaDNA's Blocks,
+    long_conv_lm.py:205-267): same fp32 sum, same LN. The backward adds the gradient of `sum`
+    from the residual stream to the LN's input gradient in the same kernel (dna_add_ln_bwd), so
+    the add node, autograd's gradient accumulation and the cast of x's gradient are gone."""
+
+    @staticmethod
+    def forward(ctx, x, residual, gamma, beta, eps, want_bf16):
+        _gpu(x, residual, gamma, beta)
+        ctx.set_materialize_grads(False)
+        x, residual = x.contiguous(), residual.contiguous()
+        n, d = x.shape
+        s = torch.empty(n, d, device=x.device, dtype=torch.float32)
+        y = torch.empty(n, d, device=x.device, dtype=torch.bfloat16 if want_bf16 else torch.float32)
+        mean = torch.empty(n, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        nbytes = n * (d * (x.element_size() + 8 + y.element_size()) + 8)
+        with _timed("ln_fwd", nbytes, "byte"):
+            N.call("dna_add_ln_fwd", x.data_ptr(), _dt(x), residual.data_ptr(), gamma.data_ptr(),
+                   beta.data_ptr(), n, d, eps, s.data_ptr(), None if want_bf16 else y.data_ptr(),
+                   y.data_ptr() if want_bf16 else None, mean.data_ptr(), rstd.data_ptr(),
+                   N.stream_ptr())
+        ctx.save_for_backward(x, residual, gamma, mean, rstd)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        x, residual, gamma, mean, rstd = ctx.saved_tensors
+        n, d = x.shape
+        dx = torch.empty_like(x)
+        dres = torch.empty(n, d, device=x.device, dtype=torch.float32)
+        dg = torch.empty_like(gamma)
+        db = torch.empty_like(gamma)
+        nws = N.lib().dna_ln_bwd_workspace(n, d)
+        ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
+        dy = None if dy is None else dy.contiguous()
+        ds = None if ds is None else ds.contiguous().float()
+        dyf = dy if (dy is not None and dy.dtype == torch.float32) else None
+        dyb = dy if (dy is not None and dy.dtype == torch.bfloat16) else None
+        nbytes = n * (d * ((4 if dyf is not None else 0) + (2 if dyb is not None else 0)
+                           + (4 if ds is not None else 0) + 2 * x.element_size() + 8) + 8)
+        with _timed("ln_bwd", nbytes, "byte"):
+            N.call("dna_add_ln_bwd", _p(dyf), _p(dyb), _p(ds), x.data_ptr(), _dt(x),
+                   residual.data_ptr(), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, d,
+                   dres.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), ws.data_ptr(),
+                   nws, N.stream_ptr())
+        return dx, dres, dg, db, None, None
+
+
 class RMSNormFn(torch.autograd.Function):
     """x * rsqrt(mean(x^2) + eps) * gamma -> (y fp32|None, y_bf16|None): mamba_ssm's RMSNorm
     as the Caduceus Blocks / norm_f apply it (modeling_caduceus.py:25-65, :214-216)."""

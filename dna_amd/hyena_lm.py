@@ -73,6 +73,26 @@ class LayerNorm(nn.LayerNorm):
         y = yb if bf16_out else y32
         return y.view(*x.shape[:-1], d)
 
+    def add_ok(self, x, residual):
+        """Whether add_norm(x, residual) applies: the fused kernel's widths and dtypes, an fp32
+        residual stream (then `x + residual` is fp32 in torch too)."""
+        return (not _TORCH_LN and x.is_cuda and residual is not None
+                and residual.dtype == torch.float32 and x.dtype in (torch.float32, torch.bfloat16)
+                and self.elementwise_affine and self.bias is not None
+                and x.shape[-1] in _LN_COLS and self.weight.dtype == torch.float32
+                and residual.shape == x.shape)
+
+    def add_norm(self, x, residual):
+        """(residual + x, self(residual + x)) in one pass (functional.AddLayerNorm): the fp32 sum
+        is the new residual stream, the LN output is bf16 under bf16 autocast (as forward)."""
+        from . import functional as DF
+        d = x.shape[-1]
+        bf16_out = (torch.is_autocast_enabled("cuda")
+                    and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        s, y = DF.AddLayerNorm.apply(x.reshape(-1, d), residual.reshape(-1, d), self.weight,
+                                     self.bias, self.eps, bf16_out)
+        return s.view(*x.shape), y.view(*x.shape)
+
 
 class Mlp(nn.Module):
     """flash_attn.modules.mlp.Mlp: fc2(act(fc1(x)))."""
@@ -106,18 +126,30 @@ class Block(nn.Module):
         self.residual_in_fp32 = residual_in_fp32
 
     def forward(self, hidden_states, residual=None):
-        dropped = self.dropout1(hidden_states)
-        residual = dropped + residual if residual is not None else dropped
-        hidden_states = self.norm1(residual.to(dtype=self.norm1.weight.dtype))
-        if self.residual_in_fp32:
-            residual = residual.to(torch.float32)
+        # add + norm in one kernel when the residual stream is fp32 and the dropout is a no-op
+        # (norm1 / norm2 .add_norm: the same fp32 sum and LN, functional.AddLayerNorm)
+        if _no_drop(self.dropout1) and self.norm1.add_ok(hidden_states, residual):
+            residual, hidden_states = self.norm1.add_norm(hidden_states, residual)
+        else:
+            dropped = self.dropout1(hidden_states)
+            residual = dropped + residual if residual is not None else dropped
+            hidden_states = self.norm1(residual.to(dtype=self.norm1.weight.dtype))
+            if self.residual_in_fp32:
+                residual = residual.to(torch.float32)
         hidden_states = self.mixer(hidden_states)
-        dropped = self.dropout2(hidden_states)
-        residual = dropped + residual
-        hidden_states = self.norm2(residual.to(dtype=self.norm2.weight.dtype))
-        if self.residual_in_fp32:
-            residual = residual.to(torch.float32)
+        if _no_drop(self.dropout2) and self.norm2.add_ok(hidden_states, residual):
+            residual, hidden_states = self.norm2.add_norm(hidden_states, residual)
+        else:
+            dropped = self.dropout2(hidden_states)
+            residual = dropped + residual
+            hidden_states = self.norm2(residual.to(dtype=self.norm2.weight.dtype))
+            if self.residual_in_fp32:
+                residual = residual.to(torch.float32)
         return self.mlp(hidden_states), residual
+
+
+def _no_drop(m):
+    return m.p == 0.0 or not m.training
 
 
 def _init_weights(module, n_layer, initializer_range=0.02, rescale_prenorm_residual=True):
@@ -169,6 +201,8 @@ class LMBackbone(nn.Module):
         residual = None
         for layer in self.layers:
             hidden_states, residual = layer(hidden_states, residual)
+        if _no_drop(self.drop_f) and self.ln_f.add_ok(hidden_states, residual):
+            return self.ln_f.add_norm(hidden_states, residual)[1]
         dropped = self.drop_f(hidden_states)
         residual = dropped + residual if residual is not None else dropped
         return self.ln_f(residual.to(dtype=self.ln_f.weight.dtype))

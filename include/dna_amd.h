@@ -122,6 +122,22 @@ int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, int x_dtype,
                int rows, int cols, float* dresidual, void* dx, float* dgamma, float* dbeta,
                float* dbias, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Pre-norm residual add + LayerNorm: sum = x + residual (fp32, written), y = LN(sum).
+ * Replaces the flash_attn Block's `residual = dropout(x) + residual; norm(residual)` with
+ * residual_in_fp32 (HyenaDNA's create_block, src/models/sequence/long_conv_lm.py:205-267; dropout
+ * p = 0). x [rows, cols] x_dtype; residual, sum [rows, cols] fp32; y fp32 and / or y_bf16.
+ * Backward: dsum = gradient of `sum` from its other consumers (NULL: none), added to the LN's
+ * input gradient; writes dresidual (fp32) = dx (x_dtype) = that total, dgamma / dbeta (written).
+ * workspace >= dna_ln_bwd_workspace(rows, cols). */
+int dna_add_ln_fwd(const void* x, int x_dtype, const float* residual, const float* gamma,
+                   const float* beta, int rows, int cols, float eps, float* sum, float* y,
+                   void* y_bf16, float* mean, float* rstd, void* stream);
+int dna_add_ln_bwd(const float* dy, const void* dy_bf16, const float* dsum, const void* x,
+                   int x_dtype, const float* residual, const float* gamma, const float* mean,
+                   const float* rstd, int rows, int cols, float* dresidual, void* dx,
+                   float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
 /* RMSNorm y = x * rsqrt(mean(x^2) + eps) * gamma with fp32 statistics -- replaces mamba_ssm's
  * RMSNorm as the Caduceus Blocks and norm_f apply it (src/models/caduceus/modeling_caduceus.py
  * :25-65 and :214-216 build them with rms_norm=True; the fused add is left to the caller).
