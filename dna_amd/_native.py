@@ -33,6 +33,8 @@ _SIGS = {
     "dna_flash_bwd": (_i, [_vp, _i, _vp, _i, _i, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i,
                            _f, _vp, _vp, _vp]),
     "dna_colsum_f32": (_i, [_vp, _i, _i, _vp, _i, _vp]),
+    "dna_colsum_bf16_workspace": (_sz, [_i, _i]),
+    "dna_colsum_bf16": (_i, [_vp, _i, _i, _vp, _i, _vp, _sz, _vp]),
     "dna_causal_conv1d_fwd": (_i, [_vp, _sz, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "dna_causal_conv1d_part_rows": (_sz, [_i, _i]),
     "dna_causal_conv1d_bwd": (_i, [_vp, _sz, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _sz, _vp, _vp]),
@@ -41,6 +43,8 @@ _SIGS = {
     "dna_hyena_shortconv_bwd": (_i, [_vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "dna_hyena_gate_out_fwd": (_i, [_vp, _vp, _i, _i, _i, _i, _sz, _vp, _vp]),
     "dna_hyena_gate_out_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _sz, _vp, _vp, _vp]),
+    "dna_hyena_modulate_t_fwd": (_i, [_vp, _i, _vp, _vp, _f, _i, _i, _i, _vp, _vp]),
+    "dna_hyena_modulate_t_bwd": (_i, [_vp, _vp, _vp, _f, _i, _i, _i, _vp, _i, _vp]),
     "dna_ln_fwd": (_i, [_vp, _i, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _i, _i, _f, _vp, _vp,
                         _vp, _vp, _vp]),
     "dna_ln_bwd_workspace": (_sz, [_i, _i]),

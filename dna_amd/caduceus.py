@@ -96,7 +96,7 @@ class RCPSEmbedding(nn.Module):
         if cm.numel() != vocab_size:
             raise ValueError(f"complement_map has {cm.numel()} entries for a vocabulary of {vocab_size}")
         self.register_buffer("complement_map", cm)
-        self.embedding = nn.Embedding(vocab_size, d_model)
+        self.embedding = DF.HipEmbedding(vocab_size, d_model)
 
     @property
     def weight(self):
@@ -213,7 +213,7 @@ class CaduceusEmbeddings(nn.Module):
     def __init__(self, vocab_size, d_model, rcps=False, complement_map=None):
         super().__init__()
         self.word_embeddings = (RCPSEmbedding(vocab_size, d_model, complement_map) if rcps
-                                else nn.Embedding(vocab_size, d_model))
+                                else DF.HipEmbedding(vocab_size, d_model))
 
     def forward(self, input_ids):
         return self.word_embeddings(input_ids)

@@ -62,6 +62,49 @@ __global__ __launch_bounds__(64 * CS_GROUPS) void colsum_kernel(const float* __r
   }
 }
 
+// Column sums of a bf16 matrix (a Linear's bias gradient sum_r dy[r][c]), stage 1: partial
+// sums per chunk of CS_CHUNK rows. A block = W column groups of 8 (one 16-B load each) x 256/W
+// row groups; a thread sums its rows of the chunk in row order (4 loads in flight), the row
+// groups are combined through LDS in fixed order -> part[chunk][c]. Stage 2 is colsum_kernel
+// over the chunks (deterministic end to end).
+constexpr int CS_CHUNK = 256;
+template <int W>
+__global__ __launch_bounds__(256) void colsum_bf16_part_kernel(const bf16* __restrict__ x, int rows,
+                                                               int cols, float* __restrict__ part) {
+  constexpr int RG = 256 / W;
+  __shared__ f32x4 red[RG][W][2];
+  const int cg = threadIdx.x % W, rg = threadIdx.x / W;
+  const int c0 = (blockIdx.x * W + cg) * 8;
+  const int r0 = blockIdx.y * CS_CHUNK, r1 = min(rows, r0 + CS_CHUNK);
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+  int r = r0 + rg;
+  for (; r + 3 * RG < r1; r += 4 * RG) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const bf16x8*>(x + (size_t)(r + u * RG) * cols + c0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { a0[e] += (float)v[u][e]; a1[e] += (float)v[u][4 + e]; }
+    }
+  }
+  for (; r < r1; r += RG) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (size_t)r * cols + c0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { a0[e] += (float)v[e]; a1[e] += (float)v[4 + e]; }
+  }
+  red[rg][cg][0] = a0;
+  red[rg][cg][1] = a1;
+  __syncthreads();
+  if (rg == 0) {
+#pragma unroll
+    for (int g = 1; g < RG; ++g) { a0 += red[g][cg][0]; a1 += red[g][cg][1]; }
+    float* o = part + (size_t)blockIdx.y * cols + c0;
+    *reinterpret_cast<f32x4*>(o) = a0;
+    *reinterpret_cast<f32x4*>(o + 4) = a1;
+  }
+}
+
 constexpr int SEG_CHUNK = 32;
 
 // Deterministic: a run of equal ids lying inside one chunk belongs to that chunk's wave (plain
@@ -211,6 +254,36 @@ extern "C" int dna_colsum_f32(const float* part, int rows, int cols, float* out,
   hipLaunchKernelGGL(gacc::colsum_kernel, dim3(cols / 64), dim3(64 * gacc::CS_GROUPS), 0,
                      as_stream(stream), part, rows, cols, accumulate, out);
   DNA_LAUNCH_CHECK("dna_colsum_f32");
+  return DNA_OK;
+}
+
+extern "C" size_t dna_colsum_bf16_workspace(int rows, int cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return (size_t)((rows + gacc::CS_CHUNK - 1) / gacc::CS_CHUNK) * cols * sizeof(float);
+}
+
+extern "C" int dna_colsum_bf16(const void* x, int rows, int cols, float* out, int accumulate,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  DNA_CHECK_ARG(x && out && rows >= 1 && cols >= 64 && cols % 64 == 0,
+                "dna_colsum_bf16: bad args (rows %d, cols %d; cols %% 64 == 0 required)", rows, cols);
+  DNA_CHECK_ARG(((uintptr_t)x & 15) == 0, "dna_colsum_bf16: x must be 16-B aligned");
+  DNA_CHECK_ARG(workspace && workspace_bytes >= dna_colsum_bf16_workspace(rows, cols),
+                "dna_colsum_bf16: workspace too small");
+  hipStream_t s = as_stream(stream);
+  const int ng = cols / 8, chunks = (rows + gacc::CS_CHUNK - 1) / gacc::CS_CHUNK;
+  float* part = (float*)workspace;
+  if (ng % 64 == 0)
+    hipLaunchKernelGGL(gacc::colsum_bf16_part_kernel<64>, dim3(ng / 64, chunks), dim3(256), 0, s,
+                       (const bf16*)x, rows, cols, part);
+  else if (ng % 32 == 0)
+    hipLaunchKernelGGL(gacc::colsum_bf16_part_kernel<32>, dim3(ng / 32, chunks), dim3(256), 0, s,
+                       (const bf16*)x, rows, cols, part);
+  else
+    hipLaunchKernelGGL(gacc::colsum_bf16_part_kernel<8>, dim3(ng / 8, chunks), dim3(256), 0, s,
+                       (const bf16*)x, rows, cols, part);
+  hipLaunchKernelGGL(gacc::colsum_kernel, dim3(cols / 64), dim3(64 * gacc::CS_GROUPS), 0, s,
+                     (const float*)part, chunks, cols, accumulate, out);
+  DNA_LAUNCH_CHECK("dna_colsum_bf16");
   return DNA_OK;
 }
 

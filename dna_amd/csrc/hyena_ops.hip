@@ -176,6 +176,51 @@ __global__ __launch_bounds__(256) void gate_out_bwd_kernel(const T* dy, const T*
   }
 }
 
+// The implicit filter's ExponentialModulation fused with the [L, C] -> [O][C/O][L] transpose the
+// long convolution reads (reference hyena.py:140-163 and :438-441): k[o][v][t] = h[t][c] *
+// (exp(-tpos[t] * |delta[c]|) + shift), c = v * O + o. One 64 x 64 LDS tile per block; the
+// backward runs the same transpose the other way, dh[t][c] = dk[o][v][t] * (same factor).
+constexpr int MT = 64;
+__device__ __forceinline__ float modf_(const float* tpos, const float* delta, float shift, int t, int c) {
+  return expf(-tpos[t] * fabsf(delta[c])) + shift;
+}
+template <typename TH>
+__global__ __launch_bounds__(256) void modulate_t_fwd_kernel(const TH* __restrict__ h, const float* __restrict__ tpos,
+                                                             const float* __restrict__ delta, float shift,
+                                                             int L, int C, int O, float* __restrict__ k) {
+  __shared__ float tile[MT][MT + 1];
+  const int t0 = blockIdx.x * MT, c0 = blockIdx.y * MT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int r = wv; r < MT; r += 4) {
+    const int t = t0 + r, c = c0 + lane;
+    tile[r][lane] = (t < L && c < C) ? to_f32(h[(size_t)t * C + c]) * modf_(tpos, delta, shift, t, c) : 0.f;
+  }
+  __syncthreads();
+  const int V = C / O;
+  for (int r = wv; r < MT; r += 4) {
+    const int c = c0 + r, t = t0 + lane;
+    if (c < C && t < L) k[((size_t)(c % O) * V + c / O) * L + t] = tile[lane][r];
+  }
+}
+template <typename TH>
+__global__ __launch_bounds__(256) void modulate_t_bwd_kernel(const float* __restrict__ dk, const float* __restrict__ tpos,
+                                                             const float* __restrict__ delta, float shift,
+                                                             int L, int C, int O, TH* __restrict__ dh) {
+  __shared__ float tile[MT][MT + 1];
+  const int t0 = blockIdx.x * MT, c0 = blockIdx.y * MT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int V = C / O;
+  for (int r = wv; r < MT; r += 4) {
+    const int c = c0 + r, t = t0 + lane;
+    tile[r][lane] = (c < C && t < L) ? dk[((size_t)(c % O) * V + c / O) * L + t] : 0.f;
+  }
+  __syncthreads();
+  for (int r = wv; r < MT; r += 4) {
+    const int t = t0 + r, c = c0 + lane;
+    if (t < L && c < C) dh[(size_t)t * C + c] = cvt<TH>(tile[lane][r] * modf_(tpos, delta, shift, t, c));
+  }
+}
+
 struct Bwd {
   const void* u; const float* w; const float* bias; int B, L, d, order, K;
   const void* dxs; const void* dvx; void* du; float* part;  // part [B * nL][C][K + 1]
@@ -512,5 +557,41 @@ extern "C" int dna_hyena_gate_out_bwd(const void* dy, const void* yc, const void
   else
     DNA_CHECK_ARG(false, "dna_hyena_gate_out_bwd: bad dtype");
   DNA_LAUNCH_CHECK("dna_hyena_gate_out_bwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_hyena_modulate_t_fwd(const void* h, int dtype, const float* tpos, const float* delta,
+                                        float shift, int L, int C, int O, float* k, void* stream) {
+  DNA_CHECK_ARG(h && tpos && delta && k && L > 0 && C > 0 && O > 0 && C % O == 0,
+                "dna_hyena_modulate_t_fwd: bad args");
+  const dim3 grid((L + MT - 1) / MT, (C + MT - 1) / MT);
+  hipStream_t s = as_stream(stream);
+  if (dtype == DNA_F32)
+    hipLaunchKernelGGL(modulate_t_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)h, tpos, delta,
+                       shift, L, C, O, k);
+  else if (dtype == DNA_BF16)
+    hipLaunchKernelGGL(modulate_t_fwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)h, tpos, delta,
+                       shift, L, C, O, k);
+  else
+    DNA_CHECK_ARG(false, "dna_hyena_modulate_t_fwd: bad dtype");
+  DNA_LAUNCH_CHECK("dna_hyena_modulate_t_fwd");
+  return DNA_OK;
+}
+
+extern "C" int dna_hyena_modulate_t_bwd(const float* dk, const float* tpos, const float* delta, float shift,
+                                        int L, int C, int O, void* dh, int dtype, void* stream) {
+  DNA_CHECK_ARG(dk && tpos && delta && dh && L > 0 && C > 0 && O > 0 && C % O == 0,
+                "dna_hyena_modulate_t_bwd: bad args");
+  const dim3 grid((L + MT - 1) / MT, (C + MT - 1) / MT);
+  hipStream_t s = as_stream(stream);
+  if (dtype == DNA_F32)
+    hipLaunchKernelGGL(modulate_t_bwd_kernel<float>, grid, dim3(256), 0, s, dk, tpos, delta, shift, L, C,
+                       O, (float*)dh);
+  else if (dtype == DNA_BF16)
+    hipLaunchKernelGGL(modulate_t_bwd_kernel<bf16>, grid, dim3(256), 0, s, dk, tpos, delta, shift, L, C,
+                       O, (bf16*)dh);
+  else
+    DNA_CHECK_ARG(false, "dna_hyena_modulate_t_bwd: bad dtype");
+  DNA_LAUNCH_CHECK("dna_hyena_modulate_t_bwd");
   return DNA_OK;
 }

@@ -317,6 +317,35 @@ class ExponentialModulation(_OptimModule):
         return x * (torch.exp(-t * self.deltas.abs()) + self.shift)
 
 
+class ModulateT(torch.autograd.Function):
+    """k [O, C/O, L] fp32 = transpose(h [L, C] * (exp(-t |deltas|) + shift)), the
+    ExponentialModulation of the implicit filter fused with the filter layout the long
+    convolution reads (dna_hyena_modulate_t_fwd / _bwd; reference hyena.py:140-163, :438-441).
+    deltas is a constant here (registered with lr 0 in every reference config)."""
+
+    @staticmethod
+    def forward(ctx, h, tpos, deltas, shift, O):
+        _gpu(h, tpos, deltas)
+        L, C = h.shape
+        h = h.contiguous()
+        k = torch.empty(O, C // O, L, device=h.device, dtype=torch.float32)
+        N.call("dna_hyena_modulate_t_fwd", h.data_ptr(), _dt(h), tpos.data_ptr(), deltas.data_ptr(),
+               float(shift), L, C, O, k.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(tpos, deltas)
+        ctx.cfg = (L, C, O, float(shift), h.dtype)
+        return k
+
+    @staticmethod
+    def backward(ctx, dk):
+        tpos, deltas = ctx.saved_tensors
+        L, C, O, shift, hdt = ctx.cfg
+        dk = dk.contiguous().float()
+        dh = torch.empty(L, C, device=dk.device, dtype=hdt)
+        N.call("dna_hyena_modulate_t_bwd", dk.data_ptr(), tpos.data_ptr(), deltas.data_ptr(), shift,
+               L, C, O, dh.data_ptr(), _dt(dh), N.stream_ptr())
+        return dh, None, None, None, None
+
+
 def _split_k_linear(x, lin):
     """nn.Linear over the L positions of the implicit filter MLP ([1, L, K] -> [1, L, N], K 3-5
     and N 64-256) on the strided MFMA GEMM (`functional.strided_linear`). As one library GEMM
@@ -372,6 +401,26 @@ class HyenaFilter(_OptimModule):
         if self.normalized:
             h = h / torch.norm(h, dim=-1, p=1, keepdim=True)
         return h
+
+    def filter_t(self, L, O):
+        """filter(L)[0] as the long convolution reads it: k [O, d_model / O, L] with
+        k[o][v][l] = filter(L)[0][l][v * O + o]. On the GPU the modulation and the transpose are
+        one kernel (ModulateT); otherwise the reshape / permute of the reference."""
+        z, t = self.pos_emb(L)
+        h = z
+        for layer in self.implicit_filter:
+            h = _split_k_linear(h, layer) if isinstance(layer, nn.Linear) else layer(h)
+        deltas = self.modulation.deltas
+        if (self.modulate and not self.normalized and h.is_cuda and h.dim() == 3 and h.shape[0] == 1
+                and not deltas.requires_grad and h.dtype in (torch.float32, torch.bfloat16)):
+            tpos = t.reshape(-1).float().contiguous()
+            return ModulateT.apply(h[0], tpos, deltas.reshape(-1).float().contiguous(),
+                                   self.modulation.shift, O)
+        if self.modulate:
+            h = self.modulation(t, h)
+        if self.normalized:
+            h = h / torch.norm(h, dim=-1, p=1, keepdim=True)
+        return h[0].reshape(L, h.shape[-1] // O, O).permute(2, 1, 0)
 
     def forward(self, x, L, k=None, bias=None, *args, **kwargs):
         if k is None:
@@ -453,14 +502,15 @@ class HyenaOperator(nn.Module):
         d, order = self.d_model, self.order
         u = self.in_proj(x)                                                   # [B, L, C] token-major
         xs, v = ShortConvSplit.apply(u, self.short_filter.weight, self.short_filter.bias, order, d)
-        k = self.filter_fn.filter(L)
-        k = k[0].reshape(L, self.head_dim, order - 1).permute(2, 1, 0)        # o v l
+        k = self.filter_fn.filter_t(L, order - 1)                              # o v l
+        # order 2: the one filter as a view (no select node, whose backward is a zero fill + copy)
+        ks = [k.view(k.shape[1], L)] if order == 2 else [k[o] for o in range(order - 1)]
         bias = self.filter_fn.bias.reshape(self.head_dim, order - 1).t()       # o v
         for o in range(order - 1):
             if o > 0:  # reversed(x[1:]): x_{order-1} was gated in the fused kernel
                 v = v * xs[:, order - 1 - o]
             v = self.dropout(v)
-            v = self.filter_fn(v, L, k=k[o], bias=bias[o])
+            v = self.filter_fn(v, L, k=ks[o], bias=bias[o])
         y = self.activation(GateOut.apply(v, xs))
         y = self.out_proj(y)
         if self.return_state:

@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .functional import HipEmbedding
 from .hyena import HipLinear, HyenaOperator
 
 
@@ -33,7 +34,7 @@ class GPT2Embeddings(nn.Module):
                  device=None, dtype=None):
         super().__init__()
         fk = {"device": device, "dtype": dtype}
-        self.word_embeddings = nn.Embedding(vocab_size, embed_dim, padding_idx=padding_idx, **fk)
+        self.word_embeddings = HipEmbedding(vocab_size, embed_dim, padding_idx=padding_idx, **fk)
         self.max_position_embeddings = max_position_embeddings
         if max_position_embeddings > 0:
             self.position_embeddings = nn.Embedding(max_position_embeddings, embed_dim, **fk)

@@ -193,6 +193,13 @@ int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_ids, const i
  * cols % 64 == 0. Finishes the fused bias-gradient partials (Linear bias grads, autograd's
  * dy.sum(0)). */
 int dna_colsum_f32(const float* part, int rows, int cols, float* out, int accumulate, void* stream);
+/* out[c] (+)= sum_r x[r][c] for a bf16 matrix x [rows, cols] (16-B aligned, cols % 64 == 0): a
+ * Linear's bias gradient from the bf16 output gradient (replaces autograd's dy.sum(0) for
+ * nn.Linear under bf16 autocast). fp32 partials per 256-row chunk in workspace (>=
+ * dna_colsum_bf16_workspace(rows, cols) bytes), summed in chunk order (deterministic). */
+size_t dna_colsum_bf16_workspace(int rows, int cols);
+int dna_colsum_bf16(const void* x, int rows, int cols, float* out, int accumulate, void* workspace,
+                    size_t workspace_bytes, void* stream);
 /* out[i] += sum_{k<s} parts[k*n + i]: split-K partials of a weight gradient folded straight
  * into the flat fp32 gradient buffer (16-byte loads when the buffers are 16-byte aligned and
  * n % 4 == 0, element-wise otherwise). */
@@ -336,6 +343,15 @@ int dna_hyena_gate_out_fwd(const void* yc, const void* x0, int dtype, int B, int
 /* dyc = dy * x_0, dx0 = dy * yc (channel-major; dx0 with the same batch stride as x_0). */
 int dna_hyena_gate_out_bwd(const void* dy, const void* yc, const void* x0, int dtype, int B, int L,
                            int d, size_t x_bstride, void* dyc, void* dx0, void* stream);
+
+/* HyenaFilter's ExponentialModulation fused with the filter transpose (reference hyena.py:140-163,
+ * :438-441): k[o][v][t] = h[t][c] * (exp(-tpos[t] * |delta[c]|) + shift), c = v * O + o, for
+ * h [L, C] (dtype fp32 / bf16), k [O][C / O][L] fp32. Backward: dh[t][c] = dk[o][v][t] * (same
+ * factor) in h's dtype (delta taken as a constant: the reference registers it with lr 0). */
+int dna_hyena_modulate_t_fwd(const void* h, int dtype, const float* tpos, const float* delta,
+                             float shift, int L, int C, int O, float* k, void* stream);
+int dna_hyena_modulate_t_bwd(const float* dk, const float* tpos, const float* delta, float shift,
+                             int L, int C, int O, void* dh, int dtype, void* stream);
 
 /* ------------------------------------------------------------------ causal depthwise conv1d (+ SiLU)
  * Mamba.forward's x = silu(conv1d(x)[..., :L]) (depthwise, kernel K = d_conv, padding K-1;

@@ -102,6 +102,36 @@ def _op_state(d_model, l_max, order, seed, **kw):
     return op, {k: v.detach().double().clone() for k, v in op.state_dict().items()}
 
 
+@pytest.mark.parametrize("order,autocast", [(2, True), (3, False), (2, False)])
+def test_filter_t_equals_filter_permuted(order, autocast):
+    """HyenaFilter.filter_t (ModulateT: modulation + transpose in one kernel) against the
+    reference layout filter(L)[0].reshape(L, v, o).permute(2, 1, 0): forward and the gradients of
+    the implicit-filter MLP parameters."""
+    op, _ = _op_state(64, 2048, order, 5, emb_dim=5)
+    f = op.filter_fn.to(DEV)
+    L, O = 2048, order - 1
+    g = torch.Generator(device="cpu").manual_seed(9)
+    dk = torch.randn(O, 64, L, generator=g).to(DEV)
+    outs = []
+    for fused in (True, False):
+        f.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            if fused:
+                k = f.filter_t(L, O)
+            else:
+                k = f.filter(L)[0].reshape(L, 64, O).permute(2, 1, 0)
+        (k.float() * dk).sum().backward()
+        outs.append((k.detach().float().clone(),
+                     {n: p.grad.detach().clone() for n, p in f.named_parameters() if p.grad is not None}))
+    (k1, g1), (k2, g2) = outs
+    assert k1.shape == k2.shape == (O, 64, L)
+    assert (k1 - k2).abs().max().item() <= 1e-6 * k2.abs().max().item() + 1e-7
+    assert g1.keys() == g2.keys() and len(g1) > 0
+    for n in g1:
+        sc = g2[n].abs().max().item()
+        assert (g1[n] - g2[n]).abs().max().item() <= 2e-5 * max(sc, 1e-3), n
+
+
 def test_hyena_operator_matches_reference_fixture():
     """dna_amd.hyena.HyenaOperator (HIP long conv) on the reference operator's state_dict and
     input (hyena_op_golden.npz, produced by running the reference): fp32 output vs the fp64 y."""

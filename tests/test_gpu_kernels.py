@@ -232,6 +232,54 @@ def test_add_layernorm_vs_torch(dtype, cols):
         assert (a.grad.float() - r.grad).abs().max().item() < tol * sc
 
 
+@pytest.mark.parametrize("rows,cols", [(1, 64), (300, 192), (131072, 256), (5001, 768), (70000, 1024)])
+def test_colsum_bf16_bias_grad(rows, cols):
+    """dna_colsum_bf16 (functional.bias_grad): fp32 column sums of a bf16 gradient vs a float64
+    sum, deterministic (two calls bit-equal), accumulate mode adds onto the output."""
+    from dna_amd import _native as N
+    from dna_amd import functional as DF
+    g = torch.Generator(device="cpu").manual_seed(rows + cols)
+    dy = torch.randn(rows, cols, generator=g).to(torch.bfloat16).to(DEV)
+    ref = dy.double().sum(0)
+    a = DF.bias_grad(dy)
+    b = DF.bias_grad(dy)
+    assert a.dtype == torch.float32 and torch.equal(a, b)
+    assert (a.double() - ref).abs().max().item() < 1e-5 * max(rows, 1) ** 0.5 + 1e-5
+    out = torch.full((cols,), 2.0, device=DEV)
+    nws = N.lib().dna_colsum_bf16_workspace(rows, cols)
+    ws = torch.empty(nws, device=DEV, dtype=torch.uint8)
+    N.call("dna_colsum_bf16", dy.data_ptr(), rows, cols, out.data_ptr(), 1, ws.data_ptr(), nws,
+           N.stream_ptr())
+    assert torch.allclose(out, a + 2.0, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("V,d,shape,pad", [(16, 256, (2, 65536), None), (12, 128, (3, 777), 4),
+                                           (4096, 64, (5000,), 0)])
+def test_embedding_fn_grad_vs_torch(V, d, shape, pad):
+    """functional.embedding (HipEmbedding): forward = F.embedding; the table gradient of the
+    sorted segmented sum matches torch's embedding backward (fp32 sums in another order) and is
+    bit-identical run to run; the padding row gets no gradient."""
+    from dna_amd import functional as DF
+    g = torch.Generator(device="cpu").manual_seed(V + d)
+    ids = torch.randint(0, V, shape, generator=g).to(DEV)
+    E = torch.randn(V, d, generator=g).to(DEV)
+    dy = torch.randn(*shape, d, generator=g).to(DEV)
+    grads = []
+    for _ in range(2):
+        w = E.clone().requires_grad_(True)
+        y = DF.embedding(ids, w, pad)
+        assert torch.equal(y, torch.nn.functional.embedding(ids, E, pad))
+        y.backward(dy)
+        grads.append(w.grad)
+    assert torch.equal(grads[0], grads[1])
+    wr = E.clone().requires_grad_(True)
+    torch.nn.functional.embedding(ids, wr, pad).backward(dy)
+    sc = wr.grad.abs().max().item()
+    assert (grads[0] - wr.grad).abs().max().item() < 1e-5 * max(sc, 1.0)
+    if pad is not None:
+        assert grads[0][pad].abs().max().item() == 0.0
+
+
 def test_dropout_mask_consistent_fwd_bwd():
     """GeGLU dropout: backward regenerates the forward mask (Philox), keep rate ~0.9."""
     from dna_amd import functional as DF
