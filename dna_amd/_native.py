@@ -50,9 +50,9 @@ _SIGS = {
     "dna_ln_bwd_workspace": (_sz, [_i, _i]),
     "dna_ln_bwd": (_i, [_vp, _vp, _vp, _i, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _vp, _i, _i,
                         _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
-    "dna_add_ln_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "dna_add_ln_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp,
-                            _vp, _sz, _vp]),
+    "dna_add_ln_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "dna_add_ln_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp,
+                            _vp, _vp, _sz, _vp]),
     "dna_rms_fwd": (_i, [_vp, _i, _vp, _i, _i, _f, _vp, _vp, _vp, _vp]),
     "dna_rms_bwd": (_i, [_vp, _vp, _vp, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "dna_embed_ln_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _f, _f, _u64, _u64, _vp, _vp,

@@ -57,6 +57,23 @@ class RMSNorm(nn.Module):
         y = yb if bf16_out else y32.to(x.dtype)
         return y.view(*x.shape[:-1], d)
 
+    def add_ok(self, x, residual):
+        """add_norm applies: kernel widths / dtypes and an fp32 residual stream (torch's
+        x + residual is then fp32 too)."""
+        return (not _TORCH_NORM and x.is_cuda and residual is not None
+                and residual.dtype == torch.float32 and x.dtype in (torch.float32, torch.bfloat16)
+                and x.shape[-1] in _LN_COLS and self.weight.dtype == torch.float32
+                and residual.shape == x.shape)
+
+    def add_norm(self, x, residual):
+        """(x + residual, self(x + residual)) in one kernel (functional.AddLayerNorm, RMS mode)."""
+        d = x.shape[-1]
+        bf16_out = (torch.is_autocast_enabled("cuda")
+                    and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        s, y = DF.AddLayerNorm.apply(x.reshape(-1, d), residual.reshape(-1, d), self.weight, None,
+                                     self.eps, bf16_out)
+        return s.view(*x.shape), y.view(*x.shape)
+
 
 class MambaBlock(nn.Module):
     """mamba_ssm.modules.mamba_simple.Block: (hidden, residual) -> (mixer(norm(add)), add)."""
@@ -68,6 +85,10 @@ class MambaBlock(nn.Module):
         self.residual_in_fp32 = residual_in_fp32
 
     def forward(self, hidden_states, residual=None):
+        if hasattr(self.norm, "add_ok") and self.norm.add_ok(hidden_states, residual):
+            # add + norm in one kernel (fp32 residual stream: the same sum and norm)
+            residual, hidden_states = self.norm.add_norm(hidden_states, residual)
+            return self.mixer(hidden_states), residual
         residual = hidden_states + residual if residual is not None else hidden_states
         hidden_states = self.norm(residual.to(dtype=self.norm.weight.dtype))
         if self.residual_in_fp32:
@@ -131,6 +152,9 @@ class RCPSWrapper(nn.Module):
 def _add_norm(norm, x, residual, residual_in_fp32):
     """mamba_ssm's fused add + norm (prenorm=True): (norm(x + residual), x + residual), the
     residual kept in fp32 when residual_in_fp32 -- the same arithmetic MambaBlock.forward uses."""
+    if hasattr(norm, "add_ok") and norm.add_ok(x, residual):
+        residual, y = norm.add_norm(x, residual)  # one kernel, fp32 residual stream
+        return y, residual
     residual = x if residual is None else x + residual
     y = norm(residual.to(dtype=norm.weight.dtype))
     return y, (residual.to(torch.float32) if residual_in_fp32 else residual)
@@ -261,6 +285,8 @@ class CaduceusMixerModel(nn.Module):
                               None if residual is None else _rc(residual[..., c:]),
                               self.residual_in_fp32)
             return torch.cat([fwd, _rc(rc)], dim=-1)
+        if hasattr(self.norm_f, "add_ok") and self.norm_f.add_ok(hidden_states, residual):
+            return self.norm_f.add_norm(hidden_states, residual)[1]
         residual = hidden_states + residual if residual is not None else hidden_states
         return self.norm_f(residual.to(dtype=self.norm_f.weight.dtype))
 

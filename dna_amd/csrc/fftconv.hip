@@ -28,6 +28,7 @@
 #include <math.h>
 
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -263,7 +264,36 @@ __global__ FFT_BOUNDS void col_fwd_kernel(const T* __restrict__ x, Pairing pr, G
   bt.init(g.logN);
   const T* xa = x + (size_t)ra * g.L;
   const T* xb = rb >= 0 ? x + (size_t)rb * g.L : nullptr;
-  {
+  // 16-B loads: VE consecutive columns of one n1 row of both rows of the pair per load (a chunk
+  // never straddles the [0, L) edge when cw, off and L are multiples of VE)
+  constexpr int VE = 16 / sizeof(T);
+  typedef typename std::conditional<sizeof(T) == 2, bf16x8, f32x4>::type V16;
+  if (LN > 0 && cw % VE == 0 && off % VE == 0 && g.L % VE == 0 && cw * M1 == PTS &&
+      ((uintptr_t)x & 15) == 0) {
+    constexpr int NP = PPT / VE;  // (n1, chunk) pairs per thread
+    const int cpr = cw / VE;
+    V16 va[NP], vb[NP];
+#pragma unroll
+    for (int it = 0; it < NP; ++it) {
+      const int q = threadIdx.x + it * NTH;
+      const int cc = q % cpr, n1 = q / cpr;
+      const int i = n1 * M2 + n20 + cc * VE - off;
+#pragma unroll
+      for (int j = 0; j < VE; ++j) { va[it][j] = T(0.f); vb[it][j] = T(0.f); }
+      if (i >= 0 && i < g.L) {
+        va[it] = *reinterpret_cast<const V16*>(xa + i);
+        if (xb) vb[it] = *reinterpret_cast<const V16*>(xb + i);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NP; ++it) {
+      const int q = threadIdx.x + it * NTH;
+      const int cc = q % cpr, n1 = q / cpr;
+#pragma unroll
+      for (int j = 0; j < VE; ++j)
+        buf[lds_at(cc * VE + j, n1, S)] = make_float2(to_f32((T)va[it][j]), to_f32((T)vb[it][j]));
+    }
+  } else {
     // all PPT loads in flight before the LDS stores (a plain strided loop serialises them)
     cf v[PPT];
 #pragma unroll

@@ -494,7 +494,8 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
   return DNA_OK;
 }
 
-// Pre-norm residual add + LayerNorm (HyenaDNA / flash_attn Block with residual_in_fp32:
+// Pre-norm residual add + LayerNorm / RMSNorm (rms = 1: mamba_ssm's Block with fused_add_norm,
+// modeling_caduceus.py; HyenaDNA / flash_attn Block with residual_in_fp32:
 // residual = dropout(x) + residual; y = LN(residual), reference long_conv_lm.py:231-267 through
 // flash_attn.modules.block.Block.forward): sum = x + residual (fp32, written), y = LN(sum) (fp32
 // and / or bf16). The backward takes the gradient of `sum` from its other consumers (dsum: the
@@ -502,15 +503,16 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
 // total (fp32), dx = total in x's dtype -- the add node, its gradient accumulation and the cast
 // of the mixer-output gradient are gone.
 extern "C" int dna_add_ln_fwd(const void* x, int x_dtype, const float* residual, const float* gamma,
-                              const float* beta, int rows, int cols, float eps, float* sum, float* y,
-                              void* y_bf16, float* mean, float* rstd, void* stream) {
-  DNA_CHECK_ARG(x && residual && gamma && beta && sum && mean && rstd, "dna_add_ln_fwd: null pointer");
+                              const float* beta, int rows, int cols, float eps, int rms, float* sum,
+                              float* y, void* y_bf16, float* mean, float* rstd, void* stream) {
+  DNA_CHECK_ARG(x && residual && gamma && sum && rstd && (rms || (beta && mean)),
+                "dna_add_ln_fwd: null pointer");
   DNA_CHECK_ARG(y || y_bf16, "dna_add_ln_fwd: no output");
   DNA_CHECK_ARG(rows >= 0, "dna_add_ln_fwd: bad rows");
   DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_add_ln_fwd: bad dtype");
   if (rows == 0) return DNA_OK;
-  FwdArgs a{x, nullptr, 0, 0.f, 0u, 1.f, 0, 0, residual, gamma, beta, rows, cols, eps, y,
-            (bf16*)y_bf16, mean, rstd, 0, sum};
+  FwdArgs a{x, nullptr, 0, 0.f, 0u, 1.f, 0, 0, residual, gamma, rms ? nullptr : beta, rows, cols,
+            eps, y, (bf16*)y_bf16, rms ? nullptr : mean, rstd, rms ? 1 : 0, sum};
   hipStream_t s = as_stream(stream);
   dim3 grid((rows + WAVES - 1) / WAVES);
   int st = dispatch_cols(cols, [&](auto nv, auto vec) {
@@ -528,18 +530,19 @@ extern "C" int dna_add_ln_fwd(const void* x, int x_dtype, const float* residual,
 
 extern "C" int dna_add_ln_bwd(const float* dy, const void* dy_bf16, const float* dsum, const void* x,
                               int x_dtype, const float* residual, const float* gamma,
-                              const float* mean, const float* rstd, int rows, int cols,
+                              const float* mean, const float* rstd, int rows, int cols, int rms,
                               float* dresidual, void* dx, float* dgamma, float* dbeta,
                               void* workspace, size_t workspace_bytes, void* stream) {
-  DNA_CHECK_ARG(x && residual && gamma && mean && rstd && dx && dresidual, "dna_add_ln_bwd: null pointer");
+  DNA_CHECK_ARG(x && residual && gamma && rstd && dx && dresidual && (rms || mean),
+                "dna_add_ln_bwd: null pointer");
   DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_add_ln_bwd: bad dtype");
   if (rows == 0) return DNA_OK;
   DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
                 "dna_add_ln_bwd: workspace too small (%zu < %zu)", workspace_bytes,
                 dna_ln_bwd_workspace(rows, cols));
   const int nb = bwd_blocks(rows);
-  BwdArgs a{dy, (const bf16*)dy_bf16, x, nullptr, 0, 0.f, 0u, 1.f, 0, 0, residual, gamma, mean,
-            rstd, rows, cols, dresidual, dx, (float*)workspace, 0, dsum};
+  BwdArgs a{dy, (const bf16*)dy_bf16, x, nullptr, 0, 0.f, 0u, 1.f, 0, 0, residual, gamma,
+            rms ? nullptr : mean, rstd, rows, cols, dresidual, dx, (float*)workspace, rms ? 1 : 0, dsum};
   hipStream_t s = as_stream(stream);
   const size_t lds = (size_t)WAVES * 3 * cols * sizeof(float);
   int st = dispatch_cols(cols, [&](auto nv, auto vec) {
@@ -552,7 +555,7 @@ extern "C" int dna_add_ln_bwd(const float* dy, const void* dy_bf16, const float*
   });
   if (st) return st;
   hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
-                     (const float*)workspace, nb, cols, dgamma, dbeta, (float*)nullptr);
+                     (const float*)workspace, nb, cols, dgamma, rms ? (float*)nullptr : dbeta, (float*)nullptr);
   DNA_LAUNCH_CHECK("dna_add_ln_bwd");
   return DNA_OK;
 }

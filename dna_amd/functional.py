@@ -335,7 +335,8 @@ class FusedLayerNorm(torch.autograd.Function):
 
 class AddLayerNorm(torch.autograd.Function):
     """Pre-norm residual add + LN: (x, residual fp32) -> (sum = x + residual fp32, LN(sum) fp32
-    or bf16) in one pass (dna_add_ln_fwd). The flash_attn Block's `residual = dropout(x) +
+    or bf16) in one pass (dna_add_ln_fwd); beta None = RMSNorm (mamba_ssm's fused add + RMSNorm
+    of the Caduceus Blocks). The flash_attn Block's `residual = dropout(x) +
     residual; norm(residual)` with residual_in_fp32 and dropout p = 0 (HyenaDNA's Blocks,
     long_conv_lm.py:205-267): same fp32 sum, same LN. The backward adds the gradient of `sum`
     from the residual stream to the LN's input gradient in the same kernel (dna_add_ln_bwd), so
@@ -347,27 +348,30 @@ class AddLayerNorm(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         x, residual = x.contiguous(), residual.contiguous()
         n, d = x.shape
+        rms = beta is None  # RMSNorm (AddRMSNorm)
         s = torch.empty(n, d, device=x.device, dtype=torch.float32)
         y = torch.empty(n, d, device=x.device, dtype=torch.bfloat16 if want_bf16 else torch.float32)
-        mean = torch.empty(n, device=x.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
+        mean = None if rms else torch.empty(n, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(n, device=x.device, dtype=torch.float32)
         nbytes = n * (d * (x.element_size() + 8 + y.element_size()) + 8)
         with _timed("ln_fwd", nbytes, "byte"):
             N.call("dna_add_ln_fwd", x.data_ptr(), _dt(x), residual.data_ptr(), gamma.data_ptr(),
-                   beta.data_ptr(), n, d, eps, s.data_ptr(), None if want_bf16 else y.data_ptr(),
-                   y.data_ptr() if want_bf16 else None, mean.data_ptr(), rstd.data_ptr(),
-                   N.stream_ptr())
+                   _p(beta), n, d, eps, int(rms), s.data_ptr(),
+                   None if want_bf16 else y.data_ptr(), y.data_ptr() if want_bf16 else None,
+                   _p(mean), rstd.data_ptr(), N.stream_ptr())
         ctx.save_for_backward(x, residual, gamma, mean, rstd)
+        ctx.rms = rms
         return s, y
 
     @staticmethod
     def backward(ctx, ds, dy):
         x, residual, gamma, mean, rstd = ctx.saved_tensors
+        rms = ctx.rms
         n, d = x.shape
         dx = torch.empty_like(x)
         dres = torch.empty(n, d, device=x.device, dtype=torch.float32)
         dg = torch.empty_like(gamma)
-        db = torch.empty_like(gamma)
+        db = None if rms else torch.empty_like(gamma)
         nws = N.lib().dna_ln_bwd_workspace(n, d)
         ws = torch.empty(max(nws, 16), device=x.device, dtype=torch.uint8)
         dy = None if dy is None else dy.contiguous()
@@ -378,8 +382,8 @@ class AddLayerNorm(torch.autograd.Function):
                            + (4 if ds is not None else 0) + 2 * x.element_size() + 8) + 8)
         with _timed("ln_bwd", nbytes, "byte"):
             N.call("dna_add_ln_bwd", _p(dyf), _p(dyb), _p(ds), x.data_ptr(), _dt(x),
-                   residual.data_ptr(), gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, d,
-                   dres.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), ws.data_ptr(),
+                   residual.data_ptr(), gamma.data_ptr(), _p(mean), rstd.data_ptr(), n, d, int(rms),
+                   dres.data_ptr(), dx.data_ptr(), dg.data_ptr(), _p(db), ws.data_ptr(),
                    nws, N.stream_ptr())
         return dx, dres, dg, db, None, None
 
@@ -794,17 +798,15 @@ def wgrad(dy, x):
     exact-fp32 MFMA kernel's slices for fp32)."""
     if _f32_gemm_ok(x, dy):
         parts, s = _hip_wgrad_f32_parts(dy, x)
-        out = torch.zeros(parts.shape[1:], device=dy.device, dtype=torch.float32)
-        N.call("dna_sum_slices_accum", parts.data_ptr(), s, out.numel(), out.data_ptr(),
-               N.stream_ptr())
+        out = torch.empty(parts.shape[1:], device=dy.device, dtype=torch.float32)
+        N.call("dna_sum_slices", parts.data_ptr(), s, out.numel(), out.data_ptr(), N.stream_ptr())
         return out
     if x.dtype == torch.float32:
         return torch.mm(dy.t(), x)
     if _hip_wgrad_ok(dy, x):
         parts, s = _hip_wgrad_parts(dy, x)
-        out = torch.zeros(parts.shape[1:], device=dy.device, dtype=torch.float32)
-        N.call("dna_sum_slices_accum", parts.data_ptr(), s, out.numel(), out.data_ptr(),
-               N.stream_ptr())
+        out = torch.empty(parts.shape[1:], device=dy.device, dtype=torch.float32)
+        N.call("dna_sum_slices", parts.data_ptr(), s, out.numel(), out.data_ptr(), N.stream_ptr())
         return out
     rows, m = dy.shape
     n = x.shape[1]

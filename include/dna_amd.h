@@ -128,13 +128,15 @@ int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, int x_dtype,
  * p = 0). x [rows, cols] x_dtype; residual, sum [rows, cols] fp32; y fp32 and / or y_bf16.
  * Backward: dsum = gradient of `sum` from its other consumers (NULL: none), added to the LN's
  * input gradient; writes dresidual (fp32) = dx (x_dtype) = that total, dgamma / dbeta (written).
+ * rms = 1: RMSNorm instead (no mean, no beta: beta / mean / dbeta may be NULL) -- mamba_ssm's
+ * Block with fused_add_norm as the Caduceus Blocks use it (modeling_caduceus.py:25-65).
  * workspace >= dna_ln_bwd_workspace(rows, cols). */
 int dna_add_ln_fwd(const void* x, int x_dtype, const float* residual, const float* gamma,
-                   const float* beta, int rows, int cols, float eps, float* sum, float* y,
+                   const float* beta, int rows, int cols, float eps, int rms, float* sum, float* y,
                    void* y_bf16, float* mean, float* rstd, void* stream);
 int dna_add_ln_bwd(const float* dy, const void* dy_bf16, const float* dsum, const void* x,
                    int x_dtype, const float* residual, const float* gamma, const float* mean,
-                   const float* rstd, int rows, int cols, float* dresidual, void* dx,
+                   const float* rstd, int rows, int cols, int rms, float* dresidual, void* dx,
                    float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
                    void* stream);
 

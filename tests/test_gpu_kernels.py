@@ -196,9 +196,14 @@ def test_fused_layernorm(dtype, cols, act, use_bias, use_res):
         assert (a.grad.float() - r.grad).abs().max().item() < tol * sc
 
 
+def _rms_ref(x, g, eps):
+    return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * g
+
+
+@pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cols", [128, 256, 1024])
-def test_add_layernorm_vs_torch(dtype, cols):
+def test_add_layernorm_vs_torch(dtype, cols, rms):
     """dna_add_ln_fwd / bwd (the HyenaDNA Block's residual add + norm): the fp32 sum is bit-equal
     to torch's `x + residual`; LN output and every gradient -- with the sum also consumed
     downstream, as the next Block's residual add does -- match the fp32 torch graph."""
@@ -211,10 +216,11 @@ def test_add_layernorm_vs_torch(dtype, cols):
     bt = 0.1 * torch.randn(cols, device=DEV)
     want_bf16 = dtype == torch.bfloat16
     leaves = [t.clone().requires_grad_(True) for t in (x, res, gm, bt)]
-    s, y = DF.AddLayerNorm.apply(*leaves, 1e-5, want_bf16)
+    s, y = DF.AddLayerNorm.apply(*leaves[:3], None if rms else leaves[3], 1e-5, want_bf16)
     refl = [t.detach().clone().requires_grad_(True) for t in (x, res, gm, bt)]
     sr = refl[0] + refl[1]
-    yr = torch.nn.functional.layer_norm(sr, (cols,), refl[2], refl[3], 1e-5)
+    yr = (_rms_ref(sr, refl[2], 1e-5) if rms
+          else torch.nn.functional.layer_norm(sr, (cols,), refl[2], refl[3], 1e-5))
     assert s.dtype == torch.float32 and torch.equal(s, sr)
     assert y.dtype == (torch.bfloat16 if want_bf16 else torch.float32)
     assert (y.float() - yr.float()).abs().max().item() < (3e-2 if want_bf16 else 1e-4)
@@ -223,11 +229,12 @@ def test_add_layernorm_vs_torch(dtype, cols):
     ((s * ds).sum() + (y.float() * dy.float()).sum()).backward()
     refl2 = [t.detach().float().clone().requires_grad_(True) for t in (x, res, gm, bt)]
     s2 = refl2[0] + refl2[1]
-    y2 = torch.nn.functional.layer_norm(s2, (cols,), refl2[2], refl2[3], 1e-5)
+    y2 = (_rms_ref(s2, refl2[2], 1e-5) if rms
+          else torch.nn.functional.layer_norm(s2, (cols,), refl2[2], refl2[3], 1e-5))
     ((s2 * ds).sum() + (y2 * dy.float()).sum()).backward()
     assert leaves[0].grad.dtype == dtype and leaves[1].grad.dtype == torch.float32
     tol = 2e-4 if dtype == torch.float32 else 3e-2
-    for a, r in zip(leaves, refl2):
+    for a, r in zip(leaves[:3] if rms else leaves, refl2):
         sc = max(r.grad.abs().max().item(), 1.0)
         assert (a.grad.float() - r.grad).abs().max().item() < tol * sc
 
