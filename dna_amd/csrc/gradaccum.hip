@@ -22,7 +22,15 @@ __global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gridDim.x * blockDim.x) {
     f32x4 acc = accum ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < s; ++k) acc += reinterpret_cast<const f32x4*>(parts + (size_t)k * n)[i];
+    int k = 0;
+    for (; k + 8 <= s; k += 8) {  // 8 slice loads in flight, added in slice order
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const f32x4*>(parts + (size_t)(k + u) * n)[i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; k < s; ++k) acc += reinterpret_cast<const f32x4*>(parts + (size_t)k * n)[i];
     reinterpret_cast<f32x4*>(out)[i] = acc;
   }
   for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
