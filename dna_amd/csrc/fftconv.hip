@@ -617,9 +617,35 @@ __global__ __launch_bounds__(NTH) void dbias_kernel(const T* __restrict__ dy, co
   __shared__ float red[NTH / 64];
   const int d = blockIdx.x, ch = blockIdx.y;
   const size_t tot = (size_t)B * L;
-  const size_t per = (tot + DB_CHUNKS - 1) / DB_CHUNKS;
-  const size_t beg = ch * per, end = min(tot, beg + per);
+  constexpr int VE = 16 / sizeof(T);
+  // 16-B path: chunk bounds on multiples of VE, so a VE-run never crosses a row (L % VE == 0)
+  const bool vec = L % VE == 0 && (((uintptr_t)dy | (uintptr_t)u) & 15) == 0;
+  size_t per = (tot + DB_CHUNKS - 1) / DB_CHUNKS;
+  if (vec) per = (per + VE - 1) / VE * VE;
+  const size_t beg = min(tot, ch * per), end = min(tot, beg + per);
   float s = 0.f;
+  typedef typename std::conditional<sizeof(T) == 2, bf16x8, f32x4>::type V16;
+  if (vec) {
+    for (size_t q = beg + (size_t)threadIdx.x * VE; q < end; q += (size_t)2 * NTH * VE) {
+      V16 a[2], b[2];
+#pragma unroll
+      for (int u2 = 0; u2 < 2; ++u2) {
+        const size_t qq = q + (size_t)u2 * NTH * VE;
+        if (qq < end) {
+          const size_t o = ((qq / L) * D + d) * (size_t)L + qq % L;
+          a[u2] = *reinterpret_cast<const V16*>(dy + o);
+          b[u2] = *reinterpret_cast<const V16*>(u + o);
+        } else {
+#pragma unroll
+          for (int j = 0; j < VE; ++j) { a[u2][j] = T(0.f); b[u2][j] = T(0.f); }
+        }
+      }
+#pragma unroll
+      for (int u2 = 0; u2 < 2; ++u2)
+#pragma unroll
+        for (int j = 0; j < VE; ++j) s += to_f32((T)a[u2][j]) * to_f32((T)b[u2][j]);
+    }
+  } else
   for (size_t q = beg + threadIdx.x; q < end; q += 4 * NTH) {
     float a[4], b[4];
 #pragma unroll
