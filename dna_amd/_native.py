@@ -85,6 +85,7 @@ _SIGS = {
     "dna_geglu_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
     "dna_geglu_linear_dgrad": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
     "dna_geglu_linear_dgrad_p": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
+    "dna_gelu_linear_dgrad_p": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_fftconv_workspace": (_sz, [_i, _i, _i]),
     "dna_fftconv_kspec_elems": (_sz, [_i]),
     "dna_fftconv_filter": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _sz, _vp]),

@@ -129,6 +129,18 @@ __device__ __forceinline__ void gelu_erf_and_grad(float x, float& g, float& dg) 
   g = x * cdf;
   dg = fmaf(x * 0.3989422804014327f, e, cdf);  // e = exp(-x^2 / 2)
 }
+// d/dx of the tanh-approximation GELU 0.5 x (1 + tanh(k (x + 0.044715 x^3))), k = sqrt(2/pi),
+// in the operation order of torch's GeluBackward (approximate="tanh")
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float kBeta = 0.7978845608028654f, kKappa = 0.044715f;
+  const float x_sq = x * x, x_cube = x_sq * x;
+  const float inner = kBeta * (x + kKappa * x_cube);
+  const float t = tanhf(inner);
+  const float left = 0.5f * x, right = 1.f + t;
+  const float left_derivative = 0.5f * right;
+  const float right_derivative = left * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x_sq);
+  return left_derivative + right_derivative;
+}
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   float g, dg;
   gelu_erf_and_grad(x, g, dg);

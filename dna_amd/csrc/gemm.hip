@@ -38,7 +38,7 @@ constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
 constexpr int HALF = 128 * BK * 2;      // bytes of one half-tile image (16 KB)
 constexpr int LDS_BYTES = 8 * HALF;     // 2 buffers x {A0, A1, B0, B1} = 128 KB
 
-enum Epi { EPI_BF16 = 0, EPI_F32 = 1, EPI_GEGLU = 2, EPI_GEGLU_BWD = 3 };
+enum Epi { EPI_BF16 = 0, EPI_F32 = 1, EPI_GEGLU = 2, EPI_GEGLU_BWD = 3, EPI_GELU_BWD = 4 };
 
 typedef __attribute__((address_space(3))) void lds_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -586,7 +586,8 @@ static_assert(pend_stores<EPI_BF16>(1, 0) == 16 && pend_stores<EPI_BF16>(1, 3) =
 template <int EPI, int ABL = 0, int SCH = 0>
 __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU ||
-                    (EPI == EPI_GEGLU_BWD && SCH == 2 && (ABL == 0 || ABL == 64 || ABL == 128)),
+                    (EPI == EPI_GEGLU_BWD && SCH == 2 && (ABL == 0 || ABL == 64 || ABL == 128)) ||
+                    (EPI == EPI_GELU_BWD && SCH == 2 && ABL == 0),
                 "persistent kernel: bf16 / GeGLU epilogues (GeGLU backward: lean body only)");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   const int KT = a.K / BK;
   const int V = nb * KT;
   float* bias_lds = reinterpret_cast<float*>(smem + LDS_BYTES);
-  const int nbias = EPI == EPI_GEGLU ? 2 * a.F : EPI == EPI_GEGLU_BWD ? 0 : a.N;
+  const int nbias = EPI == EPI_GEGLU ? 2 * a.F : (EPI == EPI_GEGLU_BWD || EPI == EPI_GELU_BWD) ? 0 : a.N;
   for (int c = tid * 4; c < nbias; c += NTHR * 4)
     *reinterpret_cast<f32x4*>(bias_lds + c) =
         a.bias ? *reinterpret_cast<const f32x4*>(a.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -716,7 +717,8 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   // past M fall outside the resource and are dropped
   const int cq = 4 * (lane >> 4);
   const int ldo = EPI == EPI_GEGLU ? 2 * a.F : a.ldc;
-  const auto rC = out_rsrc(EPI == EPI_GEGLU_BWD ? (void*)a.aux : a.C, (uint32_t)((size_t)a.M * ldo * 2));
+  const auto rC = out_rsrc((EPI == EPI_GEGLU_BWD || EPI == EPI_GELU_BWD) ? (void*)a.aux : a.C,
+                           (uint32_t)((size_t)a.M * ldo * 2));
   const uint32_t voC = (uint32_t)(((wr * 64 + (lane & 15)) * ldo + wc * 32 + cq) * 2);
   // BF16: a quadrant (mq, nq) is final right after its MFMAs in a unit's last K-step, so it is
   // stored there (bias from LDS), overlapping the remaining phases. For each (row block i) the
@@ -1118,16 +1120,20 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
     // exchange) are loaded in the phase's load half-phase, beside the fragment reads, and used
     // after its MFMAs -- the compiler's own vmcnt waits count them against the LDS-DMA stages
     // issued before; da is rounded to bf16 first, as the separate pass reads it
-    const auto rGi = out_rsrc(a.g, (uint32_t)((size_t)a.M * 2 * a.F * 2));
-    // g / dg rows are 2F wide = a.ldc (launcher), so the lane offset is voQ's (no extra VGPR)
+    // GeGLU backward: g / dg rows are 2F wide; GELU backward (EPI_GELU_BWD): h / dh rows F wide
+    // -- either way = a.ldc (launcher), so the lane offset is voQ's (no extra VGPR)
+    constexpr bool GELU = EPI == EPI_GELU_BWD;
+    const int gld = GELU ? a.F : 2 * a.F;
+    const auto rGi = out_rsrc(a.g, (uint32_t)((size_t)a.M * gld * 2));
     const uint32_t voGB = voQ;
     auto lgload = [&](const LCur& c, int mq, int nq, bf16x8 (&gv)[4][2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
-                                        ((c.m0 + mq * 128 + i * 16) * 2 * a.F + c.n0 + nq * 128) * 2);
+                                        ((c.m0 + mq * 128 + i * 16) * gld + c.n0 + nq * 128) * 2);
         gv[i][0] = load_b128h(rGi, (ABL & 128) ? kOOB : off);
       }
+      if constexpr (GELU) return;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
@@ -1140,6 +1146,17 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       for (int i = 0; i < 4; ++i) {
         const bf16x8 d = __builtin_bit_cast(bf16x8, swap8(acc[mq][nq][i][0], acc[mq][nq][i][1]));
         const int row = c.m0 + mq * 128 + i * 16;
+        if constexpr (GELU) {
+          // dh = bf16(da) * gelu_tanh'(h), da rounded to bf16 first as torch's separate
+          // GeluBackward reads it (the MLP fc2 data gradient, HyenaDNA Mlp)
+          bf16x8 o;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (bf16)((float)d[q] * gelu_tanh_grad((float)gv[i][0][q]));
+          const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
+                                          (row * a.F + c.n0 + nq * 128) * 2);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rC, off, 0, 0);
+          continue;
+        }
         // element index within the launch's row block (< 2^31: the launcher's row blocks keep
         // M * 2F * 2 bytes below 2^31); e % 8 == 0
         const uint32_t e = (uint32_t)(row + wr * 64 + l16) * (uint32_t)a.F + (uint32_t)(c.n0 + nq * 128 + colq);
@@ -1188,11 +1205,12 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       // GeGLU backward: each phase of the last step issues its quadrant's 8 g loads before its
       // stage (they stay in flight through the wait: + 8) and 8 stores after its MFMAs, each
       // group after an epilogue wait that retired everything older than its g loads
-      constexpr int QB = 8;
+      // (GELU backward: 4 h loads and 4 dh stores per quadrant)
+      constexpr int QB = EPI == EPI_GELU_BWD ? 4 : 8;
       constexpr int n = EPI == EPI_BF16
                             ? (role == 0 ? 8 : role == 1 ? 8 + p * QS : 8 + (4 - p) * QS)
-                            : EPI == EPI_GEGLU_BWD
-                            ? (role == 0 ? 8 : role == 1 ? 16 + p * QB : 8 + (4 - p) * QB)
+                            : (EPI == EPI_GEGLU_BWD || EPI == EPI_GELU_BWD)
+                            ? (role == 0 ? 8 : role == 1 ? 8 + QB + p * QB : 8 + (4 - p) * QB)
                             : (role == 0 ? 8 : role == 1 ? 8 + (p >= 2 ? GS : 0) : 8 + (p < 2 ? 2 * GS : GS));
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(n));
     };
@@ -1201,7 +1219,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       __builtin_amdgcn_sched_barrier(0);
     };
     constexpr bool SB = EPI == EPI_BF16;  // per-quadrant stores (else GeGLU halves)
-    constexpr bool GB = EPI == EPI_GEGLU_BWD;  // per-quadrant GeGLU-backward epilogue
+    constexpr bool GB = EPI == EPI_GEGLU_BWD || EPI == EPI_GELU_BWD;  // per-quadrant backward epilogue
     // one K-step k of the current unit in buffer parity par; ZI: the unit's first K-step (MFMA
     // chains start from zero)
     auto lstep = [&](auto par_c, auto role_c, auto zi_c, int k, const LCur& cur, const LCur& nxt) {
@@ -2069,6 +2087,45 @@ extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const vo
     else if (abl == 128) hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 128, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
     else hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 0, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
     DNA_LAUNCH_CHECK("dna_geglu_linear_dgrad_p");
+  }
+  return DNA_OK;
+}
+
+// dh = gelu_tanh'(h) * (dy . W) for the Mlp's fc2 (HyenaDNA Block, flash_attn Mlp with
+// activation gelu approximate="tanh"): the data gradient of fc2 through the transposed weight
+// copy wt [F][N] with the GELU backward in the epilogue (da never stored). dy [M][N], h / dh [M][F].
+extern "C" int dna_gelu_linear_dgrad_p(const void* dy, const void* wt, const void* h, int M, int F,
+                                       int N, void* dh, void* stream) {
+  DNA_CHECK_ARG(dy && wt && h && dh, "dna_gelu_linear_dgrad_p: null pointer");
+  DNA_CHECK_ARG(M >= 0 && N % BK == 0 && (N / BK) % 2 == 0 && N >= 2 * BK && F % BN == 0,
+                "dna_gelu_linear_dgrad_p: N %% 128 and F %% 256 required (N=%d F=%d)", N, F);
+  DNA_CHECK_ARG((size_t)F * N * 2 < (1ull << 31), "dna_gelu_linear_dgrad_p: weight too large");
+  if (M == 0) return DNA_OK;
+  Args a = base_args();
+  a.A = (const bf16*)dy; a.lda = N;
+  a.B = (const bf16*)wt; a.ldb = N;
+  a.C = nullptr; a.ldc = F; a.g = (const bf16*)h; a.aux = (bf16*)dh;
+  a.N = F; a.K = N; a.ksplit = N; a.F = F;
+  a.p = 0.f;
+  a.tilesN = F / BN;
+  a.GM = 8;
+  if (const char* e = getenv("DNA_GEMM_GM")) a.GM = atoi(e);
+  const size_t wide = (size_t)(N > F ? N : F) * 2;
+  const int cap = (int)(((1ull << 31) - 1) / wide / BM * BM);
+  DNA_CHECK_ARG(cap >= BM, "dna_gelu_linear_dgrad_p: rows of %zu bytes exceed 32-bit offsets", wide);
+  const int mc = row_block(M, cap);
+  for (int r0 = 0; r0 < M; r0 += mc) {
+    Args c = a;
+    c.A = a.A + (size_t)r0 * N;
+    c.g = a.g + (size_t)r0 * F;
+    c.aux = a.aux + (size_t)r0 * F;
+    c.M = M - r0 < mc ? M - r0 : mc;
+    c.tilesM = (c.M + BM - 1) / BM;
+    const int U = c.tilesM * c.tilesN;
+    int G = num_cus();
+    G = U < G ? U : (G & ~7);
+    hipLaunchKernelGGL((gemmp_kernel<EPI_GELU_BWD, 0, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
+    DNA_LAUNCH_CHECK("dna_gelu_linear_dgrad_p");
   }
   return DNA_OK;
 }

@@ -648,6 +648,60 @@ def bias_grad(dy):
     return dy.sum(0, dtype=torch.float32)
 
 
+class GeluLinear(torch.autograd.Function):
+    """o = gelu_tanh(h) . w^T + b as one autograd node (the flash_attn Mlp's act + fc2 in the
+    HyenaDNA Blocks, activation F.gelu(approximate="tanh")): forward = torch's GELU kernel then the
+    persistent GEMM; backward = fc2's data gradient with the GELU backward in its epilogue
+    (dna_gelu_linear_dgrad_p: dh = bf16(dy . w) * gelu'(h), the intermediate da never stored),
+    weight gradient from a = gelu(h), bias gradient by the native column sum."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, w_lp, w_lpt):
+        _gpu(h)
+        h = h.contiguous()
+        a = F.gelu(h, approximate="tanh")
+        flops = 2.0 * h.shape[0] * w_lp.shape[0] * w_lp.shape[1]
+        with _timed("gemm_hip", flops):
+            o = _hip_linear(a, w_lp, None if b is None else b.float())
+        ctx.save_for_backward(h, a, w_lpt)
+        ctx.weight = w
+        ctx.has_b = b is not None
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        h, a, w_lpt = ctx.saved_tensors
+        do = do.contiguous()
+        M, F_ = h.shape
+        Nn = do.shape[1]
+        flops = 2.0 * M * Nn * F_
+        dh = torch.empty_like(h)
+        with _timed("gemm_gelu_bwd", flops):
+            N.call("dna_gelu_linear_dgrad_p", do.data_ptr(), w_lpt.data_ptr(), h.data_ptr(), M, F_,
+                   Nn, dh.data_ptr(), N.stream_ptr())
+        dw = _weight_grad(ctx.weight, do, a, flops)
+        db = bias_grad(do) if ctx.has_b else None
+        return dh, dw, db, None, None
+
+
+def gelu_linear_ok(h, w):
+    """GeluLinear applies: bf16 CUDA activations, the persistent kernel's shapes (fc2's output
+    and input widths % 256: the forward is then the same GEMM hip_linear runs), the hand-written
+    GEMM path enabled."""
+    Nn, F_ = w.shape
+    return (h.is_cuda and h.dtype == torch.bfloat16 and Nn % 256 == 0
+            and F_ % 256 == 0 and _gemm_impl() == "hip"
+            and os.environ.get("DNA_GELU_BWD_FUSED", "1") != "0")
+
+
+def gelu_linear(h, w, b):
+    """F.linear(F.gelu(h, approximate="tanh"), w, b) under bf16 autocast (GeluLinear)."""
+    lead, F_ = h.shape[:-1], h.shape[-1]
+    w_lp = w.to(torch.bfloat16)
+    y = GeluLinear.apply(h.reshape(-1, F_), w, b, w_lp, w_lp.t().contiguous())
+    return y.view(*lead, w.shape[0])
+
+
 class Linear(torch.autograd.Function):
     """y = x @ w_lp^T (+ b): forward and dgrad on the compute dtype copy `w_lp` of the fp32
     master weight `w` -- bf16: the hand-written MFMA kernel (csrc/gemm.hip), the data gradient

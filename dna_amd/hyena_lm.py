@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import functional as DF
 from .functional import HipEmbedding
 from .hyena import HipLinear, HyenaOperator
 
@@ -50,6 +51,9 @@ class GPT2Embeddings(nn.Module):
 
 _LN_COLS = {64, 128, 192, 256, 512, 768, 1024}  # widths dna_ln_fwd/bwd are instantiated for
 _TORCH_LN = os.environ.get("DNA_HYENA_TORCH_LN", "0") == "1"  # A/B switch: torch's LayerNorm
+# A/B switch: the Mlp's act + fc2 as separate torch GELU + HipLinear nodes
+_TORCH_LINEAR_MLP = (os.environ.get("DNA_HYENA_TORCH_LINEAR", "0") == "1"
+                     or os.environ.get("DNA_GELU_BWD_FUSED", "1") == "0")
 
 
 class LayerNorm(nn.LayerNorm):
@@ -108,7 +112,19 @@ class Mlp(nn.Module):
         self.fc2 = HipLinear(hidden_features, out_features or in_features, **fk)
 
     def forward(self, x):
-        return self.fc2(self.activation(self.fc1(x)))
+        h = self.fc1(x)
+        if self._gelu_fused(h):
+            # act + fc2 as one node: fc2's data gradient carries the GELU backward (GeluLinear)
+            return DF.gelu_linear(h, self.fc2.weight, self.fc2.bias)
+        return self.fc2(self.activation(h))
+
+    def _gelu_fused(self, h):
+        act = self.activation
+        return (isinstance(act, partial) and act.func is F.gelu and not act.args
+                and act.keywords == {"approximate": "tanh"} and isinstance(self.fc2, HipLinear)
+                and not _TORCH_LINEAR_MLP and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16
+                and DF.gelu_linear_ok(h, self.fc2.weight))
 
 
 class Block(nn.Module):

@@ -299,6 +299,14 @@ int dna_geglu_linear_dgrad(const void* dy, const void* wo, const void* g, int M,
 int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const void* g, int M, int F, int N,
                              float p_drop, uint64_t seed, uint64_t offset, void* dg, void* stream);
 
+/* dh = gelu_tanh'(h) * bf16(dy . W) -- the data gradient of a Linear fed by a tanh-GELU (the
+ * flash_attn Mlp's fc2 in the HyenaDNA Blocks, reference long_conv_lm.py create_mlp_cls with
+ * activation gelu(approximate="tanh")) with torch's GeluBackward in the persistent kernel's
+ * epilogue. dy [M][N] bf16, wt = W^T [F][N] bf16 (W [N][F]), h / dh [M][F] bf16;
+ * N % 128 == 0, F % 256 == 0. */
+int dna_gelu_linear_dgrad_p(const void* dy, const void* wt, const void* h, int M, int F, int N,
+                            void* dh, void* stream);
+
 /* ------------------------------------------------------------------ HyenaDNA FFT long convolution
  * fftconv_ref (src/models/sequence/hyena.py:60-92) as used by HyenaFilter.forward (:253-280):
  *   y[b,d,t] = sum_{j<L} k[d,j] * u~[b,d,(t-j) mod 2L] + bias[d] * u[b,d,t],   t < L

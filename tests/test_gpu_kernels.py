@@ -803,3 +803,37 @@ def test_masked_cross_entropy_fwd_bwd_vs_torch(V):
     ref.backward()
     assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
     assert (logits.grad.float() - l32.grad).abs().max().item() <= 1e-2 * l32.grad.abs().max().item()
+
+
+@pytest.mark.parametrize("M,F,Nn", [(5000, 1024, 256), (131072, 1024, 256), (700, 256, 256)])
+def test_gelu_linear_fused_bwd_vs_separate(M, F, Nn):
+    """functional.GeluLinear (fc2 of the HyenaDNA Mlp: tanh-GELU + Linear, the GELU backward in
+    the data-gradient epilogue) against the separate torch GELU + HIP Linear nodes on the same
+    bf16 operands: same forward (bit-equal), dh within bf16 rounding of the unfused dh (da is
+    rounded to bf16 in both), weight / bias gradients equal."""
+    from dna_amd import functional as DF
+    from dna_amd.hyena import hip_linear
+    g = torch.Generator(device="cpu").manual_seed(M + F)
+    h = (torch.randn(M, F, generator=g) * 2).to(DEV).bfloat16()
+    w = (torch.randn(Nn, F, generator=g) / F ** 0.5).to(DEV)
+    b = torch.randn(Nn, generator=g).to(DEV) * 0.1
+    do = torch.randn(M, Nn, generator=g).to(DEV).bfloat16()
+    outs = []
+    for fused in (True, False):
+        hh = h.clone().requires_grad_(True)
+        ww = w.clone().requires_grad_(True)
+        bb = b.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if fused:
+                assert DF.gelu_linear_ok(hh, ww)
+                o = DF.gelu_linear(hh, ww, bb)
+            else:
+                o = hip_linear(torch.nn.functional.gelu(hh, approximate="tanh"), ww, bb)
+        o.backward(do)
+        outs.append((o.detach(), hh.grad, ww.grad, bb.grad))
+    (o1, dh1, dw1, db1), (o2, dh2, dw2, db2) = outs
+    assert torch.equal(o1, o2)
+    assert dh1.dtype == torch.bfloat16 and torch.isfinite(dh1.float()).all()
+    err = (dh1.float() - dh2.float()).abs().max().item()
+    assert err <= 1e-2 * dh2.float().abs().max().item(), err
+    assert torch.allclose(dw1, dw2, rtol=1e-5, atol=1e-5) and torch.allclose(db1, db2, rtol=1e-5, atol=1e-5)
