@@ -537,6 +537,27 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
     pr.rows(p, d, ra, rb);
     T* ya = y + (size_t)ra * g.L;
     T* yb = rb >= 0 ? y + (size_t)rb * g.L : nullptr;
+    constexpr int VE = 16 / sizeof(T);
+    typedef typename std::conditional<sizeof(T) == 2, bf16x8, f32x4>::type V16;
+    if (LN > 0 && cw % VE == 0 && off % VE == 0 && g.L % VE == 0 && ((uintptr_t)y & 15) == 0) {
+      // 16-B stores: VE consecutive columns of one n1 row (a chunk never straddles [0, L))
+      const int cpr = cw / VE;
+      for (int q = threadIdx.x; q < M1 * cpr; q += NTH) {
+        const int cc = q % cpr, n1 = q / cpr;
+        const int i = n1 * M2 + n20 + cc * VE - off;
+        if (i < 0 || i >= g.L) continue;
+        V16 va, vb;
+#pragma unroll
+        for (int j = 0; j < VE; ++j) {
+          const cf v = buf[lds_at(cc * VE + j, n1, S)];
+          va[j] = from_f32<T>(v.x);
+          vb[j] = from_f32<T>(v.y);
+        }
+        *reinterpret_cast<V16*>(ya + i) = va;
+        if (yb) *reinterpret_cast<V16*>(yb + i) = vb;
+      }
+      return;
+    }
     for (int e = threadIdx.x; e < cw * M1; e += NTH) {
       const int n1 = e >> lcw, c = e & (cw - 1);
       const int i = n1 * M2 + n20 + c - off;
@@ -546,6 +567,19 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
       if (yb) yb[i] = from_f32<T>(v.y);
     }
   } else {
+    if (LN > 0 && cw % 4 == 0 && g.L % 4 == 0 && ((uintptr_t)outf & 15) == 0) {
+      const int cpr = cw / 4;  // 16-B stores of 4 consecutive columns
+      for (int q = threadIdx.x; q < M1 * cpr; q += NTH) {
+        const int cc = q % cpr, n1 = q / cpr;
+        const int i = n1 * M2 + n20 + cc * 4;
+        if (i >= g.L) continue;
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = buf[lds_at(cc * 4 + j, n1, S)].x * scale;
+        *reinterpret_cast<f32x4*>(outf + (size_t)p * g.L + i) = o;
+      }
+      return;
+    }
     for (int e = threadIdx.x; e < cw * M1; e += NTH) {
       const int n1 = e >> lcw, c = e & (cw - 1);
       const int i = n1 * M2 + n20 + c;
