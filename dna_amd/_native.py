@@ -35,6 +35,7 @@ _SIGS = {
     "dna_colsum_f32": (_i, [_vp, _i, _i, _vp, _i, _vp]),
     "dna_colsum_bf16_workspace": (_sz, [_i, _i]),
     "dna_colsum_bf16": (_i, [_vp, _i, _i, _vp, _i, _vp, _sz, _vp]),
+    "dna_flip_rows": (_i, [_vp, _i, _i, _sz, _vp, _vp]),
     "dna_causal_conv1d_fwd": (_i, [_vp, _sz, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "dna_causal_conv1d_part_rows": (_sz, [_i, _i]),
     "dna_causal_conv1d_bwd": (_i, [_vp, _sz, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _sz, _vp, _vp]),

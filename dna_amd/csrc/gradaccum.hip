@@ -359,8 +359,31 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
     if (c0 + c < cols && r0 + r < rows) *reinterpret_cast<bf16x8*>(dst + (size_t)(c0 + c) * rows + r0 + r) = v;
   }
 }
+
+// dst[b][t][:] = src[b][L - 1 - t][:] (rows of `row16` 16-B chunks): the sequence flip of the
+// bidirectional Mamba wrapper, one 16-B chunk per thread, grid-stride over all chunks
+__global__ __launch_bounds__(256) void flip_rows_kernel(const uint4* __restrict__ src, int L, int row16,
+                                                        size_t total, uint4* __restrict__ dst) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t row = i / row16, c = i - row * row16;
+    const size_t b = row / L, t = row - b * L;
+    dst[i] = src[(b * L + (L - 1 - t)) * row16 + c];
+  }
+}
 }  // namespace gacc
 }  // namespace dna
+
+extern "C" int dna_flip_rows(const void* src, int B, int L, size_t row_bytes, void* dst, void* stream) {
+  DNA_CHECK_ARG(src && dst && src != dst && B > 0 && L > 0 && row_bytes > 0 && row_bytes % 16 == 0,
+                "dna_flip_rows: bad args (row_bytes %% 16 == 0, distinct buffers)");
+  DNA_CHECK_ARG((((uintptr_t)src | (uintptr_t)dst) & 15) == 0, "dna_flip_rows: 16-B alignment required");
+  const size_t total = (size_t)B * L * (row_bytes / 16);
+  const size_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(gacc::flip_rows_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     as_stream(stream), (const uint4*)src, L, (int)(row_bytes / 16), total, (uint4*)dst);
+  DNA_LAUNCH_CHECK("dna_flip_rows");
+  return DNA_OK;
+}
 
 extern "C" int dna_transpose_bf16(const void* src, int rows, int cols, void* dst, void* stream) {
   DNA_CHECK_ARG(src && dst && src != dst, "dna_transpose_bf16: bad pointers");

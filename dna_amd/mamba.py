@@ -399,6 +399,36 @@ class Mamba(nn.Module):
         return OutProj.apply(y, self.out_proj.weight, self.out_proj.bias)
 
 
+class FlipL(torch.autograd.Function):
+    """x.flip(dims=(1,)) of a [B, L, C] CUDA tensor by a 16-B row copy (dna_flip_rows); the
+    backward is the same flip. torch's flip kernel ran at ~2.9 TB/s on these shapes."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return _flip_rows(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _flip_rows(g)
+
+
+def _flip_rows(x):
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    B, L = x.shape[0], x.shape[1]
+    N.call("dna_flip_rows", x.data_ptr(), B, L, x[0, 0].numel() * x.element_size(), out.data_ptr(),
+           N.stream_ptr())
+    return out
+
+
+def flip_l(x):
+    """x.flip(dims=(1,)) (FlipL on CUDA tensors whose rows are whole 16-B chunks)."""
+    if (x.is_cuda and x.dim() >= 2 and x.numel() > 0 and x.is_contiguous()
+            and (x[0, 0].numel() * x.element_size()) % 16 == 0 and x.data_ptr() % 16 == 0):
+        return FlipL.apply(x)
+    return x.flip(dims=(1,))
+
+
 class BiMambaWrapper(nn.Module):
     """The reference's BiMambaWrapper (modeling_caduceus.py:68-121) over `Mamba` above."""
 
@@ -425,8 +455,7 @@ class BiMambaWrapper(nn.Module):
     def forward(self, hidden_states, inference_params=None):
         out = self.mamba_fwd(hidden_states, inference_params=inference_params)
         if self.bidirectional:
-            out_rev = self.mamba_rev(hidden_states.flip(dims=(1,)),
-                                     inference_params=inference_params).flip(dims=(1,))
+            out_rev = flip_l(self.mamba_rev(flip_l(hidden_states), inference_params=inference_params))
             if self.bidirectional_strategy == "add":
                 out = out + out_rev
             elif self.bidirectional_strategy == "ew_multiply":

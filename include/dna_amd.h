@@ -202,6 +202,11 @@ int dna_colsum_f32(const float* part, int rows, int cols, float* out, int accumu
 size_t dna_colsum_bf16_workspace(int rows, int cols);
 int dna_colsum_bf16(const void* x, int rows, int cols, float* out, int accumulate, void* workspace,
                     size_t workspace_bytes, void* stream);
+
+/* dst[b][t] = src[b][L - 1 - t] for rows of row_bytes (% 16 == 0) bytes, src / dst distinct and
+ * 16-B aligned: torch.flip(x, dims=(1,)) of a [B, L, C] tensor as the Caduceus BiMambaWrapper
+ * applies it (src/models/caduceus/modeling_caduceus.py:68-121). */
+int dna_flip_rows(const void* src, int B, int L, size_t row_bytes, void* dst, void* stream);
 /* out[i] += sum_{k<s} parts[k*n + i]: split-K partials of a weight gradient folded straight
  * into the flat fp32 gradient buffer (16-byte loads when the buffers are 16-byte aligned and
  * n % 4 == 0, element-wise otherwise). */

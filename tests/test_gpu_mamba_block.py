@@ -91,3 +91,18 @@ def test_bimamba_fwd_bwd_vs_oracle(strategy):
     assert _rel(hg.grad, hr.grad) < 2e-3
     for n, p in w.named_parameters():  # tied ones appear once, under the forward name
         assert _rel(p.grad, sd[n].grad) < 2e-3, n
+
+
+@pytest.mark.parametrize("shape,dtype", [((1, 131072, 256), torch.bfloat16), ((3, 77, 8), torch.float32),
+                                         ((2, 1000, 40), torch.bfloat16)])
+def test_flip_l_equals_torch_flip(shape, dtype):
+    """mamba.flip_l (dna_flip_rows, the BiMamba wrapper's sequence flip) == torch.flip(x, (1,)),
+    forward and gradient, bit for bit; rows that are not whole 16-B chunks take torch's flip."""
+    from dna_amd.mamba import flip_l
+    g = torch.Generator(device="cpu").manual_seed(shape[1])
+    x = torch.randn(*shape, generator=g).to(dtype).to("cuda").requires_grad_(True)
+    y = flip_l(x)
+    assert torch.equal(y, x.detach().flip(dims=(1,)))
+    dy = torch.randn(*shape, generator=g).to(dtype).to("cuda")
+    y.backward(dy)
+    assert torch.equal(x.grad, dy.flip(dims=(1,)))
