@@ -193,9 +193,14 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-b64", action="store_true", help="skip the extra per-GPU b=64 measurement")
     ap.add_argument("--no-data-pipeline", action="store_true", help="skip the host data-path timing")
+    ap.add_argument("--grad-wire", choices=("fp32", "bf16"), default="fp32",
+                    help="gradient all-reduce wire format (GradBucketReducer wire_dtype)")
     ap.add_argument("--dist-dry-run", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dump-params", default=None, help=argparse.SUPPRESS)  # debug: per-rank digest
     args = ap.parse_args()
+    # the timed step must stay on the hand-written kernels: any torch/hipBLASLt GEMM fallback in
+    # dna_amd.functional raises (DNA_STRICT_NATIVE=0 turns the check off for experiments)
+    os.environ.setdefault("DNA_STRICT_NATIVE", "1")
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: become one (N rank processes), before any GPU call in this process
@@ -217,8 +222,9 @@ def main():
         data_pipeline = measure_data_pipeline(args.batch, torch.device("cuda", local))
     # DNA_DIST_BACKEND=gloo (rehearsal only): every rank on the visible GPUs round-robin, gradient
     # all-reduce over gloo -- exercises the multi-rank bench path on a one-GPU box
-    from dna_amd.launch import init_rank_process_group, rank_device_index
-    if world > 1:
+    from dna_amd.launch import init_rank_process_group, rank_device_index, wants_process_group
+    use_pg = wants_process_group(world)  # DNA_DDP_FORCE=1: the RCCL leg at world 1 too
+    if use_pg:
         device = init_rank_process_group(local)
     else:
         device = torch.device("cuda", rank_device_index(local))
@@ -230,7 +236,8 @@ def main():
 
     torch.manual_seed(2222)
     model = BertForMaskedLM(MODEL_CFG, precision="bf16")
-    trainer = MLMTrainer(model, device, lr=5e-4, weight_decay=1e-5, max_grad_norm=1.0)
+    trainer = MLMTrainer(model, device, lr=5e-4, weight_decay=1e-5, max_grad_norm=1.0,
+                         wire_dtype=args.grad_wire)
     t_data = time.perf_counter()
     batches = make_batches(4, args.batch, rank, device)
     t_data = time.perf_counter() - t_data
@@ -347,7 +354,9 @@ def main():
                     "masking), random-init weights",
             "config": {"workload": "DNABERT-2-117M MLM pretrain seq_len=512 bf16 (BASELINE configs[1])",
                        "model": "DNABERT-2-117M", "global_batch": args.batch * world,
-                       "seq_len": SEQ, "parallelism": f"dp{world}"},
+                       "seq_len": SEQ, "parallelism": f"dp{world}", "grad_wire": args.grad_wire,
+                       "grad_allreduce": trainer.reducer.enabled},
+            "native_only": os.environ.get("DNA_STRICT_NATIVE") == "1",
             "model_tflops_per_gpu": round(value / world * TRAIN_FLOP_PER_SEQ / 1e12, 1),
             "model_mfu": round(value / world * TRAIN_FLOP_PER_SEQ / 1e12 / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(final_loss, 4),
@@ -355,7 +364,7 @@ def main():
             "data_pipeline": data_pipeline, "b64": b64,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -25,7 +25,7 @@ import os
 import numpy as np
 import torch
 
-from .hg38 import SequenceDataset, bert_mask, random_mask
+from .hg38 import FaultTolerantMixin, SequenceDataset, bert_mask, random_mask
 from .tokenizer import DNABertTokenizer
 
 _CODE = np.zeros(256, dtype=np.uint8)  # char -> 2-bit code (unknown -> 0 = 'A')
@@ -150,7 +150,7 @@ class DNABERT2Dataset(torch.utils.data.Dataset):
         return random_mask(data, tok.mask_token_id), target
 
 
-class DNABERT2Pretrain(SequenceDataset):
+class DNABERT2Pretrain(FaultTolerantMixin, SequenceDataset):
     """Data module "dnabert2_pretrain" (genomics.py:1326-1500)."""
     _name_ = "dnabert2_pretrain"
 
@@ -184,6 +184,8 @@ class DNABERT2Pretrain(SequenceDataset):
         self.pad_interval = pad_interval
         self.use_tokenizer = use_tokenizer
         self.objective = objective
+        self._init_fault_tolerant(shuffle, fault_tolerant, ddp, fast_forward_epochs,
+                                  fast_forward_batches)
 
     def setup(self, stage=None):
         if self.tokenizer_name != "bpe":

@@ -254,6 +254,8 @@ extern "C" int dna_gemm_f32_strided(const float* A, long long sam, long long sak
   DNA_CHECK_ARG(A && B && C, "dna_gemm_f32_strided: null pointer");
   DNA_CHECK_ARG(sak == 1 || sam == 1, "dna_gemm_f32_strided: A needs a unit stride along k or m");
   DNA_CHECK_ARG(sbk == 1 || sbn == 1, "dna_gemm_f32_strided: B needs a unit stride along k or n");
+  DNA_CHECK_ARG(splits == 1 || !bias_n,
+                "dna_gemm_f32_strided: a bias with split-K would be added once per slice");
   Args a{};
   a.A = A; a.sam = sam; a.sak = sak; a.saz = saz;
   a.B = B; a.sbk = sbk; a.sbn = sbn; a.sbz = sbz;

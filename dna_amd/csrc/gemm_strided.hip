@@ -253,6 +253,8 @@ extern "C" int dna_gemm_bf16_strided(const void* A, long long sam, long long sak
   DNA_CHECK_ARG(A && B && C, "dna_gemm_bf16_strided: null pointer");
   DNA_CHECK_ARG(sak == 1 || sam == 1, "dna_gemm_bf16_strided: A needs a unit stride along k or m");
   DNA_CHECK_ARG(sbk == 1 || sbn == 1, "dna_gemm_bf16_strided: B needs a unit stride along k or n");
+  DNA_CHECK_ARG(splits == 1 || !(bias_m || bias_n),
+                "dna_gemm_bf16_strided: a bias with split-K would be added once per slice");
   Args a{};
   a.A = (const bf16*)A; a.sam = sam; a.sak = sak; a.saz = saz;
   a.B = (const bf16*)B; a.sbk = sbk; a.sbn = sbn; a.sbz = sbz;

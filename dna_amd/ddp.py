@@ -14,6 +14,8 @@ The expected contribution count per parameter is discovered on the first backwar
 reduces everything at the end, unoverlapped) -- robust to unused / shared parameters like DDP's
 find_unused_parameters=True (train.py:630-639).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -25,7 +27,11 @@ class GradBucketReducer:
     into the fp32 flat gradient in finish(), after its collective. The 1/world average stays in
     the AdamW kernel either way (grad_scale)."""
 
-    def __init__(self, flat, bucket_mb: float = 25.0, group=None, wire_dtype="fp32"):
+    def __init__(self, flat, bucket_mb: float = 25.0, group=None, wire_dtype="fp32", force=None):
+        """force=True (or DNA_DDP_FORCE=1) runs the bucketed collectives even at world size 1,
+        over an initialised process group: on a one-GPU box that is the only way the RCCL leg
+        (per-bucket async all-reduce on RCCL's stream, finish()'s waits, the bf16 wire cast-back)
+        executes on hardware before a multi-GPU run (tests/test_gpu_rccl.py)."""
         self.flat = flat
         self.group = group
         if wire_dtype not in ("fp32", "bf16"):
@@ -54,7 +60,12 @@ class GradBucketReducer:
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in flat.params]
         for p in flat.params:  # contributions written directly by fused kernels report here
             p._dna_notify = self._hook
-        self.enabled = self.world > 1
+        if force is None:
+            force = os.environ.get("DNA_DDP_FORCE", "0") == "1"
+        if force and not dist.is_initialized():
+            raise RuntimeError("GradBucketReducer(force=True) needs an initialised process group "
+                               "(DNA_DDP_FORCE=1 with WORLD_SIZE=1: bench.py / train.py create it)")
+        self.enabled = self.world > 1 or bool(force)
 
     def _hook(self, p):
         if not self.enabled or not self._sync:
@@ -92,7 +103,7 @@ class GradBucketReducer:
         """Call before each backward; sync=False for accumulation micro-batches (no collective,
         gradients keep accumulating locally, like DDP's no_sync())."""
         self._sync = sync
-        if not sync:
+        if not sync or not self.enabled:
             return
         self._seen = {}
         self._works = []
@@ -134,10 +145,14 @@ def reduce_metrics(loss, num_tokens, group=None, extra=None):
     torchmetric states whose dist_reduce_fx is "sum"), returns (mean_loss, [their global sums])
     in place of the token count, still one collective."""
     lv = loss.detach().reshape(()).to(torch.float64)
+    grouped = dist.is_available() and dist.is_initialized()
+    if grouped and dist.get_backend(group) == "nccl" and not lv.is_cuda:
+        # RCCL reduces device buffers only (evaluate() passes a CPU placeholder loss)
+        lv = lv.to(torch.device("cuda", torch.cuda.current_device()))
     vals = [num_tokens] if extra is None else list(extra)
     t = torch.stack([lv] + [torch.as_tensor(v).detach().to(device=lv.device, dtype=torch.float64)
                             .reshape(()) for v in vals])
-    if dist.is_available() and dist.is_initialized():
+    if grouped:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         world = dist.get_world_size(group)
     else:

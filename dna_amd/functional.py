@@ -35,6 +35,26 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+class LibraryFallbackError(RuntimeError):
+    """A projection left the hand-written kernels for a torch/hipBLASLt GEMM under
+    DNA_STRICT_NATIVE=1 (bench.py sets it: the timed step must stay native)."""
+
+
+_FALLBACK_SEEN = set()
+
+
+def library_fallback(what, *shapes):
+    """Called wherever a projection is about to run on torch.mm / addmm / bmm instead of the
+    hand-written MFMA kernels (shapes the kernels do not take, or the DNA_GEMM_IMPL /
+    DNA_WGRAD_IMPL=torch A/B arms). DNA_STRICT_NATIVE=1 turns it into an error; otherwise each
+    (site, shapes) pair is counted once in `_FALLBACK_SEEN` (tests and bench read it)."""
+    key = (what,) + tuple(tuple(s) for s in shapes)
+    if os.environ.get("DNA_STRICT_NATIVE", "0") == "1":
+        raise LibraryFallbackError(f"dna_amd: {what} {shapes} would run on a library GEMM "
+                                   "(DNA_STRICT_NATIVE=1)")
+    _FALLBACK_SEEN.add(key)
+
+
 class OpTimer:
     """Optional HIP-event timing of ops on the stream they launch on (bench.py roofline).
     Disabled (None) by default: zero overhead on the product path."""
@@ -729,6 +749,7 @@ class Linear(torch.autograd.Function):
         if _f32_gemm_ok(x, w_lp):
             with _timed("gemm_f32", flops):
                 return _hip_linear_f32(x, w_lp, b)
+        library_fallback("linear forward", x.shape, w_lp.shape)
         with _timed("gemm", flops):
             if b is not None:
                 return torch.addmm(b.to(x.dtype), x, w_lp.t())
@@ -751,6 +772,7 @@ class Linear(torch.autograd.Function):
                 with _timed("gemm_f32", flops):
                     dx = _hip_dgrad_f32(dy, w_lp)
             else:
+                library_fallback("linear data gradient", dy.shape, w_lp.shape)
                 with _timed("gemm", flops):
                     dx = torch.mm(dy, w_lp)
         dw = _weight_grad(ctx.weight, dy, x, flops)
@@ -856,12 +878,14 @@ def wgrad(dy, x):
         N.call("dna_sum_slices", parts.data_ptr(), s, out.numel(), out.data_ptr(), N.stream_ptr())
         return out
     if x.dtype == torch.float32:
+        library_fallback("weight gradient", dy.shape, x.shape)
         return torch.mm(dy.t(), x)
     if _hip_wgrad_ok(dy, x):
         parts, s = _hip_wgrad_parts(dy, x)
         out = torch.empty(parts.shape[1:], device=dy.device, dtype=torch.float32)
         N.call("dna_sum_slices", parts.data_ptr(), s, out.numel(), out.data_ptr(), N.stream_ptr())
         return out
+    library_fallback("weight gradient", dy.shape, x.shape)
     rows, m = dy.shape
     n = x.shape[1]
     s = wgrad_splits(rows, m, n)
@@ -882,6 +906,7 @@ def wgrad_accumulate(dy, x, grad):
         parts, s = _hip_wgrad_parts(dy, x)
         N.call("dna_sum_slices_accum", parts.data_ptr(), s, m * n, grad.data_ptr(), N.stream_ptr())
         return
+    library_fallback("weight gradient", dy.shape, x.shape)
     s = wgrad_splits(rows, m, n)
     if s == 1:
         parts = torch.mm(dy.t(), x, out_dtype=torch.float32)

@@ -257,6 +257,76 @@ class EpochSampler(torch.utils.data.Sampler):
         return len(self.base)
 
 
+class FaultTolerantDistributedSampler(torch.utils.data.distributed.DistributedSampler):
+    """The reference's resumable sampler (fault_tolerant_sampler.py:64-122): a DistributedSampler
+    (permutation randperm(seed + epoch), padded / trimmed to whole shards, rank-strided) that
+    counts the indices it has yielded; state_dict() = {epoch, counter}; after load_state_dict the
+    next iteration starts `counter` indices into this rank's shard, once. Used for every world
+    size when the data module has fault_tolerant=True (the reference's one-process
+    RandomFaultTolerantSampler draws its permutation from an unseeded generator; here one
+    process is the world-1 case of the same seeded sampler)."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.counter = 0
+        self.restarting = False
+
+    def state_dict(self):
+        return {"epoch": self.epoch, "counter": self.counter}
+
+    def load_state_dict(self, state):
+        self.epoch = int(state["epoch"])
+        self.counter = int(state["counter"])
+        self.restarting = True
+
+    def __iter__(self):
+        shard = list(super().__iter__())
+        if self.restarting:
+            shard = shard[self.counter:]
+            self.restarting = False
+        else:
+            self.counter = 0
+        for i in shard:
+            self.counter += 1
+            yield i
+        self.counter = 0
+
+
+def check_fault_tolerant_args(shuffle, fault_tolerant, ddp, fast_forward_epochs,
+                              fast_forward_batches):
+    """The reference data modules' argument checks (genomics.py:1117-1126)."""
+    if fault_tolerant and not shuffle:
+        raise ValueError("fault_tolerant=True needs shuffle=True (genomics.py:1117-1118)")
+    if ddp and not fault_tolerant:
+        raise ValueError("ddp=True needs fault_tolerant=True (genomics.py:1120-1121)")
+    if (fast_forward_epochs is not None or fast_forward_batches is not None) and \
+            not (ddp and fault_tolerant):
+        raise ValueError("fast_forward_epochs / fast_forward_batches need ddp=True and "
+                         "fault_tolerant=True (genomics.py:1125-1126)")
+
+
+class FaultTolerantMixin:
+    """fault_tolerant / ddp / fast_forward_* of the reference's data modules: train.py reads
+    them and, on a resume, fast-forwards the FaultTolerantDistributedSampler instead of reading
+    and discarding the consumed batches."""
+
+    def _init_fault_tolerant(self, shuffle, fault_tolerant, ddp, fast_forward_epochs,
+                             fast_forward_batches):
+        check_fault_tolerant_args(shuffle, fault_tolerant, ddp, fast_forward_epochs,
+                                  fast_forward_batches)
+        self.fault_tolerant = bool(fault_tolerant)
+        self.ddp = bool(ddp)
+        self.fast_forward_epochs = fast_forward_epochs
+        self.fast_forward_batches = fast_forward_batches
+
+    def load_state_dict(self, checkpoint):
+        """genomics.py:1249-1253: the fit loop's completed epochs / batches of a checkpoint."""
+        if self.fault_tolerant:
+            loops = checkpoint["loops"]["fit_loop"]
+            self.fast_forward_epochs = loops["epoch_progress"]["current"]["completed"]
+            self.fast_forward_batches = loops["epoch_loop.batch_progress"]["current"]["completed"]
+
+
 def _profiler_attached():
     """rocprofv3 preloads its tool library, which brings the HSA runtime up before main()."""
     pre = os.environ.get("LD_PRELOAD", "")
@@ -297,7 +367,7 @@ class SequenceDataset:
             SequenceDataset.registry[cls._name_] = cls
 
 
-class BertHG38(SequenceDataset):
+class BertHG38(FaultTolerantMixin, SequenceDataset):
     """Data module "bert_hg38" (genomics.py:1059-1254)."""
     _name_ = "bert_hg38"
 
@@ -331,6 +401,8 @@ class BertHG38(SequenceDataset):
         self.use_tokenizer = use_tokenizer
         self.pad_max_length = pad_max_length
         self.objective = objective
+        self._init_fault_tolerant(shuffle, fault_tolerant, ddp, fast_forward_epochs,
+                                  fast_forward_batches)
         if use_fixed_len_val:
             raise NotImplementedError("use_fixed_len_val (BertHG38FixedDataset) is out of scope")
 

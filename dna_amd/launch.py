@@ -70,11 +70,21 @@ def rank_device_index(local_rank):
     return local_rank % max(1, torch.cuda.device_count())
 
 
+def wants_process_group(world):
+    """A process group exists for world > 1, and at world 1 when DNA_DDP_FORCE=1 asks the
+    gradient reducer to run its collectives anyway (the one-GPU RCCL rehearsal)."""
+    return world > 1 or os.environ.get("DNA_DDP_FORCE", "0") == "1"
+
+
 def init_rank_process_group(local_rank):
     """Bind this rank's GPU and join the process group (RCCL binds the device at init)."""
     import torch
     import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:  # a forced world-1 group started without a launcher
+        os.environ["MASTER_PORT"] = str(free_port())
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
     dev = rank_device_index(local_rank)
     torch.cuda.set_device(dev)
     if dist_backend() == "nccl":

@@ -104,6 +104,9 @@ class CausalConv1d(torch.autograd.Function):
         B, C, L = x.shape
         if x.stride(2) != 1 or x.stride(1) != L:
             x = x.contiguous()
+        if L % 8 == 0 and (x.data_ptr() % 16 or x.stride(0) % 8):
+            # the backward's 16-B path (taken for every L % 8 == 0) needs 16-B aligned rows
+            x = x.clone(memory_format=torch.contiguous_format)
         K = weight.shape[-1]
         w = weight.detach().reshape(C, K).float().contiguous()
         b = None if bias is None else bias.detach().float().contiguous()
@@ -122,6 +125,8 @@ class CausalConv1d(torch.autograd.Function):
         B, C, L = x.shape
         K = w.shape[1]
         dout = dout.contiguous().to(x.dtype)
+        if L % 8 == 0 and dout.data_ptr() % 16:
+            dout = dout.clone()
         dx = torch.empty(B, C, L, device=x.device, dtype=x.dtype)
         rows = N.lib().dna_causal_conv1d_part_rows(B, L)
         part = torch.empty(rows, C * (K + 1), device=x.device, dtype=torch.float32)
@@ -409,7 +414,12 @@ class FlipL(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return _flip_rows(g)
+        return _flip_rows(g) if _flip_rows_ok(g.contiguous()) else g.flip(dims=(1,))
+
+
+def _flip_rows_ok(x):
+    return (x.is_cuda and x.dim() >= 2 and x.numel() > 0 and x.is_contiguous()
+            and (x[0, 0].numel() * x.element_size()) % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
 def _flip_rows(x):
@@ -423,8 +433,7 @@ def _flip_rows(x):
 
 def flip_l(x):
     """x.flip(dims=(1,)) (FlipL on CUDA tensors whose rows are whole 16-B chunks)."""
-    if (x.is_cuda and x.dim() >= 2 and x.numel() > 0 and x.is_contiguous()
-            and (x[0, 0].numel() * x.element_size()) % 16 == 0 and x.data_ptr() % 16 == 0):
+    if _flip_rows_ok(x):
         return FlipL.apply(x)
     return x.flip(dims=(1,))
 

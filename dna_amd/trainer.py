@@ -62,7 +62,7 @@ class ModuleTrainer:
                               max_grad_norm=max_grad_norm)
         self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
         self.world = self.reducer.world
-        if self.world > 1:  # DDP construction broadcast
+        if self.reducer.enabled:  # DDP construction broadcast
             dist.broadcast(self.flat.flat, src=0)
         self.global_step = 0
 
@@ -96,7 +96,7 @@ class MLMTrainer:
             self.sched = LinearLRSchedulerWarmup(self.opt, **scheduler)
         self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
         self.world = self.reducer.world
-        if self.world > 1:  # DDP construction broadcast (C2 in SURVEY §2.2)
+        if self.reducer.enabled:  # DDP construction broadcast (C2 in SURVEY §2.2)
             dist.broadcast(self.flat.flat, src=0)
             self.flat.refresh_shadow()
         # dropout stream: derived from train.seed when given, and distinct per rank

@@ -123,3 +123,126 @@ def test_caduceus_loss_weights():
     l1, _ = m(ids, labels, loss_weights=torch.ones(2, 64, device=DEV))
     l0, _ = m(ids, labels)
     assert torch.allclose(l1, l0, rtol=1e-5)
+
+
+# ---- RCPS layers pinned to the reference module (tests/golden/rcps_golden.npz, made from
+# /root/reference/src/models/caduceus/modeling_rcps.py by tests/golden/make_rcps_golden.py):
+# dna_amd.caduceus' RCPS classes over the HIP embedding / LayerNorm / MFMA-GEMM Linear, fp32
+# (tolerance 1e-5 relative to the largest reference value) and under bf16 autocast (3e-2)
+import os  # noqa: E402
+
+import numpy as np  # noqa: E402
+
+_Z = np.load(os.path.join(os.path.dirname(__file__), "golden", "rcps_golden.npz"))
+
+
+def _zt(k, dtype=torch.float32, grad=False):
+    return torch.tensor(_Z[k]).to(DEV, dtype).requires_grad_(grad)
+
+
+def _tol(autocast):
+    return 3e-2 if autocast else 1e-5
+
+
+def _ctx(autocast):
+    return torch.autocast("cuda", dtype=torch.bfloat16) if autocast else torch.autocast("cuda", enabled=False)
+
+
+def _set_params(mod, **vals):
+    with torch.no_grad():
+        for name, v in vals.items():
+            mod.get_parameter(name).copy_(torch.tensor(_Z[v]))
+
+
+@pytest.mark.parametrize("autocast", [False, True])
+def test_rcps_embedding_vs_reference(autocast):
+    from dna_amd.caduceus import RCPSEmbedding
+    V, D = _Z["emb_W"].shape
+    m = RCPSEmbedding(V, D, {i: int(c) for i, c in enumerate(_Z["complement"])}).to(DEV)
+    _set_params(m, **{"embedding.weight": "emb_W"})
+    with _ctx(autocast):
+        y = m(torch.tensor(_Z["emb_ids"]).to(DEV))
+    assert _rel(y, torch.tensor(_Z["emb_out"])) < 1e-6  # a gather: exact in fp32
+    y.float().backward(_zt("emb_gout"))
+    assert _rel(m.embedding.weight.grad, torch.tensor(_Z["emb_dW"])) < 1e-5
+
+
+@pytest.mark.parametrize("autocast", [False, True])
+def test_rcps_wrapper_vs_reference(autocast):
+    from dna_amd.caduceus import RCPSWrapper
+    from dna_amd.hyena import HipLinear
+    D = _Z["wrap_W"].shape[0]
+    lin = HipLinear(D, D).to(DEV)
+    _set_params(lin, weight="wrap_W", bias="wrap_b")
+    x = _zt("wrap_x", grad=True)
+    with _ctx(autocast):
+        y = RCPSWrapper(lin)(x)
+    tol = _tol(autocast)
+    assert _rel(y, torch.tensor(_Z["wrap_out"])) < tol
+    y.float().backward(_zt("wrap_gout"))
+    for t, k in ((x, "wrap_dx"), (lin.weight, "wrap_dW"), (lin.bias, "wrap_db")):
+        assert _rel(t.grad, torch.tensor(_Z[k])) < tol, k
+
+
+@pytest.mark.parametrize("tag", ["an0", "an"])
+@pytest.mark.parametrize("autocast", [False, True])
+def test_rcps_add_norm_vs_reference(tag, autocast):
+    from dna_amd.caduceus import RCPSAddNormWrapper
+    from dna_amd.hyena_lm import LayerNorm
+    D = _Z[f"{tag}_g"].shape[0]
+    ln = LayerNorm(D).to(DEV)
+    _set_params(ln, weight=f"{tag}_g", bias=f"{tag}_beta")
+    x = _zt(f"{tag}_x", grad=True)
+    res = _zt(f"{tag}_res", grad=True) if f"{tag}_res" in _Z else None
+    with _ctx(autocast):
+        y, r = RCPSAddNormWrapper(ln)(x, residual=res, prenorm=True)
+    tol = _tol(autocast)
+    assert _rel(y, torch.tensor(_Z[f"{tag}_y"])) < tol
+    assert _rel(r, torch.tensor(_Z[f"{tag}_res_out"])) < 1e-6
+    torch.autograd.backward([y.float(), r.float()], [_zt(f"{tag}_gy"), _zt(f"{tag}_gres")])
+    checks = [(x, "dx"), (ln.weight, "dg"), (ln.bias, "dbeta")] + ([(res, "dres")] if res is not None else [])
+    for t, k in checks:
+        assert _rel(t.grad, torch.tensor(_Z[f"{tag}_{k}"])) < tol, k
+
+
+@pytest.mark.parametrize("tag", ["blk0", "blk"])
+@pytest.mark.parametrize("autocast", [False, True])
+def test_rcps_block_vs_reference(tag, autocast):
+    """RCPSMambaBlock(fused_add_norm=False, residual_in_fp32=True) with a Linear mixer."""
+    from dna_amd.caduceus import RCPSMambaBlock
+    from dna_amd.hyena import HipLinear
+    from dna_amd.hyena_lm import LayerNorm
+    D = _Z[f"{tag}_norm_g"].shape[0]
+    ln, mix = LayerNorm(D).to(DEV), HipLinear(D, D).to(DEV)
+    _set_params(ln, weight=f"{tag}_norm_g", bias=f"{tag}_norm_b")
+    _set_params(mix, weight=f"{tag}_mix_W", bias=f"{tag}_mix_b")
+    blk = RCPSMambaBlock(D, mix, ln, fused_add_norm=False, residual_in_fp32=True)
+    h = _zt(f"{tag}_h", grad=True)
+    res = _zt(f"{tag}_res", grad=True) if f"{tag}_res" in _Z else None
+    with _ctx(autocast):
+        hh, rr = blk(h, residual=res)
+    tol = _tol(autocast)
+    assert rr.dtype == torch.float32
+    assert _rel(hh, torch.tensor(_Z[f"{tag}_h_out"])) < tol
+    assert _rel(rr, torch.tensor(_Z[f"{tag}_res_out"])) < 1e-6
+    torch.autograd.backward([hh.float(), rr], [_zt(f"{tag}_gh"), _zt(f"{tag}_gres")])
+    checks = [(h, "dh"), (ln.weight, "dnorm_g"), (ln.bias, "dnorm_b"), (mix.weight, "dmix_W"),
+              (mix.bias, "dmix_b")] + ([(res, "dres")] if res is not None else [])
+    for t, k in checks:
+        assert _rel(t.grad, torch.tensor(_Z[f"{tag}_{k}"])) < tol, k
+
+
+@pytest.mark.parametrize("autocast", [False, True])
+def test_rcps_lm_head_vs_reference(autocast):
+    from dna_amd.caduceus import RCPSLMHead
+    V, D = _Z["head_W"].shape
+    head = RCPSLMHead(D, V, {i: int(c) for i, c in enumerate(_Z["complement"])}).to(DEV)
+    _set_params(head, **{"lm_head.weight": "head_W"})
+    x = _zt("head_x", grad=True)
+    with _ctx(autocast):
+        y = head(x)
+    tol = _tol(autocast)
+    assert _rel(y, torch.tensor(_Z["head_out"])) < tol
+    y.float().backward(_zt("head_gout"))
+    assert _rel(x.grad, torch.tensor(_Z["head_dx"])) < tol
+    assert _rel(head.lm_head.weight.grad, torch.tensor(_Z["head_dW"])) < tol

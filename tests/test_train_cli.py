@@ -229,3 +229,43 @@ def test_bench_two_ranks_real_model(tmp_path):
     assert math.isfinite(line["final_loss"])
     d0, d1 = _digests(dump, 2)
     assert d0["sha256"] == d1["sha256"], (d0, d1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault_tolerant", [False, True])
+def test_mid_epoch_resume_replays_the_uninterrupted_run(data_root, monkeypatch, tmp_path,
+                                                        fault_tolerant):
+    """Stop after 2 optimizer steps, resume from last.ckpt, run 2 more: steps 3-4 log the same
+    losses as an uninterrupted 4-step run. fault_tolerant=True (the reference's
+    FaultTolerantDistributedSampler, fault_tolerant_sampler.py:64-122) resumes inside the sampler
+    -- the consumed windows are never read again -- and the checkpoint carries the Lightning loop
+    counters its data modules read (genomics.py:1249-1253)."""
+    import torch
+    import train
+    from dna_amd.compose import compose
+    monkeypatch.setenv("DATA_PATH", data_root)
+    ft = [f"+dataset.fault_tolerant={str(fault_tolerant).lower()}"]
+    base = ["experiment=dnabert2/dnabert2_hg38_pretrain"] + CFG_A[:-1] + ft + \
+        ["trainer.accumulate_grad_batches=1", "trainer.log_every_n_steps=1",
+         "trainer.limit_val_batches=0", "trainer.limit_test_batches=0"]
+
+    def run(d, steps, resume=None):
+        monkeypatch.chdir(d)
+        extra = [f"trainer.resume_from_checkpoint={resume}" if resume else
+                 "trainer.resume_from_checkpoint=null", f"train.max_steps={steps}"]
+        buf = io.StringIO()
+        train.train(compose(os.path.join(ROOT, "configs"), "config", base + extra), out=buf)
+        logs = [json.loads(l) for l in buf.getvalue().splitlines()]
+        assert not any("val/loss" in l for l in logs)  # limit_val_batches=0: no evaluation
+        return {l["step"]: l["train/loss"] for l in logs if "train/loss" in l}
+
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    full = run(tmp_path / "a", 4)
+    first = run(tmp_path / "b", 2)
+    ck = torch.load(tmp_path / "b" / "checkpoints" / "last.ckpt", map_location="cpu",
+                    weights_only=True)
+    assert ck["loops"]["fit_loop"]["epoch_loop.batch_progress"]["current"]["completed"] == 2
+    rest = run(tmp_path / "b", 4, resume=str(tmp_path / "b" / "checkpoints" / "last.ckpt"))
+    assert first == {1: full[1], 2: full[2]}
+    assert rest == {3: full[3], 4: full[4]}, (rest, full)

@@ -91,11 +91,14 @@ def save_checkpoint(path, trainer, epoch, batches_done=0, metrics=None, best=Non
           "optimizer_states": [trainer.opt.state_dict()],
           "lr_schedulers": [trainer.sched.state_dict()] if trainer.sched else [],
           "dna_amd": {"dropout_rng": trainer.rng_state(), "batches_done": int(batches_done),
-                      "metrics": metrics or {}}}
-    if best is not None:  # ModelCheckpoint state, as Lightning keeps it under "callbacks"
-        ck["callbacks"] = {"ModelCheckpoint": {"monitor": best.monitor, "mode": best.mode,
-                                               "best_model_score": best.score,
-                                               "best_model_path": best.path}}
+                      "metrics": metrics or {}},
+          # the two Lightning loop counters the reference's fault-tolerant data modules read on
+          # resume (genomics.py:1249-1253)
+          "loops": {"fit_loop": {"epoch_progress": {"current": {"completed": int(epoch)}},
+                                 "epoch_loop.batch_progress": {"current": {"completed":
+                                                                           int(batches_done)}}}}}
+    if best is not None:  # ModelCheckpoint state, keyed and typed as Lightning 1.8 keeps it
+        ck["callbacks"] = {best.state_key: best.state_dict()}
     os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     tmp = path + ".tmp"
     torch.save(ck, tmp)
@@ -122,7 +125,8 @@ class BestCheckpoint:
     auto_insert_metric_name=False: the filename is the monitor name, "/" making a sub-directory),
     overwritten in place whenever the monitored value improves."""
 
-    def __init__(self, dirpath, monitor, mode="min", filename=None, save_top_k=1):
+    def __init__(self, dirpath, monitor, mode="min", filename=None, save_top_k=1,
+                 every_n_train_steps=None, every_n_epochs=None):
         if mode not in ("min", "max"):
             raise ValueError(f"model_checkpoint.mode={mode!r}: min or max")
         self.monitor, self.mode = monitor, mode
@@ -130,7 +134,40 @@ class BestCheckpoint:
         if self.enabled and int(save_top_k) != 1:
             raise NotImplementedError(f"model_checkpoint.save_top_k={save_top_k} (1 or 0)")
         self.path = os.path.join(dirpath, (filename or monitor or "best") + ".ckpt")
+        self.dirpath = dirpath
+        self.every_n_train_steps = int(every_n_train_steps or 0)
+        self.every_n_epochs = int(every_n_epochs if every_n_epochs is not None else 1)
         self.score = None
+
+    @property
+    def state_key(self):
+        """Lightning 1.8's ModelCheckpoint.state_key: class name + repr of the identifying
+        arguments, so Lightning's resume_from_checkpoint finds this entry."""
+        return "ModelCheckpoint" + repr({"monitor": self.monitor, "mode": self.mode,
+                                         "every_n_train_steps": self.every_n_train_steps,
+                                         "every_n_epochs": self.every_n_epochs,
+                                         "train_time_interval": None})
+
+    def state_dict(self):
+        score = None if self.score is None else torch.tensor(float(self.score))
+        return {"monitor": self.monitor, "best_model_score": score,
+                "best_model_path": self.path, "current_score": score, "dirpath": self.dirpath,
+                "best_k_models": {self.path: score} if score is not None else {},
+                "kth_best_model_path": self.path if score is not None else "",
+                "kth_value": score, "last_model_path": ""}
+
+    def load_from_checkpoint(self, ck):
+        """Best score from a checkpoint's callbacks: Lightning's state-key entry (tensor score),
+        or the plain "ModelCheckpoint" entry of round-4 checkpoints (float score)."""
+        cbs = ck.get("callbacks") or {}
+        st = cbs.get(self.state_key)
+        if st is None:
+            st = next((v for k, v in cbs.items() if k.startswith("ModelCheckpoint")
+                       and isinstance(v, dict) and v.get("monitor") == self.monitor), None)
+        if st is None or st.get("monitor", self.monitor) != self.monitor:
+            return
+        sc = st.get("best_model_score")
+        self.score = None if sc is None else float(sc)
 
     def improves(self, value):
         if self.score is None:
@@ -159,6 +196,34 @@ def eval_loaders(cfg, ds, world, rank, final=False):
     return out
 
 
+def params_log(model, pcfg):
+    """ParamsLog.on_fit_start (src/callbacks/params.py:26-37, on the hot-path callback list
+    configs/callbacks/base.yaml): params/total, params/trainable, params/fixed, each switched by
+    the callback's total / trainable / fixed flags."""
+    pcfg = pcfg.to_container() if hasattr(pcfg, "to_container") else dict(pcfg or {})
+    ps = list(model.parameters())
+    logs = {}
+    if pcfg.get("total", True):
+        logs["params/total"] = sum(p.numel() for p in ps)
+    if pcfg.get("trainable", True):
+        logs["params/trainable"] = sum(p.numel() for p in ps if p.requires_grad)
+    if pcfg.get("fixed", True):
+        logs["params/fixed"] = sum(p.numel() for p in ps if not p.requires_grad)
+    return logs
+
+
+def eval_batches(n, limit):
+    """Batches Lightning runs of an n-batch loader under limit_{val,test}_batches: a float is a
+    fraction (at least one batch when it is > 0), an int a count; 0 / 0.0 disables the loop."""
+    if limit is None:
+        return n
+    if isinstance(limit, float) and limit <= 1.0:
+        if limit <= 0.0:
+            return 0
+        return max(1, int(n * limit)) if n else 0
+    return min(n, max(0, int(limit)))
+
+
 def evaluate(trainer, loaders, device, pad_id, limit=1.0, tokens=None):
     """validation_step / test_step through _shared_step (train.py:339-380, 442-460) for the MLM
     task: forward-only on the training kernels in eval mode (dropout off), the task loss
@@ -179,11 +244,7 @@ def evaluate(trainer, loaders, device, pad_id, limit=1.0, tokens=None):
     try:
         with torch.no_grad():
             for name, loader in loaders:
-                n = len(loader)
-                if isinstance(limit, float) and limit <= 1.0:
-                    n = max(1, int(n * limit)) if n else 0
-                elif limit is not None:
-                    n = min(n, int(limit))
+                n = eval_batches(len(loader), limit)
                 loss_w = torch.zeros((), dtype=torch.float64, device=device)
                 nll = torch.zeros((), dtype=torch.float64, device=device)
                 bs_sum, numel_sum = 0, 0
@@ -209,7 +270,11 @@ def evaluate(trainer, loaders, device, pad_id, limit=1.0, tokens=None):
     res = {}
     for i, name in enumerate(names):
         lw, bs, nl, ne, tk = g[5 * i: 5 * i + 5]
-        res[f"{name}/loss"] = lw / max(bs, 1)
+        if bs == 0:
+            # no rank ran a batch of this loader (a zero limit, or drop_last shards smaller than
+            # the eval batch): nothing is logged -- a made-up 0.0 loss would become the best score
+            continue
+        res[f"{name}/loss"] = lw / bs
         res[f"{name}/perplexity"] = math.exp(nl / max(ne, 1))
         res[f"{name}/num_tokens"] = int(round(tk))
     return res
@@ -262,22 +327,28 @@ def train(cfg, dry_run=False, out=sys.stdout):
         raise ValueError(f"trainer.devices={want} but WORLD_SIZE={world}: start the run with "
                          f"`python train.py ...` (it launches one process per device) or a "
                          f"launcher with --nproc-per-node {want}")
-    from dna_amd.launch import init_rank_process_group, rank_device_index
-    if world > 1:
+    from dna_amd.launch import init_rank_process_group, rank_device_index, wants_process_group
+    use_pg = wants_process_group(world)  # DNA_DDP_FORCE=1: the RCCL leg at world 1 too
+    if use_pg:
         device = init_rank_process_group(local)
     else:
         device = torch.device("cuda", rank_device_index(local))
     torch.cuda.set_device(device)
     if rank == 0:
         print(json.dumps({"event": "start", "world": world, "parallelism": f"dp{world}",
-                          "backend": dist.get_backend() if world > 1 else None,
+                          "backend": dist.get_backend() if use_pg else None,
                           "global_batch": int(cfg.dataset.get("batch_size", 0) or 0) * world}),
               file=out, flush=True)
+    ck_cfg = cfg.get("callbacks", {}) or {}
+    if rank == 0 and ck_cfg and ck_cfg.get("params") is not None:
+        print(json.dumps(dict({"event": "params"}, **params_log(model, ck_cfg.params))),
+              file=out, flush=True)
+    wire = str(tr.get("grad_wire", "fp32") or "fp32")
     trainer = MLMTrainer(model, device, lr=float(opt.lr),
                          weight_decay=float(opt.get("weight_decay", 0.0)),
                          betas=tuple(opt.get("betas", (0.9, 0.999))),
                          max_grad_norm=float(tr.get("gradient_clip_val", 0.0) or 0.0),
-                         scheduler=sched, seed=seed)
+                         scheduler=sched, seed=seed, wire_dtype=wire)
     resume = tr.get("resume_from_checkpoint") or cfg.train.get("ckpt")
     start_epoch, skip_batches, restored = 0, 0, {}
     if resume:
@@ -304,9 +375,20 @@ def train(cfg, dry_run=False, out=sys.stdout):
     # the permutation is randperm(seed + epoch) on every world size (DistributedSampler
     # semantics), so a mid-epoch resume replays exactly the interrupted epoch's
     # order, and the masks are keyed on (train.seed, epoch, window) (EpochSampler)
-    sampler = torch.utils.data.distributed.DistributedSampler(
+    fault_tolerant = bool(getattr(ds, "fault_tolerant", False))
+    sampler_cls = torch.utils.data.distributed.DistributedSampler
+    if fault_tolerant:
+        # the reference's FaultTolerantDistributedSampler (fault_tolerant_sampler.py:64-122,
+        # genomics.py:1208-1217): a resume skips the consumed indices in the sampler, so the
+        # loader never reads / tokenises them
+        from dna_amd.hg38 import FaultTolerantDistributedSampler as sampler_cls
+    sampler = sampler_cls(
         ds.dataset_train, num_replicas=world, rank=rank,
         shuffle=True if world > 1 else bool(getattr(ds, "shuffle", True)), seed=int(seed or 0))
+    if fault_tolerant and skip_batches == 0 and getattr(ds, "fast_forward_epochs", None) is not None \
+            and getattr(ds, "fast_forward_batches", None) is not None:
+        # dataset.fast_forward_{epochs,batches} given in the config (genomics.py:1212-1217)
+        start_epoch, skip_batches = int(ds.fast_forward_epochs), int(ds.fast_forward_batches)
     if seed is not None and hasattr(ds.dataset_train, "mask_seed"):
         ds.dataset_train.mask_seed = (int(seed) * 0x9E3779B1 + 2222) & (2 ** 63 - 1)
     loader = ds.train_dataloader(sampler=sampler)
@@ -316,7 +398,6 @@ def train(cfg, dry_run=False, out=sys.stdout):
     log_every = int(tr.get("log_every_n_steps", 10) or 10)
     limit = tr.get("limit_train_batches", 1.0)
     pad_id = getattr(ds.tokenizer, "pad_token_id", 3)
-    ck_cfg = cfg.get("callbacks", {}) or {}
     mc = ck_cfg.get("model_checkpoint") if ck_cfg else None
     ck_path, best = None, None
     if mc is not None:
@@ -330,10 +411,11 @@ def train(cfg, dry_run=False, out=sys.stdout):
         monitor = mc.get("monitor", cfg.train.get("monitor"))
         best = BestCheckpoint(d, monitor, mode=mc.get("mode", cfg.train.get("mode", "min")),
                               filename=mc.get("filename", monitor),
-                              save_top_k=mc.get("save_top_k", 1))
-        prev = (ck.get("callbacks") or {}).get("ModelCheckpoint") if resume and os.path.exists(resume) else None
-        if prev and prev.get("monitor") == best.monitor:
-            best.score = prev.get("best_model_score")
+                              save_top_k=mc.get("save_top_k", 1),
+                              every_n_train_steps=mc.get("every_n_train_steps"),
+                              every_n_epochs=mc.get("every_n_epochs"))
+        if resume and os.path.exists(resume):
+            best.load_from_checkpoint(ck)
     ck_every = int((mc.get("every_n_train_steps") if mc is not None else 0) or 1000)
     limit_val = tr.get("limit_val_batches", 1.0)
     limit_test = tr.get("limit_test_batches", 1.0)
@@ -378,6 +460,9 @@ def train(cfg, dry_run=False, out=sys.stdout):
         if final not in eval_cache:  # built once: persistent workers live across epochs
             eval_cache[final] = eval_loaders(cfg, ds, world, rank, final=final)
         loaders = eval_cache[final]
+        lim = limit_test if final else limit_val
+        if lim is not None and not isinstance(lim, bool) and float(lim) == 0.0:
+            return {}  # limit_{val,test}_batches=0: the evaluation loop is disabled
         res = evaluate(trainer, loaders, device, pad_id,
                        limit=limit_test if final else limit_val, tokens=eval_tokens)
         if rank == 0 and res:
@@ -418,8 +503,14 @@ def train(cfg, dry_run=False, out=sys.stdout):
         elif limit:
             n_batches = min(n_batches, int(limit))
         micro = []
-        bi = -1
-        for bi, ((masked, mask, labels), target) in enumerate(loader):
+        first = 0
+        if fault_tolerant and skip_batches:
+            # mid-epoch resume in the sampler: this rank's first skip_batches * batch_size
+            # indices of the epoch's permutation are not yielded again
+            sampler.load_state_dict({"epoch": epoch, "counter": skip_batches * int(ds.batch_size)})
+            first, skip_batches = skip_batches, 0
+        bi = first - 1
+        for bi, ((masked, mask, labels), target) in enumerate(loader, start=first):
             if bi >= n_batches:
                 bi -= 1
                 break
@@ -458,7 +549,7 @@ def train(cfg, dry_run=False, out=sys.stdout):
         with open(os.path.join(dump, f"rank{rank}.json"), "w") as f:
             json.dump(dict(flat_digest(trainer.flat.flat), rank=rank, world=world,
                            global_step=trainer.global_step), f)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
     return trainer
