@@ -118,7 +118,9 @@ def test_train_config_a_runs_on_gpu(data_root, monkeypatch, tmp_path):
     assert os.path.exists(best)
     import torch
     ck = torch.load(best, map_location="cpu", weights_only=True)
-    assert ck["callbacks"]["ModelCheckpoint"]["best_model_score"] == pytest.approx(ev[0]["test/loss"])
+    (key, st), = ck["callbacks"].items()  # Lightning 1.8's ModelCheckpoint state_key, tensor score
+    assert key.startswith("ModelCheckpoint{'monitor': 'test/loss'")
+    assert float(st["best_model_score"]) == pytest.approx(ev[0]["test/loss"])
     # resume from the Lightning-layout checkpoint
     cfg2 = compose(os.path.join(ROOT, "configs"), "config",
                    ["experiment=dnabert2/dnabert2_hg38_pretrain"] + CFG_A[:-1] +
