@@ -1531,8 +1531,8 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
     const int kl_t = tid_t & 31;
     unsigned padm_t = padm;
     asm volatile("" : "+v"(padm_t));
-    SRegs nx;
-    if (t + 1 < NS) load_slice(t + 1, nx, tid_t);
+    SRegs nx;  // next slice's Q / O / dO / LSE: loaded in the drain step of phase 1 (kb == KB,
+               // no S' / dP' registers live), stored to LDS after phase 2
     const bf16* Q = Qimg + buf * 32 * D;
     const bf16* O = Oimg + buf * 32 * D;
     const float* RC = rc + buf * 128;
@@ -1543,22 +1543,25 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
     // (one wave per SIMD: overlap has to come from this wave's own instruction order; the
     // sched_barriers keep the compiler from regrouping it)
     bf16x8 pbp[2], sbp[2];  // P and dS (bf16) of the previous block
-    f32x16 negd;            // -delta of this slice's rows: the dP' initial accumulator of every block
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 96 + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) negd[4 * g4 + e] = d4[e];
-    }
     const int tq = 4 * (g16 >> 1) + (i16 >> 2);  // tr-read row of lane
     auto tr_pair = [&](const bf16* img, int j) {  // A operand (dO^T or Q^T) of pair j = (s2, dt)
       const int qrow = 16 * (j >> 1) + tq;
       const int dcol = 32 * (j & 1) + 16 * (g16 & 1) + 4 * (i16 & 3);
       return cat(tr_read(img + swz(qrow, dcol)), tr_read(img + swz(qrow + 8, dcol)));
     };
+    // Q and dO fragments of the slice (A operands of every block's S' / dP' MFMAs): read once per
+    // slice -- re-read per block, each MFMA waited a full LDS latency on its own fragment (the
+    // compiler cannot reuse LDS reads across the block's dS^T stores)
+    bf16x8 qfr[4], ofr[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qfr[s] = *reinterpret_cast<const bf16x8*>(Q + swz(kl, 16 * s + 8 * hh));
+      ofr[s] = *reinterpret_cast<const bf16x8*>(O + swz(kl, 16 * s + 8 * hh));
+    }
 #pragma unroll
     for (int kb = 0; kb <= KB; ++kb) {
       __builtin_amdgcn_sched_barrier(0);
+      if (kb == KB && t + 1 < NS) load_slice(t + 1, nx, tid_t);
       const int kbase = wave * KPW + 32 * kb;  // uniform
       const bool after = qb > kbase, before = qb < kbase;
       f32x16 sa, pa;
@@ -1571,16 +1574,24 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) sa[4 * g4 + e] = l4[e];
         }
-        pa = negd;
+        // -delta of the slice's rows (the dP' initial accumulator), re-read per block beside the
+        // S' row constants rather than held in 16 registers across the block loop
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(RC + 96 + 8 * g4 + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pa[4 * g4 + e] = d4[e];
+        }
+        // kbase is a multiple of 32, so swz(kbase + kl, c) = kbase*D + swz(kl, c): written this
+        // way the block offset folds into the ds_read immediate instead of costing a register
+        bf16x8 kr[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          kr[s] = *reinterpret_cast<const bf16x8*>(Kw + kb * 32 * D + swz(kl, 16 * s + 8 * hh));
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          // kbase is a multiple of 32, so swz(kbase + kl, c) = kbase*D + swz(kl, c): written this
-          // way the block offset folds into the ds_read immediate instead of costing a register
-          const bf16x8 kr = *reinterpret_cast<const bf16x8*>(Kw + kb * 32 * D + swz(kl, 16 * s + 8 * hh));
-          const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + swz(kl, 16 * s + 8 * hh));
-          const bf16x8 oa = *reinterpret_cast<const bf16x8*>(O + swz(kl, 16 * s + 8 * hh));
-          sa = mfma(qa, kr, sa);         // (S - LSE2 -+ slope2 q) / c   [q][key]
-          pa = mfma(oa, vf[kb][s], pa);  // dP - delta
+          pa = mfma(ofr[s], vf[kb][s], pa);  // dP - delta
+          sa = mfma(qfr[s], kr[s], sa);      // (S - LSE2 -+ slope2 q) / c   [q][key]
         }
         const float kbias = ((padm_t >> kb) & 1) ? PAD_BIAS * LOG2E : 0.f;
         U = (after || before) ? fmaf(after ? slope2 : -slope2, (float)(kbase + kl_t), kbias) : kbias;

@@ -10,6 +10,8 @@
 #        bench, FETCH_SIZE / WRITE_SIZE passes -> profiles/ROUND/traffic.json, the
 #        rocprof-vs-HIP-event agreement table, then the default bench line
 #   bash scripts/gpu.sh ab-env VAR "v1 v2 ..." [REPS]  interleaved bench A/B of an env switch
+#   bash scripts/gpu.sh ab-lib "main base ..." [REPS] [STEPS]  interleaved bench A/B of library
+#        builds (scripts/build_variant.sh REV NAME -> dna_amd/lib/libdna_amd_NAME.so)
 #   bash scripts/gpu.sh stats OUT -- CMD...           rocprofv3 --kernel-trace --stats of CMD
 #   bash scripts/gpu.sh pmc OUT [KERNEL_RE] -- CMD... SQ counter sets + FETCH_SIZE + WRITE_SIZE,
 #        one rocprofv3 --pmc pass each (kernel-trace only, never combined with other traces),
@@ -69,6 +71,21 @@ ab-env)
       env $VAR=$v timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline \
         --no-b64 --no-data-pipeline > gpurun_out/ab.json 2> gpurun_out/ab.err
       echo "$VAR=$v $(python -c "import json;d=json.load(open('gpurun_out/ab.json'));print(d['value'], d['ms_per_step'], {k: round(v['avg_ms'],3) for k,v in d['kernels'].items()})")"
+    done
+  done | tee gpurun_out/ab.log
+  ;;
+ab-lib)
+  # interleaved bench A/B of library builds (scripts/build_variant.sh): LIBS = "main base ..."
+  # names libdna_amd.so ("main") or dna_amd/lib/libdna_amd_<name>.so
+  LIBS=${1:?libs}
+  REPS=${2:-2}
+  STEPS=${3:-20}
+  for rep in $(seq $REPS); do
+    for l in $LIBS; do
+      if [ "$l" = main ]; then f=$ROOT/dna_amd/lib/libdna_amd.so; else f=$ROOT/dna_amd/lib/libdna_amd_$l.so; fi
+      DNA_AMD_LIB=$f timeout -k 10 300 python bench.py --steps $STEPS --warmup 5 --no-cpu-baseline \
+        --no-b64 --no-data-pipeline > gpurun_out/ab.json 2> gpurun_out/ab.err
+      echo "$l $(python -c "import json;d=json.load(open('gpurun_out/ab.json'));print(d['value'], d['ms_per_step'], {k: round(v['avg_ms'],3) for k,v in d['kernels'].items()})")"
     done
   done | tee gpurun_out/ab.log
   ;;
