@@ -1606,19 +1606,25 @@ __global__ __launch_bounds__(256, 1) void bwd3_bf16_kernel(
       }
       __builtin_amdgcn_sched_barrier(0);
       bf16x8 pb[2], sb[2];
-      bf16x8 ao, aq;
+      // dO^T / Q^T operands of the dV / dK MFMAs, two pairs in flight (even / odd pair slots):
+      // pair j + 2's transposed reads are issued as soon as pair j's MFMAs have taken their
+      // operands, so each read has a whole pair of MFMAs and score work to land
+      bf16x8 ao[2], aq[2];
       float ssum = 0.f;
       const float sold = (DBL && kb < KB) ? sigl[hh * S + kbase + kl_t] : 0.f;
-      if (kb > 0) { ao = tr_pair(O, 0); aq = tr_pair(Q, 0); }
+      if (kb > 0) {
+        ao[0] = tr_pair(O, 0); aq[0] = tr_pair(Q, 0);
+        ao[1] = tr_pair(O, 1); aq[1] = tr_pair(Q, 1);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         if (kb > 0) {  // dV/dK MFMA i of block kb-1: pair j = i >> 1 = (s2, dt), dV then dK
           const int j = i >> 1;
           if ((i & 1) == 0) {
-            mfma_acc(dv[kb - 1][j & 1], ao, pbp[j >> 1]);
+            mfma_acc(dv[kb - 1][j & 1], ao[j & 1], pbp[j >> 1]);
           } else {
-            mfma_acc(dk[kb - 1][j & 1], aq, sbp[j >> 1]);
-            if (j < 3) { ao = tr_pair(O, j + 1); aq = tr_pair(Q, j + 1); }
+            mfma_acc(dk[kb - 1][j & 1], aq[j & 1], sbp[j >> 1]);
+            if (j < 2) { ao[j & 1] = tr_pair(O, j + 2); aq[j & 1] = tr_pair(Q, j + 2); }
           }
         }
         if (kb < KB) {  // scores 2i, 2i+1 of block kb
