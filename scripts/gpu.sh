@@ -89,6 +89,25 @@ ab-lib)
     done
   done | tee gpurun_out/ab.log
   ;;
+fftpmc)
+  # config-D FFT long conv: rocprofv3 --stats + separate FETCH_SIZE / WRITE_SIZE passes of
+  # scripts/fftconv_bench.py, per-kernel traffic table (scripts/fft_traffic.py) -> $OUT/traffic.md
+  OUT=$ROOT/gpurun_out/${1:?out}
+  shift
+  mkdir -p $OUT
+  cd /tmp && export TMPDIR=/tmp
+  ARGS="--B 2 --D 256 --L 65536 --dtype bf16 --bidirectional 1 --iters 5"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
+    python $ROOT/scripts/fftconv_bench.py $ARGS > $OUT/bench.txt 2>&1
+  for c in FETCH_SIZE WRITE_SIZE; do
+    d=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
+    timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/$d -o run -- \
+      python $ROOT/scripts/fftconv_bench.py $ARGS > $OUT/$d.log 2>&1
+  done
+  python $ROOT/scripts/fft_traffic.py $OUT/fetch $OUT/write $OUT/stats/run_kernel_stats.csv > $OUT/traffic.md
+  cat $OUT/bench.txt $OUT/traffic.md
+  rm -rf $OUT/fetch $OUT/write
+  ;;
 stats)
   OUT=$ROOT/gpurun_out/${1:?out}
   shift
