@@ -91,6 +91,48 @@ template <bool INV> __device__ __forceinline__ void dft8(cf* x) {
     x[k + 4] = csub(e[k], o[k]);
   }
 }
+// x * W_16^m (forward: exp(-2 pi i m / 16); INV: conjugate), m in 1..9
+template <bool INV, int m> __device__ __forceinline__ cf mul_w16(cf a) {
+  constexpr float c1 = 0.92387953251128674f, s1 = 0.38268343236508977f;
+  if constexpr (m == 2) return mul_w8<INV>(a);
+  else if constexpr (m == 4) return mul_w4<INV>(a);
+  else if constexpr (m == 6) return mul_w4<INV>(mul_w8<INV>(a));
+  else {
+    // W_16^1 = (c1, -s1), W_16^3 = (s1, -c1), W_16^9 = (-c1, s1)
+    constexpr float wr = m == 1 ? c1 : m == 3 ? s1 : -c1;
+    constexpr float wi0 = m == 1 ? -s1 : m == 3 ? -c1 : s1;
+    const float wi = INV ? -wi0 : wi0;
+    return make_float2(a.x * wr - a.y * wi, a.x * wi + a.y * wr);
+  }
+}
+// 16-point DFT in registers, natural order in and out: radix 4 x 4, n = na + 4 nb,
+// k = ka + 4 kb: X[ka + 4 kb] = sum_na W_4^(na kb) W_16^(na ka) DFT4_nb(x[na + 4 nb])[ka]
+template <bool INV> __device__ __forceinline__ void dft16(cf* x) {
+  cf a[4][4];
+#pragma unroll
+  for (int na = 0; na < 4; ++na) {
+    cf t[4] = {x[na], x[na + 4], x[na + 8], x[na + 12]};
+    dft4<INV>(t);
+#pragma unroll
+    for (int ka = 0; ka < 4; ++ka) a[na][ka] = t[ka];
+  }
+  a[1][1] = mul_w16<INV, 1>(a[1][1]);
+  a[1][2] = mul_w16<INV, 2>(a[1][2]);
+  a[1][3] = mul_w16<INV, 3>(a[1][3]);
+  a[2][1] = mul_w16<INV, 2>(a[2][1]);
+  a[2][2] = mul_w16<INV, 4>(a[2][2]);
+  a[2][3] = mul_w16<INV, 6>(a[2][3]);
+  a[3][1] = mul_w16<INV, 3>(a[3][1]);
+  a[3][2] = mul_w16<INV, 6>(a[3][2]);
+  a[3][3] = mul_w16<INV, 9>(a[3][3]);
+#pragma unroll
+  for (int ka = 0; ka < 4; ++ka) {
+    cf t[4] = {a[0][ka], a[1][ka], a[2][ka], a[3][ka]};
+    dft4<INV>(t);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) x[ka + 4 * kb] = t[kb];
+  }
+}
 template <int R, bool INV> __device__ __forceinline__ void dft(cf* x) {
   if constexpr (R == 8) dft8<INV>(x);
   else if constexpr (R == 4) dft4<INV>(x);
@@ -204,6 +246,19 @@ __host__ __device__ __forceinline__ int big_twiddle_elems(int logN) {
   return (1 << (logN >> 1)) + (1 << (logN - (logN >> 1)));
 }
 
+// W_N^(n2 (a + 16 b)), b = 4 q + r < 16, as tq[q] * sr[r]: tq[q] = W_N^(n2 (a + 64 q)) and
+// sr[r] = W_N^(16 n2 r) are exact table values (7 lookups), so every twiddle of the radix-16
+// column passes is at most two roundings from exact (a 15-step recurrence lost ~1e-6 relative,
+// which the 8-layer config-D model amplified past its logits tolerance)
+__device__ __forceinline__ void big16(const BigTwiddle& bt, uint32_t n2, uint32_t a, uint32_t mask,
+                                      cf (&tq)[4], cf (&sr)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tq[q] = bt((n2 * (a + 64u * q)) & mask);
+  sr[0] = make_float2(1.f, 0.f);
+#pragma unroll
+  for (int r = 1; r < 4; ++r) sr[r] = bt((n2 * 16u * r) & mask);
+}
+
 template <typename T> __device__ __forceinline__ float ld(const T* p, size_t i) { return to_f32(p[i]); }
 
 // Row pairing: pair p (channel-major so consecutive pairs share a filter) of a [B][D][L] tensor.
@@ -315,9 +370,45 @@ __global__ FFT_BOUNDS void col_fwd_kernel(const T* __restrict__ x, Pairing pr, G
     }
   }
   __syncthreads();
+  const uint32_t mask = (1u << g.logN) - 1;
+  if constexpr (LN == 17) {
+    // N = 2^17: the 256-point column FFT as two register radix-16 steps (one LDS exchange
+    // instead of three Stockham passes; the W_256 twiddles are wave-uniform table reads),
+    // n1 = j + 16 r, k1 = ka + 16 kb. Thread (c, j): 16 points of column c at stride 16 ->
+    // DFT16 over r, times W_256^(j ka), back to the same slots; thread (c, ka): the 16
+    // contiguous slots 16 ka + j -> DFT16 over j = X[ka + 16 kb]; times W_N^(n2 k1) by
+    // recurrence over kb; stored straight from registers (32 columns = 256-B row segments).
+    static_assert(NTH == 512 && PTS == 8192, "radix-16 column pass geometry");
+    const int c = threadIdx.x & 31, j = threadIdx.x >> 5;
+    cf* col = buf + c * S;
+    cf v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = col[j + 17 * r];  // lds_at(c, j + 16 r, S)
+    dft16<false>(v);
+#pragma unroll
+    for (int ka = 1; ka < 16; ++ka) v[ka] = cmul(v[ka], tw[(j * ka) & 255]);
+#pragma unroll
+    for (int ka = 0; ka < 16; ++ka) col[j + 17 * ka] = v[ka];
+    __syncthreads();
+    const int ka = j;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) v[jj] = col[17 * ka + jj];  // lds_at(c, jj + 16 ka, S)
+    dft16<false>(v);
+    const uint32_t n2 = (uint32_t)(n20 + c);
+    cf tq[4], sr[4];
+    big16(bt, n2, (uint32_t)ka, mask, tq, sr);
+    cf* out = ws + ((size_t)p << g.logN) + n2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kb = 4 * q + r;
+        out[(size_t)(ka + 16 * kb) * M2] = cmul(v[kb], r == 0 ? tq[q] : cmul(tq[q], sr[r]));
+      }
+    return;
+  }
   fft_lds<false>(buf, cw, g.logM1, S, tw);
   cf* out = ws + ((size_t)p << g.logN);
-  const uint32_t mask = (1u << g.logN) - 1;
   for (int e = threadIdx.x; e < cw * M1; e += NTH) {
     const int k1 = e >> lcw, c = e & (cw - 1);
     const int n2 = n20 + c;
@@ -514,6 +605,42 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
   __syncthreads();
   const cf* src = ws + ((size_t)p << g.logN);
   const uint32_t mask = (1u << g.logN) - 1;
+  if constexpr (LN == 17) {
+    // radix-16 form of the inverse 256-point column FFT (see col_fwd_kernel), k1 = ma + 16 mb,
+    // n1 = la + 16 lb: thread (c, ma) loads its 16 rows k1 of column n2 straight into registers
+    // (256-B row segments per wave), times conj W_N^(n2 k1) by recurrence, inverse DFT16 over
+    // mb, times conj W_256^(ma la), to LDS slots ma + 16 la; thread (c, la): slots 16 la + ma ->
+    // inverse DFT16 over ma = z[n1 = la + 16 lb], stored to lds_at(c, n1) for the output copy.
+    static_assert(NTH == 512 && PTS == 8192, "radix-16 column pass geometry");
+    const int c = threadIdx.x & 31, ma = threadIdx.x >> 5;
+    const uint32_t n2 = (uint32_t)(n20 + c);
+    cf* col = buf + c * S;
+    cf v[16];
+#pragma unroll
+    for (int mb = 0; mb < 16; ++mb) v[mb] = src[(size_t)(ma + 16 * mb) * M2 + n2];
+    cf tq[4], sr[4];
+    big16(bt, n2, (uint32_t)ma, mask, tq, sr);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mb = 4 * q + r;
+        v[mb] = cmul(v[mb], cconj(r == 0 ? tq[q] : cmul(tq[q], sr[r])));
+      }
+    dft16<true>(v);
+#pragma unroll
+    for (int la = 1; la < 16; ++la) v[la] = cmul(v[la], cconj(tw[(ma * la) & 255]));
+#pragma unroll
+    for (int la = 0; la < 16; ++la) col[ma + 17 * la] = v[la];  // lds_at(c, ma + 16 la, S)
+    __syncthreads();
+    const int la = ma;
+#pragma unroll
+    for (int mm = 0; mm < 16; ++mm) v[mm] = col[17 * la + mm];  // lds_at(c, mm + 16 la, S)
+    dft16<true>(v);
+    __syncthreads();
+#pragma unroll
+    for (int lb = 0; lb < 16; ++lb) col[la + 17 * lb] = v[lb];  // lds_at(c, la + 16 lb, S)
+  } else {
   {
     cf v[PPT];
 #pragma unroll
@@ -532,6 +659,8 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
   }
   __syncthreads();
   fft_lds<true>(buf, cw, g.logM1, S, tw);
+  }
+  __syncthreads();
   if (MODE == OUT_PAIR) {
     int d, ra, rb;
     pr.rows(p, d, ra, rb);
