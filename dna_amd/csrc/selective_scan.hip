@@ -111,22 +111,34 @@ __device__ __forceinline__ void combine(float Po, float So, float& P, float& S) 
   P = Po * P;
 }
 
+// One scan step as two DPP-fused VALU ops: S += S[src lane] * P, then P = P[src lane] * P.
+// Without bound_ctrl a lane whose DPP source is out of range (or whose row is masked off) is
+// not written, i.e. keeps (P, S) -- exactly the identity map, so no identity-valued movs and
+// no separate v_mov_dpp (the intrinsic form costs ~6 instructions per step, this 2 + a nop).
+// Hazards (the compiler does not look inside asm): a DPP read of a VGPR needs 2 wait states
+// after the VALU write -- the leading s_nop 1 covers the producers before the block, the
+// trailing s_nop 0 of each step the next step's DPP reads of S and P.
+#define DNA_SCAN_STEP(CTRL, RM)                                                   \
+  "v_fmac_f32_dpp %1, %1, %0 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"       \
+  "v_mul_f32_dpp %0, %0, %0 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"        \
+  "s_nop 0\n\t"
+
 // Inclusive wave scan of affine maps (P, S), earlier lanes applied first.
 __device__ __forceinline__ void scan_fwd(float& P, float& S, int /*lane*/) {
-  combine(dpp<0x111>(1.f, P), dpp<0x111>(0.f, S), P, S);  // row_shr:1
-  combine(dpp<0x112>(1.f, P), dpp<0x112>(0.f, S), P, S);  // row_shr:2
-  combine(dpp<0x114>(1.f, P), dpp<0x114>(0.f, S), P, S);  // row_shr:4
-  combine(dpp<0x118>(1.f, P), dpp<0x118>(0.f, S), P, S);  // row_shr:8
-  combine(dpp<0x142, 0xA>(1.f, P), dpp<0x142, 0xA>(0.f, S), P, S);  // row_bcast:15 -> rows 1, 3
-  combine(dpp<0x143, 0xC>(1.f, P), dpp<0x143, 0xC>(0.f, S), P, S);  // row_bcast:31 -> rows 2, 3
+  asm volatile("s_nop 1\n\t"
+               DNA_SCAN_STEP("row_shr:1", "0xf") DNA_SCAN_STEP("row_shr:2", "0xf")
+               DNA_SCAN_STEP("row_shr:4", "0xf") DNA_SCAN_STEP("row_shr:8", "0xf")
+               DNA_SCAN_STEP("row_bcast:15", "0xa")   // rows 1, 3 <- lane 15 of the row before
+               DNA_SCAN_STEP("row_bcast:31", "0xc")   // rows 2, 3 <- lane 31
+               : "+v"(P), "+v"(S));
 }
 // Inclusive suffix scan (later lanes applied first): row_shl within the 16-lane rows, then the
 // row totals (lanes 16, 32, 48) composed with readlane and applied per row.
 __device__ __forceinline__ void scan_rev(float& P, float& S, int lane) {
-  combine(dpp<0x101>(1.f, P), dpp<0x101>(0.f, S), P, S);  // row_shl:1
-  combine(dpp<0x102>(1.f, P), dpp<0x102>(0.f, S), P, S);
-  combine(dpp<0x104>(1.f, P), dpp<0x104>(0.f, S), P, S);
-  combine(dpp<0x108>(1.f, P), dpp<0x108>(0.f, S), P, S);
+  asm volatile("s_nop 1\n\t"
+               DNA_SCAN_STEP("row_shl:1", "0xf") DNA_SCAN_STEP("row_shl:2", "0xf")
+               DNA_SCAN_STEP("row_shl:4", "0xf") DNA_SCAN_STEP("row_shl:8", "0xf")
+               : "+v"(P), "+v"(S));
   const float P1 = bcast(P, 16), S1 = bcast(S, 16), P2 = bcast(P, 32), S2 = bcast(S, 32);
   const float P3 = bcast(P, 48), S3 = bcast(S, 48);
   float P23 = P2, S23 = S2;
@@ -406,6 +418,50 @@ __device__ __forceinline__ void stage(T* lds, const T* M, int c, int len) {
   }
 }
 
+// stage one [N][CHUNK] slice as fp32, items interleaved for 16-B reads: position p = lane*8 + i
+// of row n lives at n*CHUNK + (i >> 2)*256 + lane*4 + (i & 3). The per-state reads of B / C in
+// the chunk kernels are then two conflict-free ds_read_b128 per lane and no bf16 -> fp32
+// conversions (16 VALU per state and lane in chunk_bwd otherwise).
+template <typename T, int N>
+__device__ __forceinline__ void stagef(float* lds, const T* M, int c, int len) {
+  constexpr int VE = 16 / sizeof(T);  // 8 (bf16) or 4 (fp32) consecutive positions per load
+  constexpr int NV = N * CHUNK / VE;
+  for (int vi = threadIdx.x; vi < NV; vi += CT) {
+    const int e = vi * VE;
+    const int n = e / CHUNK, p = e - n * CHUNK;
+    const int gp = c * CHUNK + p;
+    const T* src = M + (size_t)n * len + gp;
+    float v[VE];
+    if (gp + VE <= len && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8 w = *reinterpret_cast<const bf16x8*>(src);
+#pragma unroll
+        for (int q = 0; q < VE; ++q) v[q] = (float)w[q];
+      } else {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+        for (int q = 0; q < VE; ++q) v[q] = w[q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < VE; ++q) v[q] = (gp + q < len) ? to_f32(src[q]) : 0.f;
+    }
+    const int ln = p >> 3, i0 = p & 7;
+    float* d = lds + n * CHUNK + ln * 4;
+#pragma unroll
+    for (int h = 0; h < VE / 4; ++h)
+      *reinterpret_cast<f32x4*>(d + ((i0 >> 2) + h) * 256) =
+          f32x4{v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]};
+  }
+}
+// a lane's 8 items of row n from a stagef image (row = lds + n*CHUNK)
+__device__ __forceinline__ void lds8f(const float* row, int lane, float (&v)[ITEMS]) {
+  const f32x4 x = *reinterpret_cast<const f32x4*>(row + lane * 4);
+  const f32x4 y = *reinterpret_cast<const f32x4*>(row + 256 + lane * 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[i] = x[i]; v[i + 4] = y[i]; }
+}
+
 template <typename T>
 __device__ __forceinline__ void lds8(const T* p, float (&v)[ITEMS]) {
   if constexpr (sizeof(T) == 2) {
@@ -440,13 +496,13 @@ __device__ __forceinline__ void delta_sums(float tl, int lane, float& pre, float
 
 template <typename T, int N>
 __global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
-  __shared__ __attribute__((aligned(16))) T Bs[N * CHUNK];
+  __shared__ __attribute__((aligned(16))) float Bs[N * CHUNK];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
   float* Sbuf = a.states;
   float* dsum = a.states + 2 * (size_t)a.batch * a.dim * nchN;
-  stage<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
+  stagef<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
   __syncthreads();
   const int pos = c * CHUNK + lane * ITEMS;
   for (int j = 0; j < q.k; ++j) {
@@ -467,7 +523,7 @@ __global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
 #pragma unroll 4
     for (int n = 0; n < N; ++n) {
       float Bv[ITEMS];
-      lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
+      lds8f(Bs + n * CHUNK, lane, Bv);
       const float An = bcast(Al, n), An2 = An * LOG2E;
       float x = 0.f;
 #pragma unroll
@@ -482,12 +538,12 @@ __global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
 
 template <typename T, int N>
 __global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
-  __shared__ __attribute__((aligned(16))) T Cs[N * CHUNK];
+  __shared__ __attribute__((aligned(16))) float Cs[N * CHUNK];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
   float* Rbuf = a.states + (size_t)a.batch * a.dim * nchN;
-  stage<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
+  stagef<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
   __syncthreads();
   const int pos = c * CHUNK + lane * ITEMS;
   for (int j = 0; j < q.k; ++j) {
@@ -514,7 +570,7 @@ __global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
 #pragma unroll 4
     for (int n = 0; n < N; ++n) {
       float Cv[ITEMS];
-      lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
+      lds8f(Cs + n * CHUNK, lane, Cv);
       const float An = bcast(Al, n), An2 = An * LOG2E;
       float r = 0.f;
 #pragma unroll
@@ -572,13 +628,13 @@ __global__ __launch_bounds__(64) void carry_par_kernel(Args a, Chunked q, int re
 
 template <typename T, int N>
 __global__ __launch_bounds__(CT) void chunk_fwd_kernel(Args a, Chunked q) {
-  __shared__ __attribute__((aligned(16))) T Bs[N * CHUNK];
-  __shared__ __attribute__((aligned(16))) T Cs[N * CHUNK];
+  __shared__ __attribute__((aligned(16))) float Bs[N * CHUNK];
+  __shared__ __attribute__((aligned(16))) float Cs[N * CHUNK];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
-  stage<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
-  stage<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
+  stagef<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
+  stagef<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
   __syncthreads();
   const int pos = c * CHUNK + lane * ITEMS;
   for (int j = 0; j < q.k; ++j) {
@@ -599,8 +655,8 @@ __global__ __launch_bounds__(CT) void chunk_fwd_kernel(Args a, Chunked q) {
 #pragma unroll 2
     for (int n = 0; n < N; ++n) {
       float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS];
-      lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
-      lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
+      lds8f(Bs + n * CHUNK, lane, Bv);
+      lds8f(Cs + n * CHUNK, lane, Cv);
       const float An = bcast(Al, n), An2 = An * LOG2E;
       float P = ex2(tl * An2), S = 0.f;  // prod_i exp(dl_i A) = exp(A sum_i dl_i)
 #pragma unroll
@@ -642,16 +698,16 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
   // accumulator slot has one writer at a time and is updated with a plain read-modify-write.
   constexpr int R = CW > N ? CW / N : 1;
   float* acc = reinterpret_cast<float*>(smem);
-  T* Bs = reinterpret_cast<T*>(acc + R * 2 * N * CHUNK);   // [N][CHUNK]
-  T* Cs = Bs + N * CHUNK;
+  float* Bs = acc + R * 2 * N * CHUNK;   // [N][CHUNK] fp32 (stagef layout)
+  float* Cs = Bs + N * CHUNK;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
   const float* hbuf = a.states + (size_t)a.batch * a.dim * nchN;
   for (int e = threadIdx.x; e < R * 2 * N * CHUNK; e += CT) acc[e] = 0.f;
   float* accw = acc + (w / N) * 2 * N * CHUNK;
-  stage<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
-  stage<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
+  stagef<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
+  stagef<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
   __syncthreads();
   const int pos = c * CHUNK + lane * ITEMS;
   for (int j = 0; j < q.k; ++j) {
@@ -690,8 +746,8 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
     // current step)
     auto state = [&](const int n) __attribute__((always_inline)) {
       float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
-      lds8(Bs + n * CHUNK + lane * ITEMS, Bv);
-      lds8(Cs + n * CHUNK + lane * ITEMS, Cv);
+      lds8f(Bs + n * CHUNK, lane, Bv);
+      lds8f(Cs + n * CHUNK, lane, Cv);
       const float An = bcast(Al, n), An2 = An * LOG2E;
       const float Pt = ex2(tl * An2);  // prod_i a_i, for both directions
       float P = Pt, S = 0.f;
@@ -891,7 +947,7 @@ extern "C" int dna_selective_scan_bwd(const void* u, const void* delta, const fl
     constexpr int NS = decltype(n)::value;
     if (chunked) {
       constexpr int R = CW > NS ? CW / NS : 1;
-      const size_t bytes = (size_t)2 * NS * CHUNK * (R * sizeof(float) + sizeof(T));
+      const size_t bytes = (size_t)2 * NS * CHUNK * (R + 1) * sizeof(float);
       allow_lds(chunk_bwd_kernel<T, NS>, bytes);
       hipLaunchKernelGGL((sum_bwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
       hipLaunchKernelGGL((carry_par_kernel<NS>), dim3(batch * dim * NS), dim3(64), 0, s, a, q, 1);
