@@ -65,11 +65,78 @@ __device__ __forceinline__ void load8<float>(const float* p, int pos, int len, f
     for (int i = 0; i < ITEMS; ++i) v[i] = (pos + i < len) ? p[pos + i] : 0.f;
   }
 }
+// a lane's 8 positions held raw (bf16: 4 VGPRs) between a prefetch and its use
+template <typename T> struct Raw8;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+// one channel row as a raw buffer resource: loads past `len` read 0 and stores past it are
+// dropped by the hardware range check, so the vector path needs no per-lane branch (a branch
+// around a load makes the compiler wait for it at the join, which defeats a prefetch)
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const T* row, int len) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(row), (short)0, len * (int)sizeof(T),
+                                           0x00020000);
+}
+template <> struct Raw8<bf16> {
+  bf16x8 w;
+  // VEC rows: len % 8 == 0 and a 16-B aligned row base (host-checked)
+  __device__ __forceinline__ void loadv(const bf16* row, int pos, int len) {
+    w = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(row, len),
+                                                                         pos * 2, 0, 0));
+  }
+  __device__ __forceinline__ void load(const bf16* p, int pos, int len) {
+    if (pos + ITEMS <= len && (reinterpret_cast<uintptr_t>(p + pos) & 15) == 0) {
+      w = *reinterpret_cast<const bf16x8*>(p + pos);
+    } else {
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) w[i] = (pos + i < len) ? p[pos + i] : (bf16)0.f;
+    }
+  }
+  __device__ __forceinline__ void get(float (&v)[ITEMS]) const {
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) v[i] = (float)w[i];
+  }
+};
+template <> struct Raw8<float> {
+  float w[ITEMS];
+  __device__ __forceinline__ void loadv(const float* row, int pos, int len) {
+    const auto r = row_rsrc(row, len);
+    const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, pos * 4, 0, 0));
+    const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, pos * 4 + 16, 0, 0));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { w[i] = a[i]; w[i + 4] = b[i]; }
+  }
+  __device__ __forceinline__ void load(const float* p, int pos, int len) { load8(p, pos, len, w); }
+  __device__ __forceinline__ void get(float (&v)[ITEMS]) const {
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) v[i] = w[i];
+  }
+};
+
 template <typename T>
 __device__ __forceinline__ void store8(T* p, int pos, int len, const float (&v)[ITEMS]) {
 #pragma unroll
   for (int i = 0; i < ITEMS; ++i)
     if (pos + i < len) p[pos + i] = from_f32<T>(v[i]);
+}
+// store8 on a VEC row (see Raw8::loadv): 16-B buffer stores, lanes past `len` dropped
+template <typename T>
+__device__ __forceinline__ void store8v(T* row, int pos, int len, const float (&v)[ITEMS]) {
+  const auto r = row_rsrc(row, len);
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 h;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) h[i] = (bf16)v[i];
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), r, pos * 2, 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}),
+                                           r, pos * 4, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[4], v[5], v[6], v[7]}),
+                                           r, pos * 4 + 16, 0, 0);
+  }
+}
+template <bool VEC, typename T>
+__device__ __forceinline__ void store8x(T* row, int pos, int len, const float (&v)[ITEMS]) {
+  if constexpr (VEC) store8v(row, pos, len, v); else store8(row, pos, len, v);
 }
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -81,8 +148,10 @@ __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x)
 // chunk kernels.
 __device__ __forceinline__ float softplus(float x) {
   const float y = ex2(-fabsf(x) * LOG2E);
-  const float s = y < 1e-2f ? y * (1.f - y * (0.5f - y * (1.f / 3.f - 0.25f * y))) : __logf(1.f + y);
-  return fmaxf(x, 0.f) + s;
+  // both branches computed and selected (a per-lane branch here became 8 divergent blocks)
+  const float sp = y * (1.f - y * (0.5f - y * (1.f / 3.f - 0.25f * y)));
+  const float sl = __builtin_amdgcn_logf(1.f + y) * 0.6931471805599453f;
+  return fmaxf(x, 0.f) + (y < 1e-2f ? sp : sl);
 }
 __device__ __forceinline__ float sigmoidf(float x) {
   return __builtin_amdgcn_rcpf(1.f + ex2(-x * LOG2E));
@@ -132,13 +201,8 @@ __device__ __forceinline__ void scan_fwd(float& P, float& S, int /*lane*/) {
                DNA_SCAN_STEP("row_bcast:31", "0xc")   // rows 2, 3 <- lane 31
                : "+v"(P), "+v"(S));
 }
-// Inclusive suffix scan (later lanes applied first): row_shl within the 16-lane rows, then the
-// row totals (lanes 16, 32, 48) composed with readlane and applied per row.
-__device__ __forceinline__ void scan_rev(float& P, float& S, int lane) {
-  asm volatile("s_nop 1\n\t"
-               DNA_SCAN_STEP("row_shl:1", "0xf") DNA_SCAN_STEP("row_shl:2", "0xf")
-               DNA_SCAN_STEP("row_shl:4", "0xf") DNA_SCAN_STEP("row_shl:8", "0xf")
-               : "+v"(P), "+v"(S));
+// row totals of a row_shl suffix scan (lanes 16, 32, 48) composed with readlane, applied per row
+__device__ __forceinline__ void rev_rows(float& P, float& S, int lane) {
   const float P1 = bcast(P, 16), S1 = bcast(S, 16), P2 = bcast(P, 32), S2 = bcast(S, 32);
   const float P3 = bcast(P, 48), S3 = bcast(S, 48);
   float P23 = P2, S23 = S2;
@@ -149,6 +213,31 @@ __device__ __forceinline__ void scan_rev(float& P, float& S, int lane) {
   const float Po = row == 0 ? P13 : row == 1 ? P23 : row == 2 ? P3 : 1.f;
   const float So = row == 0 ? S13 : row == 1 ? S23 : row == 2 ? S3 : 0.f;
   combine(Po, So, P, S);
+}
+// Inclusive suffix scan (later lanes applied first): row_shl within the 16-lane rows, then the
+// row totals.
+__device__ __forceinline__ void scan_rev(float& P, float& S, int lane) {
+  asm volatile("s_nop 1\n\t"
+               DNA_SCAN_STEP("row_shl:1", "0xf") DNA_SCAN_STEP("row_shl:2", "0xf")
+               DNA_SCAN_STEP("row_shl:4", "0xf") DNA_SCAN_STEP("row_shl:8", "0xf")
+               : "+v"(P), "+v"(S));
+  rev_rows(P, S, lane);
+}
+// scan_fwd of (P, S) and scan_rev of (Pr, Sr) together: the two chains' in-row steps alternate,
+// so each DPP read is 3 instructions after its producer and the in-row part needs no s_nop.
+#define DNA_SCAN_PAIR(F, R)                                                        \
+  "v_fmac_f32_dpp %1, %1, %0 " F " row_mask:0xf bank_mask:0xf\n\t"              \
+  "v_mul_f32_dpp %0, %0, %0 " F " row_mask:0xf bank_mask:0xf\n\t"               \
+  "v_fmac_f32_dpp %3, %3, %2 " R " row_mask:0xf bank_mask:0xf\n\t"              \
+  "v_mul_f32_dpp %2, %2, %2 " R " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void scan_both(float& P, float& S, float& Pr, float& Sr, int lane) {
+  asm volatile("s_nop 1\n\t"
+               DNA_SCAN_PAIR("row_shr:1", "row_shl:1") DNA_SCAN_PAIR("row_shr:2", "row_shl:2")
+               DNA_SCAN_PAIR("row_shr:4", "row_shl:4") DNA_SCAN_PAIR("row_shr:8", "row_shl:8")
+               "s_nop 0\n\t"
+               DNA_SCAN_STEP("row_bcast:15", "0xa") DNA_SCAN_STEP("row_bcast:31", "0xc")
+               : "+v"(P), "+v"(S), "+v"(Pr), "+v"(Sr));
+  rev_rows(Pr, Sr, lane);
 }
 // inclusive prefix sum over the wave
 __device__ __forceinline__ float prefix_sum(float v) {
@@ -164,11 +253,12 @@ __device__ __forceinline__ float wsum(float v) { return bcast(prefix_sum(v), 63)
 
 // delta after bias + softplus for one lane's 8 positions (invalid positions -> 0: identity map)
 __device__ __forceinline__ void prep_delta(float (&dl)[ITEMS], float bias, int sp, int pos, int len) {
+  if (sp) {  // one uniform branch, not one per position
 #pragma unroll
-  for (int i = 0; i < ITEMS; ++i) {
-    float v = dl[i] + bias;
-    if (sp) v = softplus(v);
-    dl[i] = (pos + i < len) ? v : 0.f;
+    for (int i = 0; i < ITEMS; ++i) dl[i] = (pos + i < len) ? softplus(dl[i] + bias) : 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) dl[i] = (pos + i < len) ? dl[i] + bias : 0.f;
   }
 }
 
@@ -688,7 +778,7 @@ __global__ __launch_bounds__(CT) void chunk_fwd_kernel(Args a, Chunked q) {
   }
 }
 
-template <typename T, int N>
+template <typename T, int N, bool VEC>
 __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // dB/dC partials of the group: [R copies][2 (dB, dC)][N][ITEMS][64] fp32; position
@@ -700,7 +790,9 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
   float* acc = reinterpret_cast<float*>(smem);
   float* Bs = acc + R * 2 * N * CHUNK;   // [N][CHUNK] fp32 (stagef layout)
   float* Cs = Bs + N * CHUNK;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // w through readfirstlane: the channel row pointers are then SGPRs (a buffer resource built
+  // from a VGPR becomes a readfirstlane waterfall loop around every load)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
   const float* hbuf = a.states + (size_t)a.batch * a.dim * nchN;
@@ -710,36 +802,76 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
   stagef<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
   __syncthreads();
   const int pos = c * CHUNK + lane * ITEMS;
+  // The next channel's inputs are fetched while this channel's states run: the barriers keep
+  // the block's waves in step, so an unprefetched channel prologue idles every SIMD for a full
+  // HBM round trip q.k times per block.
+  struct Fetch {
+    Raw8<T> u, dr, go, z;
+    float Al, xcl, hcl, Dd, bias;
+  };
+  // VEC: every load unconditional (clamped lane index, z -> u when absent): a load under a
+  // branch is waited for at the join
+  auto fetch = [&](Fetch& f, int j) __attribute__((always_inline)) {
+    const int d = blockIdx.x * CW * q.k + j * CW + w;
+    const int ch = b * a.dim + d;
+    const size_t off = (size_t)ch * a.len;
+    if constexpr (VEC) {
+      const int ln = lane & (N - 1);
+      const float Al = a.A[d * N + ln];
+      const float xc = a.states[(size_t)ch * nchN + (size_t)c * N + ln];
+      const float hc = hbuf[(size_t)ch * nchN + (size_t)c * N + ln];
+      f.Al = lane < N ? Al : 0.f;
+      f.xcl = lane < N ? xc : 0.f;
+      f.hcl = lane < N ? hc : 0.f;
+    } else {
+      f.Al = lane < N ? a.A[d * N + lane] : 0.f;
+      f.xcl = lane < N ? a.states[(size_t)ch * nchN + (size_t)c * N + lane] : 0.f;
+      f.hcl = lane < N ? hbuf[(size_t)ch * nchN + (size_t)c * N + lane] : 0.f;
+    }
+    f.Dd = a.D ? a.D[d] : 0.f;
+    f.bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    if constexpr (VEC) {
+      f.u.loadv((const T*)a.u + off, pos, a.len);
+      f.dr.loadv((const T*)a.delta + off, pos, a.len);
+      f.go.loadv((const T*)a.dout + off, pos, a.len);
+      f.z.loadv((const T*)(a.z ? a.z : a.u) + off, pos, a.len);
+    } else {
+      f.u.load((const T*)a.u + off, pos, a.len);
+      f.dr.load((const T*)a.delta + off, pos, a.len);
+      f.go.load((const T*)a.dout + off, pos, a.len);
+      if (a.z) f.z.load((const T*)a.z + off, pos, a.len);
+    }
+  };
+  Fetch nx;
+  fetch(nx, 0);
   for (int j = 0; j < q.k; ++j) {
     const int d = blockIdx.x * CW * q.k + j * CW + w;
     const int ch = b * a.dim + d;
     const size_t off = (size_t)ch * a.len;
-    const float Al = lane < N ? a.A[d * N + lane] : 0.f;
-    const float Dd = a.D ? a.D[d] : 0.f;
-    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
-    const float xcl = lane < N ? a.states[(size_t)ch * nchN + (size_t)c * N + lane] : 0.f;
-    const float hcl = lane < N ? hbuf[(size_t)ch * nchN + (size_t)c * N + lane] : 0.f;
+    const float Al = nx.Al, Dd = nx.Dd, bias = nx.bias, xcl = nx.xcl, hcl = nx.hcl;
     float uu[ITEMS], dr[ITEMS], dl[ITEMS], go[ITEMS], dy[ITEMS];
-    load8((const T*)a.u + off, pos, a.len, uu);
-    load8((const T*)a.delta + off, pos, a.len, dr);
-    load8((const T*)a.dout + off, pos, a.len, go);
+    nx.u.get(uu);
+    nx.dr.get(dr);
+    nx.go.get(go);
+    float zz[ITEMS];
+    if (a.z) nx.z.get(zz);
+    if constexpr (VEC) fetch(nx, j + 1 < q.k ? j + 1 : j);  // the last one refetches: no branch
+    else if (j + 1 < q.k) fetch(nx, j + 1);
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) dl[i] = dr[i];
     prep_delta(dl, bias, a.softplus, pos, a.len);
-    float zz[ITEMS];
     if (a.z) {
-      load8((const T*)a.z + off, pos, a.len, zz);
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) dy[i] = go[i] * siluf(zz[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) dy[i] = go[i];
     }
-    float ddl[ITEMS], du[ITEMS], y[ITEMS], dlu[ITEMS];
+    float ddl[ITEMS], gB[ITEMS], y[ITEMS], dlu[ITEMS];
     float dDacc = 0.f, dAl = 0.f, tl = 0.f;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      ddl[i] = 0.f; du[i] = Dd * dy[i]; y[i] = 0.f; dDacc = fmaf(dy[i], uu[i], dDacc);
+      ddl[i] = 0.f; gB[i] = 0.f; y[i] = 0.f; dDacc = fmaf(dy[i], uu[i], dDacc);
       dlu[i] = dl[i] * uu[i]; tl += dl[i];
     }
     // one state's share of the backward (its dB / dC accumulator row is this wave's alone in the
@@ -748,6 +880,14 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
       float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
       lds8f(Bs + n * CHUNK, lane, Bv);
       lds8f(Cs + n * CHUNK, lane, Cv);
+      // the state's dB / dC accumulator rows, read up front so the LDS round trips overlap the
+      // scans instead of serialising read -> fma -> write at the end (occupancy is LDS-bound at
+      // 2 waves / SIMD, so the 16 extra VGPRs are free)
+      float* aB = accw + n * CHUNK + lane;
+      float* aC = aB + N * CHUNK;
+      float rB[ITEMS], rC[ITEMS];
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) { rB[i] = aB[i * 64]; rC[i] = aC[i * 64]; }
       const float An = bcast(Al, n), An2 = An * LOG2E;
       const float Pt = ex2(tl * An2);  // prod_i a_i, for both directions
       float P = Pt, S = 0.f;
@@ -757,7 +897,10 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
         bb[i] = dlu[i] * Bv[i];
         S = fmaf(aa[i], S, bb[i]);
       }
-      scan_fwd(P, S, lane);
+      float Pr = Pt, Sr = 0.f;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) Sr = aa[i] * fmaf(Cv[i], dy[i], Sr);
+      scan_both(P, S, Pr, Sr, lane);
       const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
       const float xprev = fmaf(Pe, bcast(xcl, n), Se);
       float x = xprev;
@@ -767,15 +910,9 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
         xs[i] = x;
         y[i] = fmaf(Cv[i], x, y[i]);
       }
-      float Pr = Pt, Sr = 0.f;
-#pragma unroll
-      for (int i = ITEMS - 1; i >= 0; --i) Sr = aa[i] * fmaf(Cv[i], dy[i], Sr);
-      scan_rev(Pr, Sr, lane);
       const float Pn = shl1(Pr, 1.f), Sn = shl1(Sr, 0.f);
       float h = fmaf(Pn, bcast(hcl, n), Sn);
       float dAn = 0.f;
-      float* aB = accw + n * CHUNK + lane;
-      float* aC = aB + N * CHUNK;
 #pragma unroll
       for (int i = ITEMS - 1; i >= 0; --i) {
         const float g = fmaf(Cv[i], dy[i], h);
@@ -783,13 +920,13 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
         const float da = g * xm1 * aa[i];
         ddl[i] = fmaf(da, An, ddl[i]);
         dAn = fmaf(da, dl[i], dAn);
-        const float gb = g * dl[i];
-        ddl[i] = fmaf(g, Bv[i] * uu[i], ddl[i]);
-        du[i] = fmaf(gb, Bv[i], du[i]);
-        aB[i * 64] += gb * uu[i];   // exclusive this step (see the state rotation above)
-        aC[i * 64] += dy[i] * xs[i];
+        gB[i] = fmaf(g, Bv[i], gB[i]);   // d/dδ and d/du through B: g B (u resp. δ) after the loop
+        rB[i] = fmaf(g, dlu[i], rB[i]);   // rows exclusive this step (state rotation above)
+        rC[i] = fmaf(dy[i], xs[i], rC[i]);
         h = aa[i] * g;
       }
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) { aB[i * 64] = rB[i]; aC[i * 64] = rC[i]; }
       const float dAs = wsum(dAn);
       if (lane == n) dAl = dAs;
     };
@@ -810,16 +947,17 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
         __syncthreads();
       }
     }
-    float dd[ITEMS], dbacc = 0.f;
+    float dd[ITEMS], du[ITEMS], dbacc = 0.f;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      float g = ddl[i];
+      du[i] = fmaf(gB[i], dl[i], Dd * dy[i]);
+      float g = fmaf(gB[i], uu[i], ddl[i]);
       if (a.softplus) g *= sigmoidf(dr[i] + bias);
       dd[i] = (pos + i < a.len) ? g : 0.f;
       dbacc += dd[i];
     }
-    store8((T*)a.ddelta + off, pos, a.len, dd);
-    store8((T*)a.du + off, pos, a.len, du);
+    store8x<VEC>((T*)a.ddelta + off, pos, a.len, dd);
+    store8x<VEC>((T*)a.du + off, pos, a.len, du);
     if (a.z && a.dz) {
       float dzv[ITEMS];
 #pragma unroll
@@ -828,7 +966,7 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
         const float pre = fmaf(Dd, uu[i], y[i]);
         dzv[i] = go[i] * pre * s * (1.f + zz[i] * (1.f - s));
       }
-      store8((T*)a.dz + off, pos, a.len, dzv);
+      store8x<VEC>((T*)a.dz + off, pos, a.len, dzv);
     }
     if (lane < N) atomicAdd(a.dA + d * N + lane, dAl);
     dDacc = wsum(dDacc);
@@ -940,6 +1078,10 @@ extern "C" int dna_selective_scan_bwd(const void* u, const void* delta, const fl
   a.dD = dD; a.ddelta_bias = ddelta_bias;
   hipStream_t s = as_stream(stream);
   const bool chunked = dim % CW == 0;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  // rows of whole 16-B vectors: the chunk backward's branch-free buffer I/O
+  const bool vec = len % ITEMS == 0 && al16(u) && al16(delta) && al16(dout) && al16(du) &&
+                   al16(ddelta) && (!z || (al16(z) && al16(dz)));
   const Chunked q = plan_chunks(batch, dim, len);
   const dim3 cgrid(q.groups, q.nch, batch);
   const int st = dispatch(dtype, d_state, [&](auto t, auto n) {
@@ -948,10 +1090,15 @@ extern "C" int dna_selective_scan_bwd(const void* u, const void* delta, const fl
     if (chunked) {
       constexpr int R = CW > NS ? CW / NS : 1;
       const size_t bytes = (size_t)2 * NS * CHUNK * (R + 1) * sizeof(float);
-      allow_lds(chunk_bwd_kernel<T, NS>, bytes);
       hipLaunchKernelGGL((sum_bwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
       hipLaunchKernelGGL((carry_par_kernel<NS>), dim3(batch * dim * NS), dim3(64), 0, s, a, q, 1);
-      hipLaunchKernelGGL((chunk_bwd_kernel<T, NS>), cgrid, dim3(CT), bytes, s, a, q);
+      if (vec) {
+        allow_lds(chunk_bwd_kernel<T, NS, true>, bytes);
+        hipLaunchKernelGGL((chunk_bwd_kernel<T, NS, true>), cgrid, dim3(CT), bytes, s, a, q);
+      } else {
+        allow_lds(chunk_bwd_kernel<T, NS, false>, bytes);
+        hipLaunchKernelGGL((chunk_bwd_kernel<T, NS, false>), cgrid, dim3(CT), bytes, s, a, q);
+      }
     } else {
       hipLaunchKernelGGL((bwd_kernel<T, NS>), dim3((batch * dim + WPB - 1) / WPB), dim3(64 * WPB),
                          0, s, a);
