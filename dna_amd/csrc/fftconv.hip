@@ -718,6 +718,77 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
   }
 }
 
+// ---------------------------------------------------------------- B for the filter: row FFT +
+// separation in one pass. The separation of Z = FFT(k_{2q} + i k_{2q+1}) (below) pairs bin f
+// with N - f, which for f = k1 + M1 k2 lies in row (M1 - k1) mod M1, column M2 - 1 - k2 (k1 != 0)
+// or row 0, column (M2 - k2) mod M2 (k1 == 0). A block therefore transforms row pairs
+// {j, M1 - j} (j in [j0, j0 + rw/2); j = 0 pairs row 0 with row M1/2, both self-mirrored), so
+// every bin's mirror is in its LDS and the spectrum goes straight to kspec: no spectrum round
+// trip through HBM and no separate pass (ROW_SPEC + separate_kernel read and wrote 3 N-point
+// complex arrays per pair more).
+template <int LN>
+__global__ FFT_BOUNDS void row_sep_kernel(const cf* __restrict__ ws, const float* __restrict__ bias,
+                                          int D, int pad, Geo g_, cf* __restrict__ kspec) {
+  const Geo g = fixed<LN>(g_);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int M1 = 1 << g.logM1, M2 = 1 << g.logM2;
+  const int lrw = log_row_group(g), rw = 1 << lrw, h = rw >> 1;
+  const int S = seq_stride(g.logM2, false);
+  cf* buf = reinterpret_cast<cf*>(smem);  // [rw][S] padded
+  cf* tw = buf + rw * S;
+  const int j0 = blockIdx.x * h;
+  const int q = blockIdx.y;
+  auto row_of = [&](int slot) {
+    if (slot < h) return j0 + slot;
+    const int j = j0 + slot - h;
+    return j == 0 ? M1 / 2 : M1 - j;
+  };
+  make_table(tw, g.logM2);
+  const cf* base = ws + ((size_t)q << g.logN);
+  {
+    cf v[PPT];
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      if (e < rw * M2) v[it] = base[((size_t)row_of(e >> g.logM2) << g.logM2) + (e & (M2 - 1))];
+    }
+#pragma unroll
+    for (int it = 0; it < PPT; ++it) {
+      const int e = threadIdx.x + it * NTH;
+      if (e < rw * M2) buf[lds_at(e >> g.logM2, e & (M2 - 1), S)] = v[it];
+    }
+  }
+  __syncthreads();
+  fft_lds<false>(buf, rw, g.logM2, S, tw);
+  const int logN = g.logN;
+  const uint32_t mask = (1u << logN) - 1;
+  const float sc = 0.5f / (float)(1u << logN);
+  const float ba = bias ? bias[2 * q] / (float)(1u << logN) : 0.f;
+  const bool has_b = 2 * q + 1 < D;
+  const float bb = (bias && has_b) ? bias[2 * q + 1] / (float)(1u << logN) : 0.f;
+  cf* ka = kspec + ((size_t)(2 * q) << logN);
+  cf* kb = kspec + ((size_t)(2 * q + 1) << logN);
+  for (int e = threadIdx.x; e < rw * M2; e += NTH) {
+    const int slot = e >> g.logM2, k2 = e & (M2 - 1);
+    const int k1 = row_of(slot);
+    const int j = j0 + (slot < h ? slot : slot - h);
+    const int ms = (j == 0) ? slot : (slot < h ? slot + h : slot - h);
+    const int k2m = k1 == 0 ? ((M2 - k2) & (M2 - 1)) : (M2 - 1 - k2);
+    const cf a = buf[lds_at(slot, k2, S)], b = cconj(buf[lds_at(ms, k2m, S)]);
+    cf sh = make_float2(1.f, 0.f);
+    if (pad) {
+      const uint32_t f = (uint32_t)k1 + ((uint32_t)k2 << g.logM1);
+      sh = cconj(twiddle((f * (uint32_t)pad) & mask, logN));
+    }
+    const size_t pos = ((size_t)k1 << g.logM2) + k2;
+    ka[pos] = make_float2((a.x + b.x) * sc + ba * sh.x, (a.y + b.y) * sc + ba * sh.y);
+    if (has_b) {
+      const cf dlt = csub(a, b);  // (a - b) / (2i) = (-i/2)(a - b)
+      kb[pos] = make_float2(dlt.y * sc + bb * sh.x, -dlt.x * sc + bb * sh.y);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- filter spectrum separation
 // Z = FFT(k_{2q} + i k_{2q+1}) in [k1][k2] order -> kspec rows 2q, 2q+1 (scaled 1/N):
 //   K_a[f] = (Z[f] + conj Z[N-f]) / 2,   K_b[f] = (Z[f] - conj Z[N-f]) / (2i)
@@ -1001,10 +1072,24 @@ extern "C" int dna_fftconv_filter(const float* k, const float* bias, int D, int 
   Pairing pr{D, 1, Q};  // channels paired (2q, 2q+1)
   cf* w = (cf*)ws;
   launch_col_fwd<float>(k, pr, g, 0, w, Q, s);
-  launch_row<ROW_SPEC>(w, nullptr, pr, g, Q, s);
-  const int bx = (int)((N + 255) / 256) < 1024 ? (int)((N + 255) / 256) : 1024;
-  hipLaunchKernelGGL(separate_kernel, dim3(bx, Q), dim3(256), 0, s, (const cf*)w, bias, D,
-                     pad_before(L, bidirectional), g, (cf*)kspec);
+  const int pad = pad_before(L, bidirectional);
+  static const bool unfused = getenv("DNA_FFT_FILTER_SEPARATE") && atoi(getenv("DNA_FFT_FILTER_SEPARATE")) == 1;
+  if (unfused) {  // the unfused ROW_SPEC + separate form (A/B)
+    launch_row<ROW_SPEC>(w, nullptr, pr, g, Q, s);
+    const int bx = (int)((N + 255) / 256) < 1024 ? (int)((N + 255) / 256) : 1024;
+    hipLaunchKernelGGL(separate_kernel, dim3(bx, Q), dim3(256), 0, s, (const cf*)w, bias, D, pad,
+                       g, (cf*)kspec);
+  } else {
+#define L_(LN)                                                                                 \
+    {                                                                                          \
+      auto kk = row_sep_kernel<LN>;                                                            \
+      allow_lds(kk, row_lds(g));                                                               \
+      hipLaunchKernelGGL(kk, dim3(1 << (g.logM1 - log_row_group(g)), Q), dim3(NTH), row_lds(g), \
+                         s, (const cf*)w, bias, D, pad, g, (cf*)kspec);                        \
+    }
+    DNA_FFT_DISPATCH(L_)
+#undef L_
+  }
   DNA_LAUNCH_CHECK("dna_fftconv_filter");
   return DNA_OK;
 }

@@ -45,6 +45,9 @@ struct Args {
   void* C; long long ldc, scz;
   const float* bias_m;  // [M] or null
   const float* bias_n;  // [N] or null
+  // optional second A operand supplying k in [K1, K) at the same strides (K1 % BK == 0): C = [A | A2] B
+  // (the Mamba in_proj data gradient sums its x and z halves, held in separate tensors, in one pass)
+  const bf16* A2; int K1;
   int M, N, K, kchunk, splits;
   int va, vb, vc;       // 16-B operand loads / vector output stores allowed
 };
@@ -115,6 +118,11 @@ __global__ __launch_bounds__(NT) void sgemm_kernel(Args a) {
   const int z = blockIdx.z, zb = z / a.splits, sp = z - zb * a.splits;
   const bf16* A = a.A + zb * a.saz;
   const bf16* B = a.B + zb * a.sbz;
+  // A for the k-tile at k0: with A2, tiles past K1 read A2 (rebased so the k index stays global)
+  auto a_at = [&](int k0) -> const bf16* {
+    if (a.A2 && k0 >= a.K1) return a.A2 + zb * a.saz - (long long)a.K1 * a.sak;
+    return A;
+  };
   const int kb = sp * a.kchunk;
   const int ke = min(a.K, kb + a.kchunk);
   const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
@@ -128,7 +136,7 @@ __global__ __launch_bounds__(NT) void sgemm_kernel(Args a) {
   Tile<AKC> ta;
   Tile<BKC> tb;
   if (nk > 0) {
-    ta.load(A, a.sam, a.sak, m0, a.M, kb, ke, t, a.va);
+    ta.load(a_at(kb), a.sam, a.sak, m0, a.M, kb, ke, t, a.va);
     tb.load(B, a.sbn, a.sbk, n0, a.N, kb, ke, t, a.vb);
     ta.store(smem[0][0], t);
     tb.store(smem[0][1], t);
@@ -137,7 +145,7 @@ __global__ __launch_bounds__(NT) void sgemm_kernel(Args a) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {  // the next tile into registers while this one computes
-      ta.load(A, a.sam, a.sak, m0, a.M, kb + (kt + 1) * BK, ke, t, a.va);
+      ta.load(a_at(kb + (kt + 1) * BK), a.sam, a.sak, m0, a.M, kb + (kt + 1) * BK, ke, t, a.va);
       tb.load(B, a.sbn, a.sbk, n0, a.N, kb + (kt + 1) * BK, ke, t, a.vb);
     }
     bf16x8 fa[4], fb[4];
@@ -241,11 +249,39 @@ extern "C" int dna_gemm_strided_splits(int M, int N, int K, int batch) {
   return s;
 }
 
+static int strided_impl(const void* A, const void* A2, int K1, long long sam, long long sak,
+                        long long saz, const void* B, long long sbk, long long sbn, long long sbz,
+                        void* C, long long ldc, long long scz, int out_f32, const float* bias_m,
+                        const float* bias_n, int M, int N, int K, int batch, int splits,
+                        void* stream);
+
 extern "C" int dna_gemm_bf16_strided(const void* A, long long sam, long long sak, long long saz,
                                      const void* B, long long sbk, long long sbn, long long sbz,
                                      void* C, long long ldc, long long scz, int out_f32,
                                      const float* bias_m, const float* bias_n, int M, int N, int K,
                                      int batch, int splits, void* stream) {
+  return strided_impl(A, nullptr, K, sam, sak, saz, B, sbk, sbn, sbz, C, ldc, scz, out_f32, bias_m,
+                      bias_n, M, N, K, batch, splits, stream);
+}
+
+extern "C" int dna_gemm_bf16_strided_cat(const void* A, const void* A2, int K1, long long sam,
+                                         long long sak, long long saz, const void* B, long long sbk,
+                                         long long sbn, long long sbz, void* C, long long ldc,
+                                         long long scz, int out_f32, const float* bias_m,
+                                         const float* bias_n, int M, int N, int K, int batch,
+                                         int splits, void* stream) {
+  DNA_CHECK_ARG(A2 && K1 > 0 && K1 < K && K1 % BK == 0,
+                "dna_gemm_bf16_strided_cat: need A2 and 0 < K1 < K, K1 %% %d == 0 (K1=%d K=%d)", BK,
+                K1, K);
+  return strided_impl(A, A2, K1, sam, sak, saz, B, sbk, sbn, sbz, C, ldc, scz, out_f32, bias_m,
+                      bias_n, M, N, K, batch, splits, stream);
+}
+
+static int strided_impl(const void* A, const void* A2, int K1, long long sam, long long sak,
+                        long long saz, const void* B, long long sbk, long long sbn, long long sbz,
+                        void* C, long long ldc, long long scz, int out_f32, const float* bias_m,
+                        const float* bias_n, int M, int N, int K, int batch, int splits,
+                        void* stream) {
   DNA_CHECK_ARG(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && splits >= 1 && splits <= 65535 / batch,
                 "dna_gemm_bf16_strided: bad shape (M=%d N=%d K=%d batch=%d splits=%d)", M, N, K,
                 batch, splits);
@@ -257,6 +293,7 @@ extern "C" int dna_gemm_bf16_strided(const void* A, long long sam, long long sak
                 "dna_gemm_bf16_strided: a bias with split-K would be added once per slice");
   Args a{};
   a.A = (const bf16*)A; a.sam = sam; a.sak = sak; a.saz = saz;
+  a.A2 = (const bf16*)A2; a.K1 = K1;
   a.B = (const bf16*)B; a.sbk = sbk; a.sbn = sbn; a.sbz = sbz;
   a.C = C; a.ldc = ldc; a.scz = scz;
   a.bias_m = bias_m; a.bias_n = bias_n;
@@ -268,7 +305,7 @@ extern "C" int dna_gemm_bf16_strided(const void* A, long long sam, long long sak
   auto al = [](const void* p, long long s1, long long s2) {
     return ((uintptr_t)p & 15) == 0 && s1 % 8 == 0 && s2 % 8 == 0;
   };
-  a.va = al(A, akc ? sam : sak, saz);
+  a.va = al(A, akc ? sam : sak, saz) && (!A2 || al(A2, akc ? sam : sak, saz));
   a.vb = al(B, bkc ? sbn : sbk, sbz);
   a.vc = ((uintptr_t)C & 15) == 0 && ldc % 8 == 0 && scz % 8 == 0;
   const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * splits);

@@ -251,6 +251,57 @@ __device__ __forceinline__ float prefix_sum(float v) {
 }
 __device__ __forceinline__ float wsum(float v) { return bcast(prefix_sum(v), 63); }
 
+// N per-lane values v[n] (one per state) summed over the wave at once, transposed: each
+// exchange step halves the values a lane carries by pairing value k with k + half across lane
+// distance 32 (v_permlane32_swap), 16 (v_permlane16_swap), then 8 / 4 (row_mirror /
+// row_half_mirror DPP; a lane keeps value k or k + half by its lane bit), and a plain reduction
+// within the remaining groups of G = 64 / N lanes finishes. Lane l ends with the total of state
+// l / G. ~40 VALU for N = 16 instead of 16 separate wave sums (8 each).
+__device__ __forceinline__ void xchg_swap32(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void xchg_swap16(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+template <int D>  // D = 8 (row_mirror) or 4 (row_half_mirror)
+__device__ __forceinline__ void xchg_mirror(float& a, float b, int lane) {
+  const bool hi = lane & D;
+  const float x = hi ? b : a, y = hi ? a : b;
+  a = x + dpp<D == 8 ? 0x140 : 0x141>(0.f, y);
+}
+template <int N>
+__device__ __forceinline__ float reduce_states(float (&v)[N], int lane) {
+  static_assert(N == 4 || N == 8 || N == 16, "d_state");
+  int m = N;
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) xchg_swap32(v[k], v[k + N / 2]);
+  m = N / 2;
+  if constexpr (N >= 4) {
+#pragma unroll
+    for (int k = 0; k < N / 4; ++k) xchg_swap16(v[k], v[k + N / 4]);
+    m = N / 4;
+  }
+  if constexpr (N >= 8) {
+#pragma unroll
+    for (int k = 0; k < N / 8; ++k) xchg_mirror<8>(v[k], v[k + N / 8], lane);
+    m = N / 8;
+  }
+  if constexpr (N >= 16) {
+    xchg_mirror<4>(v[0], v[1], lane);
+    m = 1;
+  }
+  (void)m;
+  float r = v[0];
+  // groups of G = 64 / N consecutive lanes hold one state: 4 (N=16), 8 (N=8), 16 (N=4)
+  r += dpp<0xB1>(0.f, r);  // quad_perm [1,0,3,2]
+  r += dpp<0x4E>(0.f, r);  // quad_perm [2,3,0,1]
+  if constexpr (N <= 8) r += dpp<0x141>(0.f, r);  // row_half_mirror: the two quads of 8
+  if constexpr (N <= 4) r += dpp<0x140>(0.f, r);  // row_mirror: the two halves of 16
+  return r;
+}
+
 // delta after bias + softplus for one lane's 8 positions (invalid positions -> 0: identity map)
 __device__ __forceinline__ void prep_delta(float (&dl)[ITEMS], float bias, int sp, int pos, int len) {
   if (sp) {  // one uniform branch, not one per position
@@ -584,33 +635,64 @@ __device__ __forceinline__ void delta_sums(float tl, int lane, float& pre, float
   tot = bcast(inc, 63);
 }
 
-template <typename T, int N>
+// per-lane loads of a channel's parameters: with VEC the lane index is clamped and the value
+// selected, so no load sits under a branch (see Raw8::loadv)
+template <bool VEC, int N>
+__device__ __forceinline__ float lane_param(const float* p, int lane) {
+  if constexpr (VEC) {
+    const float v = p[lane & (N - 1)];
+    return lane < N ? v : 0.f;
+  } else {
+    return lane < N ? p[lane] : 0.f;
+  }
+}
+template <bool VEC, typename T>
+__device__ __forceinline__ void fetch_row(Raw8<T>& r, const T* row, int pos, int len) {
+  if constexpr (VEC) r.loadv(row, pos, len); else r.load(row, pos, len);
+}
+
+template <typename T, int N, bool VEC>
 __global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
   __shared__ __attribute__((aligned(16))) float Bs[N * CHUNK];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
   float* Sbuf = a.states;
   float* dsum = a.states + 2 * (size_t)a.batch * a.dim * nchN;
   stagef<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
-  __syncthreads();
   const int pos = c * CHUNK + lane * ITEMS;
+  struct Fetch {
+    Raw8<T> u, dl;
+    float Al, bias;
+  };
+  auto fetch = [&](Fetch& f, int j) __attribute__((always_inline)) {
+    const int d = blockIdx.x * CW * q.k + j * CW + w;
+    const size_t off = (size_t)(b * a.dim + d) * a.len;
+    f.Al = lane_param<VEC, N>(a.A + d * N, lane);
+    f.bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    fetch_row<VEC>(f.u, (const T*)a.u + off, pos, a.len);
+    fetch_row<VEC>(f.dl, (const T*)a.delta + off, pos, a.len);
+  };
+  Fetch nx;
+  fetch(nx, 0);
+  __syncthreads();
   for (int j = 0; j < q.k; ++j) {
     const int d = blockIdx.x * CW * q.k + j * CW + w;
     const int ch = b * a.dim + d;
-    const float Al = lane < N ? a.A[d * N + lane] : 0.f;
-    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    const float Al = nx.Al, bias = nx.bias;
     float uu[ITEMS], dl[ITEMS];
-    load8((const T*)a.u + (size_t)ch * a.len, pos, a.len, uu);
-    load8((const T*)a.delta + (size_t)ch * a.len, pos, a.len, dl);
+    nx.u.get(uu);
+    nx.dl.get(dl);
+    if constexpr (VEC) fetch(nx, j + 1 < q.k ? j + 1 : j);
+    else if (j + 1 < q.k) fetch(nx, j + 1);
     prep_delta(dl, bias, a.softplus, pos, a.len);
     float tl = 0.f;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) { tl += dl[i]; uu[i] *= dl[i]; }  // uu <- δ u
     float pre, suf, tot;
     delta_sums(tl, lane, pre, suf, tot);
-    float Sl = 0.f;
-#pragma unroll 4
+    float Sv[N];
+#pragma unroll
     for (int n = 0; n < N; ++n) {
       float Bv[ITEMS];
       lds8f(Bs + n * CHUNK, lane, Bv);
@@ -618,36 +700,54 @@ __global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
       float x = 0.f;
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) x = fmaf(ex2(dl[i] * An2), x, uu[i] * Bv[i]);
-      const float S = wsum(x * ex2(An2 * suf));
-      if (lane == n) Sl = S;
+      Sv[n] = x * ex2(An2 * suf);
+      // keep the unrolled states' LDS reads from all being hoisted (VGPRs -> occupancy)
+      if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
-    if (lane < N) Sbuf[(size_t)ch * nchN + (size_t)c * N + lane] = Sl;
+    const float S = reduce_states<N>(Sv, lane);  // lane l: state l / (64 / N)
+    if ((lane & (64 / N - 1)) == 0) Sbuf[(size_t)ch * nchN + (size_t)c * N + lane / (64 / N)] = S;
     if (lane == 0) dsum[(size_t)ch * q.nch + c] = tot;
   }
 }
 
-template <typename T, int N>
+template <typename T, int N, bool VEC>
 __global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
   __shared__ __attribute__((aligned(16))) float Cs[N * CHUNK];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
   float* Rbuf = a.states + (size_t)a.batch * a.dim * nchN;
   stagef<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
-  __syncthreads();
   const int pos = c * CHUNK + lane * ITEMS;
+  struct Fetch {
+    Raw8<T> dl, dy, z;
+    float Al, bias;
+  };
+  auto fetch = [&](Fetch& f, int j) __attribute__((always_inline)) {
+    const int d = blockIdx.x * CW * q.k + j * CW + w;
+    const size_t off = (size_t)(b * a.dim + d) * a.len;
+    f.Al = lane_param<VEC, N>(a.A + d * N, lane);
+    f.bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    fetch_row<VEC>(f.dl, (const T*)a.delta + off, pos, a.len);
+    fetch_row<VEC>(f.dy, (const T*)a.dout + off, pos, a.len);
+    if constexpr (VEC) f.z.loadv((const T*)(a.z ? a.z : a.dout) + off, pos, a.len);
+    else if (a.z) f.z.load((const T*)a.z + off, pos, a.len);
+  };
+  Fetch nx;
+  fetch(nx, 0);
+  __syncthreads();
   for (int j = 0; j < q.k; ++j) {
     const int d = blockIdx.x * CW * q.k + j * CW + w;
     const int ch = b * a.dim + d;
-    const float Al = lane < N ? a.A[d * N + lane] : 0.f;
-    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
-    float dl[ITEMS], dy[ITEMS];
-    load8((const T*)a.delta + (size_t)ch * a.len, pos, a.len, dl);
-    load8((const T*)a.dout + (size_t)ch * a.len, pos, a.len, dy);
+    const float Al = nx.Al, bias = nx.bias;
+    float dl[ITEMS], dy[ITEMS], zz[ITEMS];
+    nx.dl.get(dl);
+    nx.dy.get(dy);
+    if (a.z) nx.z.get(zz);
+    if constexpr (VEC) fetch(nx, j + 1 < q.k ? j + 1 : j);
+    else if (j + 1 < q.k) fetch(nx, j + 1);
     prep_delta(dl, bias, a.softplus, pos, a.len);
     if (a.z) {
-      float zz[ITEMS];
-      load8((const T*)a.z + (size_t)ch * a.len, pos, a.len, zz);
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) dy[i] *= siluf(zz[i]);
     }
@@ -656,8 +756,8 @@ __global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
     for (int i = 0; i < ITEMS; ++i) tl += dl[i];
     float pre, suf, tot;
     delta_sums(tl, lane, pre, suf, tot);
-    float Rl = 0.f;
-#pragma unroll 4
+    float Rv[N];
+#pragma unroll
     for (int n = 0; n < N; ++n) {
       float Cv[ITEMS];
       lds8f(Cs + n * CHUNK, lane, Cv);
@@ -665,10 +765,11 @@ __global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
       float r = 0.f;
 #pragma unroll
       for (int i = ITEMS - 1; i >= 0; --i) r = ex2(dl[i] * An2) * fmaf(Cv[i], dy[i], r);
-      const float R = wsum(r * ex2(An2 * pre));
-      if (lane == n) Rl = R;
+      Rv[n] = r * ex2(An2 * pre);
+      if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
-    if (lane < N) Rbuf[(size_t)ch * nchN + (size_t)c * N + lane] = Rl;
+    const float R = reduce_states<N>(Rv, lane);
+    if ((lane & (64 / N - 1)) == 0) Rbuf[(size_t)ch * nchN + (size_t)c * N + lane / (64 / N)] = R;
   }
 }
 
@@ -716,28 +817,47 @@ __global__ __launch_bounds__(64) void carry_par_kernel(Args a, Chunked q, int re
   if (!reverse && a.last_state && lane == 0) a.last_state[(size_t)ch * N + n] = xend;
 }
 
-template <typename T, int N>
+template <typename T, int N, bool VEC>
 __global__ __launch_bounds__(CT) void chunk_fwd_kernel(Args a, Chunked q) {
   __shared__ __attribute__((aligned(16))) float Bs[N * CHUNK];
   __shared__ __attribute__((aligned(16))) float Cs[N * CHUNK];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
   stagef<T, N>(Bs, (const T*)a.B + (size_t)b * N * a.len, c, a.len);
   stagef<T, N>(Cs, (const T*)a.C + (size_t)b * N * a.len, c, a.len);
-  __syncthreads();
   const int pos = c * CHUNK + lane * ITEMS;
+  struct Fetch {
+    Raw8<T> u, dl, z;
+    float Al, xcl, Dd, bias;
+  };
+  auto fetch = [&](Fetch& f, int j) __attribute__((always_inline)) {
+    const int d = blockIdx.x * CW * q.k + j * CW + w;
+    const int ch = b * a.dim + d;
+    const size_t off = (size_t)ch * a.len;
+    f.Al = lane_param<VEC, N>(a.A + d * N, lane);
+    f.xcl = lane_param<VEC, N>(a.states + (size_t)ch * nchN + (size_t)c * N, lane);
+    f.Dd = a.D ? a.D[d] : 0.f;
+    f.bias = a.delta_bias ? a.delta_bias[d] : 0.f;
+    fetch_row<VEC>(f.u, (const T*)a.u + off, pos, a.len);
+    fetch_row<VEC>(f.dl, (const T*)a.delta + off, pos, a.len);
+    if constexpr (VEC) f.z.loadv((const T*)(a.z ? a.z : a.u) + off, pos, a.len);
+    else if (a.z) f.z.load((const T*)a.z + off, pos, a.len);
+  };
+  Fetch nx;
+  fetch(nx, 0);
+  __syncthreads();
   for (int j = 0; j < q.k; ++j) {
     const int d = blockIdx.x * CW * q.k + j * CW + w;
     const int ch = b * a.dim + d;
     const size_t off = (size_t)ch * a.len;
-    const float Al = lane < N ? a.A[d * N + lane] : 0.f;
-    const float Dd = a.D ? a.D[d] : 0.f;
-    const float bias = a.delta_bias ? a.delta_bias[d] : 0.f;
-    const float xcl = lane < N ? a.states[(size_t)ch * nchN + (size_t)c * N + lane] : 0.f;
-    float uu[ITEMS], dl[ITEMS], y[ITEMS];
-    load8((const T*)a.u + off, pos, a.len, uu);
-    load8((const T*)a.delta + off, pos, a.len, dl);
+    const float Al = nx.Al, Dd = nx.Dd, bias = nx.bias, xcl = nx.xcl;
+    float uu[ITEMS], dl[ITEMS], y[ITEMS], zz[ITEMS];
+    nx.u.get(uu);
+    nx.dl.get(dl);
+    if (a.z) nx.z.get(zz);
+    if constexpr (VEC) fetch(nx, j + 1 < q.k ? j + 1 : j);
+    else if (j + 1 < q.k) fetch(nx, j + 1);
     prep_delta(dl, bias, a.softplus, pos, a.len);
     float du_[ITEMS], tl = 0.f;  // delta * u and the lane's delta sum (state-independent)
 #pragma unroll
@@ -766,15 +886,13 @@ __global__ __launch_bounds__(CT) void chunk_fwd_kernel(Args a, Chunked q) {
     }
     float o[ITEMS];
     if (a.z) {
-      float zz[ITEMS];
-      load8((const T*)a.z + off, pos, a.len, zz);
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) o[i] = fmaf(Dd, uu[i], y[i]) * siluf(zz[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) o[i] = fmaf(Dd, uu[i], y[i]);
     }
-    store8((T*)a.out + off, pos, a.len, o);
+    store8x<VEC>((T*)a.out + off, pos, a.len, o);
   }
 }
 
@@ -1039,15 +1157,19 @@ extern "C" int dna_selective_scan_fwd(const void* u, const void* delta, const fl
   a.out = out; a.states = states; a.last_state = last_state;
   hipStream_t s = as_stream(stream);
   const bool chunked = states && dim % CW == 0;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const bool vec = len % ITEMS == 0 && al16(u) && al16(delta) && al16(out) && (!z || al16(z));
   const Chunked q = plan_chunks(batch, dim, len);
   const dim3 cgrid(q.groups, q.nch, batch);
   const int st = dispatch(dtype, d_state, [&](auto t, auto n) {
     using T = decltype(t);
     constexpr int NS = decltype(n)::value;
     if (chunked) {
-      hipLaunchKernelGGL((sum_fwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
+      if (vec) hipLaunchKernelGGL((sum_fwd_kernel<T, NS, true>), cgrid, dim3(CT), 0, s, a, q);
+      else hipLaunchKernelGGL((sum_fwd_kernel<T, NS, false>), cgrid, dim3(CT), 0, s, a, q);
       hipLaunchKernelGGL((carry_par_kernel<NS>), dim3(batch * dim * NS), dim3(64), 0, s, a, q, 0);
-      hipLaunchKernelGGL((chunk_fwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
+      if (vec) hipLaunchKernelGGL((chunk_fwd_kernel<T, NS, true>), cgrid, dim3(CT), 0, s, a, q);
+      else hipLaunchKernelGGL((chunk_fwd_kernel<T, NS, false>), cgrid, dim3(CT), 0, s, a, q);
     } else {
       hipLaunchKernelGGL((fwd_kernel<T, NS>), dim3((batch * dim + WPB - 1) / WPB), dim3(64 * WPB),
                          0, s, a);
@@ -1090,7 +1212,8 @@ extern "C" int dna_selective_scan_bwd(const void* u, const void* delta, const fl
     if (chunked) {
       constexpr int R = CW > NS ? CW / NS : 1;
       const size_t bytes = (size_t)2 * NS * CHUNK * (R + 1) * sizeof(float);
-      hipLaunchKernelGGL((sum_bwd_kernel<T, NS>), cgrid, dim3(CT), 0, s, a, q);
+      if (vec) hipLaunchKernelGGL((sum_bwd_kernel<T, NS, true>), cgrid, dim3(CT), 0, s, a, q);
+      else hipLaunchKernelGGL((sum_bwd_kernel<T, NS, false>), cgrid, dim3(CT), 0, s, a, q);
       hipLaunchKernelGGL((carry_par_kernel<NS>), dim3(batch * dim * NS), dim3(64), 0, s, a, q, 1);
       if (vec) {
         allow_lds(chunk_bwd_kernel<T, NS, true>, bytes);

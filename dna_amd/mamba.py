@@ -224,11 +224,13 @@ def _sum_parts(part, shape, dtype):
 
 class InProj(torch.autograd.Function):
     """in_proj of mamba_ssm Mamba.forward, channel-major as the reference computes it
-    (`in_proj.weight @ rearrange(hidden, "b l d -> d (b l)")`), returning x and z ([b, E, L] each)
-    as two outputs so the backward takes dx and dz apart (no cat of the two halves). The forward
-    and the data gradient are the K = d_model / E products hipBLASLt runs at ~1.2 PF/s; the weight
-    gradient -- a contraction over all b*L tokens into a [2E, d] output, which hipBLASLt ran on
-    256x32 tiles at 0.17 PF/s -- runs as fp32 split-K slices on the strided MFMA GEMM."""
+    (`in_proj.weight @ rearrange(hidden, "b l d -> d (b l)")`), returning x and z ([b, E, L]
+    views of one [b, 2E, L] product) so the backward takes dx and dz apart (no cat of the two
+    halves). All three products on the strided MFMA GEMM (csrc/gemm_strided.hip): the forward
+    writes the channel-major output directly (token-major operand read with unit k stride); the
+    data gradient dh = g_x^T W_x + g_z^T W_z contracts over both halves in one pass
+    (dna_gemm_bf16_strided_cat: k < E from g_x, k >= E from g_z); the weight gradient -- a
+    contraction over all b*L tokens into [2E, d] -- runs as fp32 split-K slices."""
 
     @staticmethod
     def forward(ctx, h, weight):
@@ -239,14 +241,18 @@ class InProj(torch.autograd.Function):
             dt = torch.get_autocast_dtype("cuda")
         else:
             dt = torch.promote_types(h.dtype, weight.dtype)
+        if dt not in (torch.bfloat16, torch.float32):
+            raise NotImplementedError(f"InProj: {dt}")
         h2 = h.reshape(b * L, d).to(dt).contiguous()
-        w = weight.detach().to(dt)
-        with torch.autocast("cuda", enabled=False):
-            xz = (w @ h2.t()).reshape(E2, b, L).permute(1, 0, 2)
+        w = weight.detach().to(dt).contiguous()
+        xz = torch.empty(b, E2, L, device=h.device, dtype=dt)
+        with _timed("mamba_proj", (b * L * d + b * E2 * L) * h2.element_size(), "byte"):
+            # xz[b][c][l] = sum_j W[c][j] h[b][l][j]
+            _strided_gemm(w, (d, 1, 0), h2, (1, d, L * d), xz, (L, E2 * L), E2, L, d, b)
         ctx.save_for_backward(h2, w)
         ctx.cfg = (b, L, h.dtype, weight.dtype)
-        x, z = xz.chunk(2, dim=1)
-        return x, z
+        E = E2 // 2
+        return xz[:, :E], xz[:, E:]
 
     @staticmethod
     def backward(ctx, dx, dz):
@@ -256,40 +262,51 @@ class InProj(torch.autograd.Function):
         E = E2 // 2
         T = b * L
         dt = h2.dtype
-        halves = []
-        for i, g in enumerate((dx, dz)):
-            if g is not None:  # [b, E, L] -> [E, T] (token index t = b * L + l)
-                halves.append((i, g.to(dt).permute(1, 0, 2).reshape(E, T).contiguous()))
+        es = h2.element_size()
+        halves = [(i, g.to(dt).contiguous()) for i, g in enumerate((dx, dz)) if g is not None]
         dh = dw = None
-        with torch.autocast("cuda", enabled=False):
-            if ctx.needs_input_grad[0]:
-                dh = torch.zeros(T, d, device=h2.device, dtype=dt) if not halves else None
-                for i, g in halves:
-                    wi = w[i * E:(i + 1) * E]
-                    dh = g.t() @ wi if dh is None else torch.addmm(dh, g.t(), wi)
-                dh = dh.reshape(b, L, d).to(hdt)
-            if ctx.needs_input_grad[1]:
-                part, s = None, 0
-                if not halves:
-                    dw = torch.zeros_like(w, dtype=wdt)
+        if ctx.needs_input_grad[0]:
+            dh = torch.empty(b, L, d, device=h2.device, dtype=dt)
+            # dh[b][l][j] = sum_c g[b][c][l] W[c][j]: A(m = l, k = c) = g[b][c][l]
+            if not halves:
+                dh.zero_()
+            elif len(halves) == 2 and dt == torch.bfloat16:
+                with _timed("mamba_proj", (2 * T * E + T * d) * es, "byte"):
+                    N.call("dna_gemm_bf16_strided_cat", halves[0][1].data_ptr(),
+                           halves[1][1].data_ptr(), E, 1, L, E * L, w.data_ptr(), d, 1, 0,
+                           dh.data_ptr(), d, L * d, 0, None, None, L, d, E2, b, 1, N.stream_ptr())
+            else:
+                if len(halves) == 2:  # fp32 parity mode: one operand of both halves
+                    g, wi = torch.cat([halves[0][1], halves[1][1]], 1), w
                 else:
-                    s = int(N.lib().dna_gemm_strided_splits(E, d, T, 1))
-                    # both halves written in full when dx and dz are both there; else the
-                    # missing half's rows must read as zero
-                    alloc = torch.empty if len(halves) == 2 else torch.zeros
-                    part = alloc(s, E2, d, device=h2.device, dtype=torch.float32)
-                    for i, g in halves:  # dW[c][j] = sum_t g[c][t] h[t][j]
-                        _wgrad_tokens(g, (T, 1, 0), h2, (d, 1, 0), E, d, T, 1, part, i * E, E2)
-                    dw = _sum_parts(part, (E2, d), wdt)
+                    i, g = halves[0]
+                    wi = w[i * E:(i + 1) * E]
+                K = g.shape[1]
+                with _timed("mamba_proj", (T * K + T * d) * es, "byte"):
+                    _strided_gemm(g, (1, L, K * L), wi, (d, 1, 0), dh, (d, L * d), L, d, K, b)
+            dh = dh.to(hdt)
+        if ctx.needs_input_grad[1]:
+            if not halves:
+                dw = torch.zeros_like(w, dtype=wdt)
+            else:
+                s = int(N.lib().dna_gemm_strided_splits(E, d, L, b))
+                # both halves written in full when dx and dz are both there; else the missing
+                # half's rows must read as zero
+                alloc = torch.empty if len(halves) == 2 else torch.zeros
+                part = alloc(s * b, E2, d, device=h2.device, dtype=torch.float32)
+                for i, g in halves:  # dW[c][j] = sum_{b,l} g[b][c][l] h[b][l][j]
+                    _wgrad_tokens(g, (L, 1, E * L), h2, (d, 1, L * d), E, d, L, b, part, i * E, E2)
+                dw = _sum_parts(part, (E2, d), wdt)
         return dh, dw
 
 
 class OutProj(torch.autograd.Function):
     """out_proj of mamba_ssm Mamba.forward on the scan output y [b, E, L] (channel-major):
-    out [b, L, d] = y^T . W^T (+ bias). Forward on hipBLASLt (a transposed-operand GEMM at
-    ~1.2 PF/s); the data gradient straight into the channel-major [b, E, L] layout the scan's
-    backward reads (token-major, it cost a 268-MB transpose copy per call) and the weight gradient
-    (contraction over all b*L tokens into [d, E], fp32 split-K slices) on the strided MFMA GEMM."""
+    out [b, L, d] = y^T . W^T (+ bias, rounded to the compute dtype first as autocast's
+    F.linear does). All three products on the strided MFMA GEMM: the forward reads y with unit
+    token stride (no transpose), the data gradient goes straight into the channel-major
+    [b, E, L] layout the scan's backward reads, the weight gradient (contraction over all b*L
+    tokens into [d, E]) as fp32 split-K slices."""
 
     @staticmethod
     def forward(ctx, y, weight, bias):
@@ -299,13 +316,19 @@ class OutProj(torch.autograd.Function):
             dt = torch.get_autocast_dtype("cuda")
         else:
             dt = torch.promote_types(y.dtype, weight.dtype)
+        if dt not in (torch.bfloat16, torch.float32):
+            raise NotImplementedError(f"OutProj: {dt}")
         yc = y.to(dt)
         if yc.stride(2) != 1 or yc.stride(1) != L:
             yc = yc.contiguous()
-        w = weight.detach().to(dt)
-        bb = None if bias is None else bias.detach().to(dt)
-        with torch.autocast("cuda", enabled=False):
-            out = F.linear(yc.transpose(1, 2), w, bb)
+        w = weight.detach().to(dt).contiguous()
+        d = w.shape[0]
+        bn = None if bias is None else bias.detach().to(dt).float().contiguous()
+        out = torch.empty(b, L, d, device=y.device, dtype=dt)
+        with _timed("mamba_proj", (b * E * L + b * L * d) * yc.element_size(), "byte"):
+            # out[b][l][o] = sum_e y[b][e][l] W[o][e] (+ bias[o])
+            _strided_gemm(yc, (1, L, yc.stride(0)), w, (1, E, 0), out, (d, L * d), L, d, E, b,
+                          bias_n=bn)
         ctx.save_for_backward(yc, w)
         ctx.cfg = (y.dtype, weight.dtype, None if bias is None else bias.dtype)
         return out

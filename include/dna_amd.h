@@ -269,6 +269,15 @@ int dna_gemm_bf16_strided(const void* A, long long sam, long long sak, long long
                           void* C, long long ldc, long long scz, int out_f32,
                           const float* bias_m, const float* bias_n, int M, int N, int K,
                           int batch, int splits, void* stream);
+/* The same product with the contraction split over two A operands of equal strides:
+ * C = [A | A2] . B, A supplying k < K1 and A2 k in [K1, K) (K1 % 32 == 0). Replaces the
+ * mm + addmm pair of the Mamba in_proj data gradient (dh = g_x^T W_x + g_z^T W_z,
+ * mamba_ssm Mamba.in_proj backward under modeling_caduceus.py:88-91). */
+int dna_gemm_bf16_strided_cat(const void* A, const void* A2, int K1, long long sam, long long sak,
+                              long long saz, const void* B, long long sbk, long long sbn,
+                              long long sbz, void* C, long long ldc, long long scz, int out_f32,
+                              const float* bias_m, const float* bias_n, int M, int N, int K,
+                              int batch, int splits, void* stream);
 int dna_gemm_f32_strided(const float* A, long long sam, long long sak, long long saz,
                          const float* B, long long sbk, long long sbn, long long sbz,
                          float* C, long long ldc, long long scz, const float* bias_n,

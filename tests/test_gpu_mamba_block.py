@@ -43,11 +43,16 @@ def _sd64(module):
     return {k: v.detach().double().cpu() for k, v in module.state_dict().items()}
 
 
-@pytest.mark.parametrize("b,l,d_model,d_state", [(2, 300, 64, 16), (1, 1100, 32, 8)])
-def test_mamba_block_fwd_bwd_vs_oracle(b, l, d_model, d_state):
+@pytest.mark.parametrize("b,l,d_model,d_state,bias", [(2, 300, 64, 16, False), (1, 1100, 32, 8, False),
+                                                       (2, 512, 64, 16, True)])
+def test_mamba_block_fwd_bwd_vs_oracle(b, l, d_model, d_state, bias):
     from dna_amd.mamba import Mamba
     torch.manual_seed(l)
-    m = Mamba(d_model=d_model, d_state=d_state)
+    m = Mamba(d_model=d_model, d_state=d_state, bias=bias)
+    if bias:
+        with torch.no_grad():
+            m.in_proj.bias.normal_(0, 0.1)
+            m.out_proj.bias.normal_(0, 0.1)
     with torch.no_grad():
         m.D.add_(torch.randn_like(m.D) * 0.1)
         m.conv1d.weight.mul_(2.0)
