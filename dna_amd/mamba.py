@@ -248,7 +248,12 @@ class InProj(torch.autograd.Function):
         xz = torch.empty(b, E2, L, device=h.device, dtype=dt)
         with _timed("mamba_proj", (b * L * d + b * E2 * L) * h2.element_size(), "byte"):
             # xz[b][c][l] = sum_j W[c][j] h[b][l][j]
-            _strided_gemm(w, (d, 1, 0), h2, (1, d, L * d), xz, (L, E2 * L), E2, L, d, b)
+            if dt == torch.bfloat16 and d in (64, 128, 256):
+                # register-resident weight, h streamed (csrc/proj_cm.hip)
+                N.call("dna_proj_cm_bf16", w.data_ptr(), h2.data_ptr(), None, E2, L, d, b,
+                       xz.data_ptr(), N.stream_ptr())
+            else:
+                _strided_gemm(w, (d, 1, 0), h2, (1, d, L * d), xz, (L, E2 * L), E2, L, d, b)
         ctx.save_for_backward(h2, w)
         ctx.cfg = (b, L, h.dtype, weight.dtype)
         E = E2 // 2

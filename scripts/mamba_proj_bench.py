@@ -62,6 +62,21 @@ def main():
     res["in_proj_fwd"] = dict(torch_us=timeit(f_t, a.iters), hip_us=timeit(f_s, a.iters),
                               max_abs_diff=float((xz_t.float() - xz_s[0].float()).abs().max()),
                               bytes=(T * d + E2 * d + E2 * T) * 2)
+    from dna_amd import _native as N
+    xz_p = torch.empty(1, E2, L, device=dev, dtype=bf)
+    f_p = lambda: N.call("dna_proj_cm_bf16", W.data_ptr(), h.data_ptr(), None, E2, L, d, 1,
+                         xz_p.data_ptr(), N.stream_ptr())
+    res["in_proj_fwd_proj_cm"] = dict(torch_us=res["in_proj_fwd"]["torch_us"],
+                                      hip_us=timeit(f_p, a.iters),
+                                      max_abs_diff=float((xz_t.float() - xz_p[0].float()).abs().max()),
+                                      bytes=(T * d + E2 * d + E2 * T) * 2)
+
+    # the same product token-major (C[T, 2E] = h . W^T): how much of the time is the layout
+    xz_k = torch.empty(T, E2, device=dev, dtype=bf)
+    f_k = lambda: strided_gemm(h, (d, 1, 0), W, (1, d, 0), xz_k, (E2, T * E2), T, E2, d, 1)
+    f_kt = lambda: torch.mm(h, W.t(), out=xz_k)
+    res["in_proj_fwd_token_major"] = dict(torch_us=timeit(f_kt, a.iters), hip_us=timeit(f_k, a.iters),
+                                          max_abs_diff=0.0, bytes=(T * d + E2 * d + E2 * T) * 2)
 
     # in_proj data gradient (both halves)
     dh_t = torch.empty(T, d, device=dev, dtype=bf)

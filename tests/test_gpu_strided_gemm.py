@@ -104,3 +104,29 @@ def test_channel_linear_sliced_input_fp32():
     torch.einsum("mk,bkl->bml", wr, xr[:, :16]).backward(dy.double())
     assert _rel(xd.grad, xr.grad) < 1e-5 and _rel(w.grad, wr.grad) < 1e-5
     assert float(xd.grad[:, 16:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("M,N_,K,batch,bias", [(1024, 4096, 256, 1, False), (1024, 2048, 256, 2, True),
+                                               (100, 1001, 64, 2, True), (300, 77, 128, 3, False),
+                                               (256, 64, 256, 1, True)])
+def test_proj_cm_vs_fp32(M, N_, K, batch, bias):
+    """dna_proj_cm_bf16 (register-resident weight, channel-major output; the Mamba in_proj
+    forward) against an fp32 matmul of the same bf16 operands: bf16 output rounding only."""
+    g = torch.Generator(device=DEV).manual_seed(M + N_ + K)
+    W = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    X = torch.randn(batch, N_, K, device=DEV, generator=g).to(torch.bfloat16)
+    b = torch.randn(M, device=DEV, generator=g) if bias else None
+    C = torch.full((batch, M, N_), float("nan"), device=DEV, dtype=torch.bfloat16)
+    N.call("dna_proj_cm_bf16", W.data_ptr(), X.data_ptr(), None if b is None else b.data_ptr(),
+           M, N_, K, batch, C.data_ptr(), N.stream_ptr())
+    ref = torch.einsum("ck,zlk->zcl", W.float(), X.float())
+    if b is not None:
+        ref = ref + b[None, :, None]
+    err = (C.float() - ref).abs().max() / ref.abs().max()
+    assert torch.isfinite(C.float()).all()
+    assert err < 8e-3, err
+
+
+def test_proj_cm_rejects_bad_k():
+    with pytest.raises(N.NativeError, match="K=96"):
+        N.call("dna_proj_cm_bf16", 16, 16, None, 64, 64, 96, 1, 16, None)
