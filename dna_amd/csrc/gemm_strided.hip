@@ -48,6 +48,7 @@ struct Args {
   // optional second A operand supplying k in [K1, K) at the same strides (K1 % BK == 0): C = [A | A2] B
   // (the Mamba in_proj data gradient sums its x and z halves, held in separate tensors, in one pass)
   const bf16* A2; int K1;
+  int accum;            // C += A B (read-modify-write epilogue) instead of C = A B
   int M, N, K, kchunk, splits;
   int va, vb, vc;       // 16-B operand loads / vector output stores allowed
 };
@@ -209,8 +210,34 @@ __global__ __launch_bounds__(NT) void sgemm_kernel(Args a) {
         const bf16x8 hb = __builtin_bit_cast(bf16x8, u32x4_t{(unsigned)sx[0], (unsigned)sy[0], (unsigned)sx[1], (unsigned)sy[1]});
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (float)hb[e];  // exact: already bf16 values
+        // accumulate: the unrounded sums in the same lane order (the swaps run with every lane
+        // active -- inside the bounds branch a swap partner may be masked off)
+        float s8[8];
+        if (a.accum) {
+          const u32x4_t a0 = __builtin_bit_cast(u32x4_t, v[0]), a1 = __builtin_bit_cast(u32x4_t, v[1]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(a0[r], a1[r], false, false);
+            s8[r] = __uint_as_float((unsigned)sw[0]);
+            s8[4 + r] = __uint_as_float((unsigned)sw[1]);
+          }
+        }
         if (m < a.M && n < a.N) {
           bf16* C = reinterpret_cast<bf16*>(a.C) + zc + (long long)m * a.ldc + n;
+          if (a.accum) {  // C = bf16(A B + C): the product is rounded once, after the sum
+            if (a.vc && n + 8 <= a.N) {
+              const bf16x8 old = *reinterpret_cast<const bf16x8*>(C);
+              bf16x8 nw;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) nw[e] = (bf16)(s8[e] + (float)old[e]);
+              *reinterpret_cast<bf16x8*>(C) = nw;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                if (n + e < a.N) C[e] = (bf16)(s8[e] + (float)C[e]);
+            }
+            continue;
+          }
           if (a.vc && n + 8 <= a.N) *reinterpret_cast<bf16x8*>(C) = hb;
           else
 #pragma unroll
@@ -221,6 +248,11 @@ __global__ __launch_bounds__(NT) void sgemm_kernel(Args a) {
       }
       if (m < a.M && n < a.N) {
         float* C = reinterpret_cast<float*>(a.C) + zc + (long long)m * a.ldc + n;
+        if (a.accum) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < a.N) o[e] += C[e];
+        }
         if (a.vc && n + 8 <= a.N) {
           *reinterpret_cast<f32x4*>(C) = f32x4{o[0], o[1], o[2], o[3]};
           *reinterpret_cast<f32x4*>(C + 4) = f32x4{o[4], o[5], o[6], o[7]};
@@ -294,6 +326,9 @@ static int strided_impl(const void* A, const void* A2, int K1, long long sam, lo
   Args a{};
   a.A = (const bf16*)A; a.sam = sam; a.sak = sak; a.saz = saz;
   a.A2 = (const bf16*)A2; a.K1 = K1;
+  a.accum = (out_f32 & 2) != 0;
+  DNA_CHECK_ARG(!a.accum || splits == 1, "dna_gemm_bf16_strided: accumulate needs splits == 1");
+  out_f32 &= 1;
   a.B = (const bf16*)B; a.sbk = sbk; a.sbn = sbn; a.sbz = sbz;
   a.C = C; a.ldc = ldc; a.scz = scz;
   a.bias_m = bias_m; a.bias_n = bias_n;

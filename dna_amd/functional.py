@@ -219,17 +219,22 @@ class HipEmbedding(nn.Embedding):
         return embedding(ids, self.weight, self.padding_idx)
 
 
-def strided_gemm(A, sa, B, sb, C, sc, M, Nc, K, batch, splits=1, out_f32=None, bias_n=None):
+def strided_gemm(A, sa, B, sb, C, sc, M, Nc, K, batch, splits=1, out_f32=None, bias_n=None,
+                 accumulate=False):
     """C[z][m][n] = sum_k A(m, k) B(k, n) (+ bias_n[n], fp32) on dna_gemm_bf16_strided /
     dna_gemm_f32_strided (z = batch * splits + split). sa = (sam, sak, saz), sb = (sbk, sbn, sbz),
-    sc = (ldc, scz); strides in elements."""
+    sc = (ldc, scz); strides in elements. accumulate (bf16 operands, splits == 1): C += A B in the
+    epilogue."""
     bn = None if bias_n is None else bias_n.data_ptr()
     if A.dtype == torch.bfloat16:
         assert B.dtype == torch.bfloat16
         f32 = C.dtype == torch.float32 if out_f32 is None else out_f32
         N.call("dna_gemm_bf16_strided", A.data_ptr(), *sa, B.data_ptr(), *sb, C.data_ptr(), *sc,
-               int(f32), None, bn, M, Nc, K, batch, splits, N.stream_ptr())
+               int(f32) | (2 if accumulate else 0), None, bn, M, Nc, K, batch, splits,
+               N.stream_ptr())
     else:
+        if accumulate:
+            raise NotImplementedError("strided_gemm: accumulate needs bf16 operands")
         assert A.dtype == B.dtype == C.dtype == torch.float32
         N.call("dna_gemm_f32_strided", A.data_ptr(), *sa, B.data_ptr(), *sb, C.data_ptr(), *sc,
                bn, M, Nc, K, batch, splits, N.stream_ptr())

@@ -25,9 +25,23 @@ from . import functional as DF
 from .functional import _dt, _gpu, _p, _timed, strided_gemm as _strided_gemm
 
 
+class GradSink:
+    """Hand-off of the scan's du to the x_proj backward (Mamba.forward): x feeds both the scan
+    (u) and x_proj, so autograd would add the two gradients of x in a separate pass over
+    [b, E, L]. With a sink the scan returns no gradient for u and leaves du here; x_proj's
+    backward then accumulates its data gradient into du in the GEMM epilogue and returns the sum
+    as the gradient of x -- the same total, one pass less. x_proj's backward necessarily runs
+    after the scan's (it needs dB / dC)."""
+    __slots__ = ("du",)
+
+    def __init__(self):
+        self.du = None
+
+
 class SelectiveScan(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, u, delta, A, B, C, D, z, delta_bias, delta_softplus, return_last_state):
+    def forward(ctx, u, delta, A, B, C, D, z, delta_bias, delta_softplus, return_last_state,
+                sink=None):
         _gpu(u, delta, A, B, C, D, z, delta_bias)
         b, d, l = u.shape
         n = A.shape[1]
@@ -53,6 +67,7 @@ class SelectiveScan(torch.autograd.Function):
         ctx.save_for_backward(u, delta, A32, B, C, D32, z, db32, states)
         ctx.cfg = (bool(delta_softplus), A.dtype, B.dtype, C.dtype, D is not None,
                    delta_bias is not None)
+        ctx.sink = sink
         if return_last_state:
             ctx.mark_non_differentiable(last)
             return out, last
@@ -81,7 +96,10 @@ class SelectiveScan(torch.autograd.Function):
                    b, d, l, n, states.data_ptr(), dout.data_ptr(), du.data_ptr(), ddelta.data_ptr(),
                    dA.data_ptr(), dB.data_ptr(), dC.data_ptr(), _p(dD), _p(dz), _p(dbias),
                    N.stream_ptr())
-        return (du, ddelta, dA.to(adt), dB.to(bdt), dC.to(cdt), dD, dz, dbias, None, None)
+        if ctx.sink is not None:
+            ctx.sink.du = du
+            du = None
+        return (du, ddelta, dA.to(adt), dB.to(bdt), dC.to(cdt), dD, dz, dbias, None, None, None)
 
 
 def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
@@ -152,7 +170,7 @@ class ChannelLinear(torch.autograd.Function):
     over b and L runs as fp32 split-K slices summed by dna_sum_slices_accum."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, sink=None):
         _gpu(x, weight)
         b, K, L = x.shape
         M = weight.shape[0]
@@ -173,12 +191,16 @@ class ChannelLinear(torch.autograd.Function):
                           M, L, K, b)
         ctx.save_for_backward(xin, w)
         ctx.cfg = (x.dtype, weight.dtype)
+        ctx.sink = sink
         return y
 
     @staticmethod
     def backward(ctx, dy):
         xin, w = ctx.saved_tensors
         xdt, wdt = ctx.cfg
+        du = None
+        if ctx.sink is not None:  # the scan's du for the same x (GradSink)
+            du, ctx.sink.du = ctx.sink.du, None
         b, K, L = xin.shape
         M = w.shape[0]
         dy = dy.to(xin.dtype)
@@ -187,10 +209,14 @@ class ChannelLinear(torch.autograd.Function):
         dx = dw = None
         es = xin.element_size()
         if ctx.needs_input_grad[0]:  # dx[b, K, L] = W^T[K, M] . dy[b, M, L]
-            dx = torch.empty(b, K, L, device=xin.device, dtype=xin.dtype)
-            with _timed("mamba_proj", (b * M * L + b * K * L) * es, "byte"):
+            acc = (du is not None and du.dtype == xin.dtype == torch.bfloat16 and du.is_contiguous()
+                   and du.shape == (b, K, L))
+            dx = du if acc else torch.empty(b, K, L, device=xin.device, dtype=xin.dtype)
+            with _timed("mamba_proj", (b * M * L + (3 if acc else 1) * b * K * L) * es, "byte"):
                 _strided_gemm(w, (1, K, 0), dy, (dy.stride(1), 1, dy.stride(0)), dx, (L, K * L),
-                              K, L, M, b)
+                              K, L, M, b, accumulate=acc)
+            if du is not None and not acc:
+                dx = dx + du.to(dx.dtype)
         if ctx.needs_input_grad[1]:  # dW[M, K] = sum_b dy[b] . x[b]^T (contraction over L)
             s = int(N.lib().dna_gemm_strided_splits(M, K, L, b))
             part = torch.empty(b * s, M, K, device=xin.device, dtype=torch.float32)
@@ -199,7 +225,7 @@ class ChannelLinear(torch.autograd.Function):
                               (1, xin.stride(1), xin.stride(0)), part, (K, M * K), M, K, L, b, s,
                               out_f32=True)
             dw = _sum_parts(part, (M, K), wdt)
-        return (None if dx is None else dx.to(xdt)), dw
+        return (None if dx is None else dx.to(xdt)), dw, None
 
 
 def _wgrad_tokens(dy, sa, x, sb, M, Nn, T, batch, part=None, row0=0, rows_total=None):
@@ -423,12 +449,13 @@ class Mamba(nn.Module):
         # [b, R + 2N, L] = x_proj.weight . x, delta [b, E, L] = dt_proj.weight . x_dbl[:, :R]
         if self.x_proj.bias is not None:
             raise NotImplementedError("Mamba: x_proj with a bias (mamba_ssm builds it bias-free)")
-        x_dbl = ChannelLinear.apply(x, self.x_proj.weight)
+        sink = GradSink()  # the scan's du summed into x_proj's dx in its GEMM epilogue
+        x_dbl = ChannelLinear.apply(x, self.x_proj.weight, sink)
         R, Ns = self.dt_rank, self.d_state
         dt = ChannelLinear.apply(x_dbl[:, :R], self.dt_proj.weight)
         Bm, Cm = x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
-        y = selective_scan_fn(x, dt, A, Bm, Cm, self.D.float(), z=z.contiguous(),
-                              delta_bias=self.dt_proj.bias.float(), delta_softplus=True)
+        y = SelectiveScan.apply(x, dt, A, Bm, Cm, self.D.float(), z.contiguous(),
+                                self.dt_proj.bias.float(), True, False, sink)
         return OutProj.apply(y, self.out_proj.weight, self.out_proj.bias)
 
 

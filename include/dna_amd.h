@@ -259,7 +259,9 @@ int dna_linear_wgrad_f32(const float* dy, const float* x, int T, int N, int K, i
  *   C[z][m][n] = sum_k A(m, k) B(k, n),  z = b * splits + s (k slice s of the contraction),
  *   A(m, k) = A[b*saz + m*sam + k*sak] (sak == 1 or sam == 1),
  *   B(k, n) = B[b*sbz + k*sbk + n*sbn] (sbk == 1 or sbn == 1),
- *   C + z*scz, row stride ldc; bf16 in, fp32 accumulate, bf16 or fp32 (out_f32) out;
+ *   C + z*scz, row stride ldc; bf16 in, fp32 accumulate, bf16 or fp32 (out_f32 bit 0) out;
+ *   out_f32 bit 1: C += A B (read-modify-write, one rounding after the sum; splits == 1) --
+ *   the x_proj data gradient summed into the scan's du without a separate add;
  *   bias_m[M] / bias_n[N] optional (may be null).
  * Weight gradients: splits from dna_gemm_strided_splits, fp32 slices summed over z by
  * dna_sum_slices_accum. csrc/gemm_strided.hip (bf16, MFMA 16x16x32), csrc/gemm_f32.hip (fp32). */

@@ -111,3 +111,26 @@ def test_flip_l_equals_torch_flip(shape, dtype):
     dy = torch.randn(*shape, generator=g).to(dtype).to("cuda")
     y.backward(dy)
     assert torch.equal(x.grad, dy.flip(dims=(1,)))
+
+
+def test_mamba_block_bf16_grads_track_fp32():
+    """Under bf16 autocast the x gradient is the scan's du with x_proj's data gradient summed into
+    it in the strided GEMM's epilogue (GradSink, no separate add): every gradient stays within
+    bf16 reach of the fp32 run of the same module (which adds the two in torch)."""
+    from dna_amd.mamba import Mamba
+    torch.manual_seed(11)
+    m = Mamba(d_model=64, d_state=16).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    h = torch.randn(2, 1024, 64, device=DEV, generator=g)
+    dy = torch.randn(2, 1024, 64, device=DEV, generator=g)
+    grads = []
+    for ac in (False, True):
+        m.zero_grad(set_to_none=True)
+        hg = h.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=ac):
+            y = m(hg)
+        y.float().backward(dy)
+        grads.append([hg.grad.float()] + [p.grad.float() for _, p in m.named_parameters()])
+    names = ["h"] + [n for n, _ in m.named_parameters()]
+    for n, a, b in zip(names, *grads):
+        assert _rel(b, a) < 5e-2, (n, _rel(b, a))

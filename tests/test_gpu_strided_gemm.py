@@ -130,3 +130,20 @@ def test_proj_cm_vs_fp32(M, N_, K, batch, bias):
 def test_proj_cm_rejects_bad_k():
     with pytest.raises(N.NativeError, match="K=96"):
         N.call("dna_proj_cm_bf16", 16, 16, None, 64, 64, 96, 1, 16, None)
+
+
+@pytest.mark.parametrize("M,N_,K,batch", [(512, 4096, 48, 1), (64, 301, 16, 2)])
+def test_strided_gemm_accumulate(M, N_, K, batch):
+    """accumulate=True: C = bf16(A B + C) in the epilogue (the x_proj data gradient summed into
+    the scan's du), against fp32 A B + C."""
+    from dna_amd.functional import strided_gemm
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N_)
+    W = torch.randn(K, M, device=DEV, generator=g).to(torch.bfloat16)        # A(m, k) = W[k][m]
+    dy = torch.randn(batch, K, N_, device=DEV, generator=g).to(torch.bfloat16)
+    C0 = torch.randn(batch, M, N_, device=DEV, generator=g).to(torch.bfloat16)
+    C = C0.clone()
+    strided_gemm(W, (1, M, 0), dy, (N_, 1, K * N_), C, (N_, M * N_), M, N_, K, batch,
+                 accumulate=True)
+    ref = torch.einsum("km,zkn->zmn", W.float(), dy.float()) + C0.float()
+    err = (C.float() - ref).abs().max() / ref.abs().max()
+    assert err < 8e-3, err
