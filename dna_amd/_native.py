@@ -80,7 +80,7 @@ _SIGS = {
     "dna_gemm_strided_splits": (_i, [_i, _i, _i, _i]),
     "dna_gemm_bf16_strided": (_i, [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64,
                                    _i, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
-    "dna_proj_cm_bf16": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "dna_proj_cm_bf16": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "dna_gemm_bf16_strided_cat": (_i, [_vp, _vp, _i, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp,
                                        _i64, _i64, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "dna_gemm_f32_strided": (_i, [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64,

@@ -36,7 +36,7 @@ template <int K, bool STAGE>
 __global__ __launch_bounds__(NT, 1) void proj_cm_kernel(const bf16* __restrict__ W,
                                                         const bf16* __restrict__ X,
                                                         const float* __restrict__ bias, int M,
-                                                        int N, bf16* __restrict__ C) {
+                                                        int N, int rev, bf16* __restrict__ C) {
   static_assert(K % 32 == 0 && K <= KMAX, "K");
   constexpr int KS = K / 32;                 // k-steps
   constexpr int CH = NTILE * K / 8 / NT;     // 16-B chunks of an X tile per thread
@@ -77,7 +77,8 @@ __global__ __launch_bounds__(NT, 1) void proj_cm_kernel(const bf16* __restrict__
       const int q = tid + NT * p;
       const int row = q / (K / 8), col = q % (K / 8);
       const int l = tile * NTILE + row;
-      r[p] = l < N ? *reinterpret_cast<const bf16x8*>(Xz + (size_t)l * K + 8 * col) : bf16x8{};
+      const int lx = rev ? N - 1 - l : l;  // rev: X read in reversed position order
+      r[p] = l < N ? *reinterpret_cast<const bf16x8*>(Xz + (size_t)lx * K + 8 * col) : bf16x8{};
     }
   };
   bf16x8 xr[CH];
@@ -176,7 +177,7 @@ using namespace dna;
 using namespace dna::pcm;
 
 extern "C" int dna_proj_cm_bf16(const void* W, const void* X, const float* bias, int M, int N,
-                                int K, int batch, void* C, void* stream) {
+                                int K, int batch, int reverse, void* C, void* stream) {
   DNA_CHECK_ARG(M >= 0 && N >= 0 && batch >= 1, "dna_proj_cm_bf16: bad shape (M=%d N=%d batch=%d)",
                 M, N, batch);
   if (M == 0 || N == 0) return DNA_OK;
@@ -200,9 +201,9 @@ extern "C" int dna_proj_cm_bf16(const void* W, const void* X, const float* bias,
   const bool stage = stage_env != 0;
 #define DNA_PCM(KK)                                                                                   \
   if (stage) hipLaunchKernelGGL((proj_cm_kernel<KK, true>), grid, dim3(NT), 0, s, (const bf16*)W,   \
-                                (const bf16*)X, bias, M, N, (bf16*)C);                               \
+                                (const bf16*)X, bias, M, N, reverse, (bf16*)C);                      \
   else hipLaunchKernelGGL((proj_cm_kernel<KK, false>), grid, dim3(NT), 0, s, (const bf16*)W,        \
-                          (const bf16*)X, bias, M, N, (bf16*)C);
+                          (const bf16*)X, bias, M, N, reverse, (bf16*)C);
   switch (K) {
     case 64: DNA_PCM(64) break;
     case 128: DNA_PCM(128) break;

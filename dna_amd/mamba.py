@@ -15,6 +15,7 @@ modeling_caduceus.py:68-121: forward + flipped reverse Mamba, tied in/out projec
 "ew_multiply").
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -248,18 +249,37 @@ def _sum_parts(part, shape, dtype):
     return out.to(dtype)
 
 
+class DhSink:
+    """Hand-off between the two in_proj backwards of a fused BiMambaWrapper (both directions read
+    the same hidden states): the first backward to run writes its dh (in forward position order)
+    here and returns no gradient; the second accumulates its dh into the same buffer in the
+    GEMM epilogue and returns the sum -- autograd's add of the two gradients never runs."""
+    __slots__ = ("dh",)
+
+    def __init__(self):
+        self.dh = None
+
+
+def _rows_from_end(t, b, L, d):
+    """[b, L, d]-strided view of t whose data_ptr is row L-1 of batch 0: with row stride -d the
+    GEMMs walk the sequence backwards (the BiMamba reverse direction, no flipped copy)."""
+    return t.view(b, L, d)[:, L - 1:]
+
+
 class InProj(torch.autograd.Function):
     """in_proj of mamba_ssm Mamba.forward, channel-major as the reference computes it
     (`in_proj.weight @ rearrange(hidden, "b l d -> d (b l)")`), returning x and z ([b, E, L]
     views of one [b, 2E, L] product) so the backward takes dx and dz apart (no cat of the two
-    halves). All three products on the strided MFMA GEMM (csrc/gemm_strided.hip): the forward
-    writes the channel-major output directly (token-major operand read with unit k stride); the
-    data gradient dh = g_x^T W_x + g_z^T W_z contracts over both halves in one pass
-    (dna_gemm_bf16_strided_cat: k < E from g_x, k >= E from g_z); the weight gradient -- a
-    contraction over all b*L tokens into [2E, d] -- runs as fp32 split-K slices."""
+    halves). The forward on the weight-stationary projection kernel (csrc/proj_cm.hip) or the
+    strided MFMA GEMM; the data gradient dh = g_x^T W_x + g_z^T W_z contracts over both halves
+    in one pass (dna_gemm_bf16_strided_cat); the weight gradient -- a contraction over all b*L
+    tokens into [2E, d] -- as fp32 split-K slices.
+    reverse: the sequence is read backwards (position l of x / z is h[L-1-l]), which is the
+    BiMambaWrapper reverse direction `mamba_rev(hidden.flip(1))` without the flipped copy; its dh
+    is written back in forward order. sink (bf16): see DhSink."""
 
     @staticmethod
-    def forward(ctx, h, weight):
+    def forward(ctx, h, weight, reverse=False, sink=None):
         _gpu(h, weight)
         b, L, d = h.shape
         E2 = weight.shape[0]
@@ -269,26 +289,33 @@ class InProj(torch.autograd.Function):
             dt = torch.promote_types(h.dtype, weight.dtype)
         if dt not in (torch.bfloat16, torch.float32):
             raise NotImplementedError(f"InProj: {dt}")
+        if (reverse or sink is not None) and dt != torch.bfloat16:
+            raise NotImplementedError("InProj: reverse / sink need bf16 (autocast)")
         h2 = h.reshape(b * L, d).to(dt).contiguous()
         w = weight.detach().to(dt).contiguous()
         xz = torch.empty(b, E2, L, device=h.device, dtype=dt)
         with _timed("mamba_proj", (b * L * d + b * E2 * L) * h2.element_size(), "byte"):
-            # xz[b][c][l] = sum_j W[c][j] h[b][l][j]
+            # xz[b][c][l] = sum_j W[c][j] h[b][l'][j],  l' = l or L-1-l
             if dt == torch.bfloat16 and d in (64, 128, 256):
                 # register-resident weight, h streamed (csrc/proj_cm.hip)
                 N.call("dna_proj_cm_bf16", w.data_ptr(), h2.data_ptr(), None, E2, L, d, b,
-                       xz.data_ptr(), N.stream_ptr())
+                       int(reverse), xz.data_ptr(), N.stream_ptr())
+            elif reverse:
+                _strided_gemm(w, (d, 1, 0), _rows_from_end(h2, b, L, d), (1, -d, L * d), xz,
+                              (L, E2 * L), E2, L, d, b)
             else:
                 _strided_gemm(w, (d, 1, 0), h2, (1, d, L * d), xz, (L, E2 * L), E2, L, d, b)
         ctx.save_for_backward(h2, w)
-        ctx.cfg = (b, L, h.dtype, weight.dtype)
+        ctx.cfg = (b, L, h.dtype, weight.dtype, bool(reverse))
+        ctx.sink = sink
         E = E2 // 2
         return xz[:, :E], xz[:, E:]
 
     @staticmethod
     def backward(ctx, dx, dz):
         h2, w = ctx.saved_tensors
-        b, L, hdt, wdt = ctx.cfg
+        b, L, hdt, wdt, rev = ctx.cfg
+        sink = ctx.sink
         E2, d = w.shape
         E = E2 // 2
         T = b * L
@@ -297,15 +324,20 @@ class InProj(torch.autograd.Function):
         halves = [(i, g.to(dt).contiguous()) for i, g in enumerate((dx, dz)) if g is not None]
         dh = dw = None
         if ctx.needs_input_grad[0]:
-            dh = torch.empty(b, L, d, device=h2.device, dtype=dt)
-            # dh[b][l][j] = sum_c g[b][c][l] W[c][j]: A(m = l, k = c) = g[b][c][l]
+            # dh[b][l'][j] = sum_c g[b][c][l] W[c][j]: A(m = l, k = c) = g[b][c][l]; the rows of
+            # the reverse direction land at l' = L-1-l (C walked backwards from row L-1)
+            acc = sink is not None and sink.dh is not None
+            dh = sink.dh if acc else torch.empty(b, L, d, device=h2.device, dtype=dt)
+            cbase, ldc = (_rows_from_end(dh, b, L, d), -d) if rev else (dh, d)
             if not halves:
-                dh.zero_()
+                if not acc:
+                    dh.zero_()
             elif len(halves) == 2 and dt == torch.bfloat16:
-                with _timed("mamba_proj", (2 * T * E + T * d) * es, "byte"):
+                with _timed("mamba_proj", (2 * T * E + (3 if acc else 1) * T * d) * es, "byte"):
                     N.call("dna_gemm_bf16_strided_cat", halves[0][1].data_ptr(),
                            halves[1][1].data_ptr(), E, 1, L, E * L, w.data_ptr(), d, 1, 0,
-                           dh.data_ptr(), d, L * d, 0, None, None, L, d, E2, b, 1, N.stream_ptr())
+                           cbase.data_ptr(), ldc, L * d, 2 if acc else 0, None, None, L, d, E2,
+                           b, 1, N.stream_ptr())
             else:
                 if len(halves) == 2:  # fp32 parity mode: one operand of both halves
                     g, wi = torch.cat([halves[0][1], halves[1][1]], 1), w
@@ -313,9 +345,17 @@ class InProj(torch.autograd.Function):
                     i, g = halves[0]
                     wi = w[i * E:(i + 1) * E]
                 K = g.shape[1]
-                with _timed("mamba_proj", (T * K + T * d) * es, "byte"):
-                    _strided_gemm(g, (1, L, K * L), wi, (d, 1, 0), dh, (d, L * d), L, d, K, b)
-            dh = dh.to(hdt)
+                with _timed("mamba_proj", (T * K + (3 if acc else 1) * T * d) * es, "byte"):
+                    _strided_gemm(g, (1, L, K * L), wi, (d, 1, 0), cbase, (ldc, L * d), L, d, K,
+                                  b, accumulate=acc)
+            if sink is not None:
+                if acc:
+                    sink.dh = None
+                else:  # the other direction's backward accumulates into it and returns the sum
+                    sink.dh = dh
+                    dh = None
+            if dh is not None:
+                dh = dh.to(hdt)
         if ctx.needs_input_grad[1]:
             if not halves:
                 dw = torch.zeros_like(w, dtype=wdt)
@@ -325,10 +365,11 @@ class InProj(torch.autograd.Function):
                 # half's rows must read as zero
                 alloc = torch.empty if len(halves) == 2 else torch.zeros
                 part = alloc(s * b, E2, d, device=h2.device, dtype=torch.float32)
-                for i, g in halves:  # dW[c][j] = sum_{b,l} g[b][c][l] h[b][l][j]
-                    _wgrad_tokens(g, (L, 1, E * L), h2, (d, 1, L * d), E, d, L, b, part, i * E, E2)
+                hb, sbk = (_rows_from_end(h2, b, L, d), -d) if rev else (h2, d)
+                for i, g in halves:  # dW[c][j] = sum_{b,l} g[b][c][l] h[b][l'][j]
+                    _wgrad_tokens(g, (L, 1, E * L), hb, (sbk, 1, L * d), E, d, L, b, part, i * E, E2)
                 dw = _sum_parts(part, (E2, d), wdt)
-        return dh, dw
+        return dh, dw, None, None
 
 
 class OutProj(torch.autograd.Function):
@@ -337,10 +378,13 @@ class OutProj(torch.autograd.Function):
     F.linear does). All three products on the strided MFMA GEMM: the forward reads y with unit
     token stride (no transpose), the data gradient goes straight into the channel-major
     [b, E, L] layout the scan's backward reads, the weight gradient (contraction over all b*L
-    tokens into [d, E]) as fp32 split-K slices."""
+    tokens into [d, E]) as fp32 split-K slices.
+    into (bf16, the BiMambaWrapper "add" strategy): the reverse direction's output is added to
+    the forward direction's output `into` in place, position l of y landing at L-1-l --
+    `out + mamba_rev(hidden.flip(1)).flip(1)` without the two flips and the add."""
 
     @staticmethod
-    def forward(ctx, y, weight, bias):
+    def forward(ctx, y, weight, bias, into=None):
         _gpu(y, weight)
         b, E, L = y.shape
         if torch.is_autocast_enabled("cuda"):
@@ -355,36 +399,48 @@ class OutProj(torch.autograd.Function):
         w = weight.detach().to(dt).contiguous()
         d = w.shape[0]
         bn = None if bias is None else bias.detach().to(dt).float().contiguous()
-        out = torch.empty(b, L, d, device=y.device, dtype=dt)
-        with _timed("mamba_proj", (b * E * L + b * L * d) * yc.element_size(), "byte"):
-            # out[b][l][o] = sum_e y[b][e][l] W[o][e] (+ bias[o])
-            _strided_gemm(yc, (1, L, yc.stride(0)), w, (1, E, 0), out, (d, L * d), L, d, E, b,
-                          bias_n=bn)
+        if into is not None:
+            if dt != torch.bfloat16 or into.dtype != dt or not into.is_contiguous() or \
+                    into.shape != (b, L, d):
+                raise NotImplementedError("OutProj(into=...): bf16 [b, L, d] contiguous target")
+            out, cbase, ldc = into, _rows_from_end(into, b, L, d), -d
+        else:
+            out = torch.empty(b, L, d, device=y.device, dtype=dt)
+            cbase, ldc = out, d
+        with _timed("mamba_proj", (b * E * L + (3 if into is not None else 1) * b * L * d)
+                    * yc.element_size(), "byte"):
+            # out[b][l'][o] (+)= sum_e y[b][e][l] W[o][e] (+ bias[o])
+            _strided_gemm(yc, (1, L, yc.stride(0)), w, (1, E, 0), cbase, (ldc, L * d), L, d, E, b,
+                          bias_n=bn, accumulate=into is not None)
         ctx.save_for_backward(yc, w)
-        ctx.cfg = (y.dtype, weight.dtype, None if bias is None else bias.dtype)
+        ctx.cfg = (y.dtype, weight.dtype, None if bias is None else bias.dtype, into is not None)
+        if into is not None:
+            ctx.mark_dirty(into)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         yc, w = ctx.saved_tensors
-        ydt, wdt, bdt = ctx.cfg
+        ydt, wdt, bdt, rev = ctx.cfg
         b, E, L = yc.shape
         d = w.shape[0]
         dt = yc.dtype
         dout = dout.to(dt).contiguous()
+        # the reverse direction's output rows are l' = L-1-l: its dout is read backwards
+        db_, sd = (_rows_from_end(dout, b, L, d), -d) if rev else (dout, d)
         dy = dw = db = None
         with torch.autocast("cuda", enabled=False):
-            if ctx.needs_input_grad[0]:  # dy[b][e][l] = sum_o W[o][e] dout[b][l][o], channel-major
+            if ctx.needs_input_grad[0]:  # dy[b][e][l] = sum_o W[o][e] dout[b][l'][o], channel-major
                 dy = torch.empty(b, E, L, device=dout.device, dtype=dt)
-                DF.strided_gemm(w, (1, E, 0), dout, (1, d, L * d), dy, (L, E * L), E, L, d, b)
+                DF.strided_gemm(w, (1, E, 0), db_, (1, sd, L * d), dy, (L, E * L), E, L, d, b)
                 dy = dy.to(ydt)
-            if ctx.needs_input_grad[1]:  # dW[o][e] = sum_{b,l} dout[b][l][o] y[b][e][l]
-                part, _ = _wgrad_tokens(dout, (1, d, L * d), yc, (1, yc.stride(1), yc.stride(0)),
+            if ctx.needs_input_grad[1]:  # dW[o][e] = sum_{b,l} dout[b][l'][o] y[b][e][l]
+                part, _ = _wgrad_tokens(db_, (1, sd, L * d), yc, (1, yc.stride(1), yc.stride(0)),
                                         d, E, L, b)
                 dw = _sum_parts(part, (d, E), wdt)
             if bdt is not None and ctx.needs_input_grad[2]:
                 db = dout.float().sum((0, 1)).to(bdt)
-        return dy, dw, db
+        return dy, dw, db, (dout if rev else None)
 
 
 class Mamba(nn.Module):
@@ -434,12 +490,17 @@ class Mamba(nn.Module):
         # profiles/r02/session4/cfge_*linear.txt)
         self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **fk)
 
-    def forward(self, hidden_states, inference_params=None):
+    def forward(self, hidden_states, inference_params=None, reverse=False, out_into=None,
+                dh_sink=None):
+        """reverse + out_into (bf16 autocast): run on hidden_states read backwards and add the
+        output, flipped back, into out_into in place; dh_sink: see DhSink (BiMambaWrapper)."""
         if inference_params is not None:
             raise NotImplementedError("Mamba: inference_params (recurrent decoding)")
+        if reverse != (out_into is not None):
+            raise ValueError("Mamba: reverse goes with out_into (the flipped-back accumulation)")
         batch, seqlen, _ = hidden_states.shape
         # in_proj computed channel-major, as the reference does (W @ x^T -> [b, 2E, l])
-        x, z = InProj.apply(hidden_states, self.in_proj.weight)
+        x, z = InProj.apply(hidden_states, self.in_proj.weight, reverse, dh_sink)
         if self.in_proj.bias is not None:
             bx, bz = self.in_proj.bias.chunk(2)
             x, z = x + bx.to(x.dtype)[:, None], z + bz.to(z.dtype)[:, None]
@@ -456,7 +517,7 @@ class Mamba(nn.Module):
         Bm, Cm = x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
         y = SelectiveScan.apply(x, dt, A, Bm, Cm, self.D.float(), z.contiguous(),
                                 self.dt_proj.bias.float(), True, False, sink)
-        return OutProj.apply(y, self.out_proj.weight, self.out_proj.bias)
+        return OutProj.apply(y, self.out_proj.weight, self.out_proj.bias, out_into)
 
 
 class FlipL(torch.autograd.Function):
@@ -516,7 +577,19 @@ class BiMambaWrapper(nn.Module):
         else:
             self.mamba_rev = None
 
+    def _fused_add(self, hidden_states):
+        # both directions on the reversed-read / in-place-accumulate projections: no flipped
+        # copies of the input, the output or their gradients, no add kernels (bf16 autocast)
+        return (self.bidirectional and self.bidirectional_strategy == "add"
+                and hidden_states.is_cuda and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16
+                and os.environ.get("DNA_BIMAMBA_FUSED", "1") != "0")
+
     def forward(self, hidden_states, inference_params=None):
+        if inference_params is None and self._fused_add(hidden_states):
+            sink = DhSink()
+            out = self.mamba_fwd(hidden_states, dh_sink=sink)
+            return self.mamba_rev(hidden_states, reverse=True, out_into=out, dh_sink=sink)
         out = self.mamba_fwd(hidden_states, inference_params=inference_params)
         if self.bidirectional:
             out_rev = flip_l(self.mamba_rev(flip_l(hidden_states), inference_params=inference_params))

@@ -271,13 +271,15 @@ int dna_gemm_bf16_strided(const void* A, long long sam, long long sak, long long
                           void* C, long long ldc, long long scz, int out_f32,
                           const float* bias_m, const float* bias_n, int M, int N, int K,
                           int batch, int splits, void* stream);
-/* C[z][c][l] = sum_{j<K} W[c][j] X[z][l][j] (+ bias[c], fp32): a channel-major projection of a
+/* C[z][c][l] = sum_{j<K} W[c][j] X[z][l'][j] (+ bias[c], fp32), l' = l (reverse == 0) or
+ * N-1-l (reverse: the BiMamba reverse direction reads the sequence backwards instead of flipping
+ * it in memory): a channel-major projection of a
  * token-major input (bf16; K in {64, 128, 256}, W / X 16-B aligned, C [batch][M][N]) with the
  * weight held in registers and X streamed: the Mamba in_proj forward, `in_proj.weight @
  * rearrange(hidden, "b l d -> d (b l)")` (mamba_ssm Mamba.forward under
  * modeling_caduceus.py:88-91). csrc/proj_cm.hip. */
 int dna_proj_cm_bf16(const void* W, const void* X, const float* bias, int M, int N, int K,
-                     int batch, void* C, void* stream);
+                     int batch, int reverse, void* C, void* stream);
 /* The same product with the contraction split over two A operands of equal strides:
  * C = [A | A2] . B, A supplying k < K1 and A2 k in [K1, K) (K1 % 32 == 0). Replaces the
  * mm + addmm pair of the Mamba in_proj data gradient (dh = g_x^T W_x + g_z^T W_z,

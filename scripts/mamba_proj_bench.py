@@ -64,7 +64,7 @@ def main():
                               bytes=(T * d + E2 * d + E2 * T) * 2)
     from dna_amd import _native as N
     xz_p = torch.empty(1, E2, L, device=dev, dtype=bf)
-    f_p = lambda: N.call("dna_proj_cm_bf16", W.data_ptr(), h.data_ptr(), None, E2, L, d, 1,
+    f_p = lambda: N.call("dna_proj_cm_bf16", W.data_ptr(), h.data_ptr(), None, E2, L, d, 1, 0,
                          xz_p.data_ptr(), N.stream_ptr())
     res["in_proj_fwd_proj_cm"] = dict(torch_us=res["in_proj_fwd"]["torch_us"],
                                       hip_us=timeit(f_p, a.iters),

@@ -134,3 +134,31 @@ def test_mamba_block_bf16_grads_track_fp32():
     names = ["h"] + [n for n, _ in m.named_parameters()]
     for n, a, b in zip(names, *grads):
         assert _rel(b, a) < 5e-2, (n, _rel(b, a))
+
+
+@pytest.mark.parametrize("b,l,bias", [(1, 2048, False), (2, 1000, True)])
+def test_bimamba_fused_reverse_equals_flips(b, l, bias, monkeypatch):
+    """BiMambaWrapper "add" under bf16 autocast: the fused form (reverse direction reads the
+    hidden states backwards, adds its output flipped back in place, the two dh accumulate in one
+    buffer) against the flip / add form of the same module -- outputs and every gradient agree
+    to bf16 rounding (the fused sums round once fewer)."""
+    from dna_amd.mamba import BiMambaWrapper
+    torch.manual_seed(b * 100 + l)
+    m = BiMambaWrapper(d_model=64, bidirectional=True, bidirectional_strategy="add",
+                       d_state=16, bias=bias).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    h = torch.randn(b, l, 64, device=DEV, generator=g)
+    dy = torch.randn(b, l, 64, device=DEV, generator=g)
+    res = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DNA_BIMAMBA_FUSED", fused)
+        m.zero_grad(set_to_none=True)
+        hg = h.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(hg)
+        y.float().backward(dy)
+        res.append([y.float()] + [hg.grad.float()] +
+                   [p.grad.float() for _, p in m.named_parameters()])
+    names = ["out", "h"] + [n for n, _ in m.named_parameters()]
+    for n, a, c in zip(names, *res):
+        assert _rel(c, a) < 2e-2, (n, _rel(c, a))

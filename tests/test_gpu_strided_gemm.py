@@ -118,7 +118,7 @@ def test_proj_cm_vs_fp32(M, N_, K, batch, bias):
     b = torch.randn(M, device=DEV, generator=g) if bias else None
     C = torch.full((batch, M, N_), float("nan"), device=DEV, dtype=torch.bfloat16)
     N.call("dna_proj_cm_bf16", W.data_ptr(), X.data_ptr(), None if b is None else b.data_ptr(),
-           M, N_, K, batch, C.data_ptr(), N.stream_ptr())
+           M, N_, K, batch, 0, C.data_ptr(), N.stream_ptr())
     ref = torch.einsum("ck,zlk->zcl", W.float(), X.float())
     if b is not None:
         ref = ref + b[None, :, None]
@@ -129,7 +129,7 @@ def test_proj_cm_vs_fp32(M, N_, K, batch, bias):
 
 def test_proj_cm_rejects_bad_k():
     with pytest.raises(N.NativeError, match="K=96"):
-        N.call("dna_proj_cm_bf16", 16, 16, None, 64, 64, 96, 1, 16, None)
+        N.call("dna_proj_cm_bf16", 16, 16, None, 64, 64, 96, 1, 0, 16, None)
 
 
 @pytest.mark.parametrize("M,N_,K,batch", [(512, 4096, 48, 1), (64, 301, 16, 2)])
