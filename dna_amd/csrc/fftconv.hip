@@ -602,7 +602,8 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
   const int p = blockIdx.y;
   make_table(tw, g.logM1);
   bt.init(g.logN);
-  __syncthreads();
+  // the tables' barrier comes after this block's column loads are issued (both from L2 / HBM:
+  // a barrier in between serialised the two latencies, ~16 us of the 100-us pass at config D)
   const cf* src = ws + ((size_t)p << g.logN);
   const uint32_t mask = (1u << g.logN) - 1;
   if constexpr (LN == 17) {
@@ -618,6 +619,7 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
     cf v[16];
 #pragma unroll
     for (int mb = 0; mb < 16; ++mb) v[mb] = src[(size_t)(ma + 16 * mb) * M2 + n2];
+    __syncthreads();  // twiddle tables
     cf tq[4], sr[4];
     big16(bt, n2, (uint32_t)ma, mask, tq, sr);
 #pragma unroll
@@ -649,6 +651,7 @@ __global__ FFT_BOUNDS void col_inv_kernel(const cf* __restrict__ ws, Pairing pr,
       const int k1 = e >> lcw, c = e & (cw - 1);
       if (e < cw * M1) v[it] = src[(size_t)k1 * M2 + n20 + c];
     }
+    __syncthreads();  // twiddle tables
 #pragma unroll
     for (int it = 0; it < PPT; ++it) {
       const int e = threadIdx.x + it * NTH;
