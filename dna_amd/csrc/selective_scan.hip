@@ -24,6 +24,7 @@ namespace dna {
 namespace ssm {
 
 constexpr int ITEMS = 8;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 constexpr int CHUNK = 64 * ITEMS;
 constexpr int WPB = 4;  // waves (channels) per block
 
@@ -1036,67 +1037,97 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) dy[i] = go[i];
     }
-    float ddl[ITEMS], gB[ITEMS], y[ITEMS], dlu[ITEMS];
+    // Per-position arrays as pairs (items 2j, 2j+1): every update that is not a chain over the
+    // positions runs as one v_pk_fma / v_pk_mul per pair (CDNA packed fp32: 2 lanes' worth per
+    // issue), and the pairs sit in aligned register pairs, so no shuffles around them.
+    f32x2 ddl2[ITEMS / 2], gB2[ITEMS / 2], y2[ITEMS / 2], dlu2[ITEMS / 2], dl2[ITEMS / 2],
+        dy2[ITEMS / 2];
     float dDacc = 0.f, dAl = 0.f, tl = 0.f;
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      ddl[i] = 0.f; gB[i] = 0.f; y[i] = 0.f; dDacc = fmaf(dy[i], uu[i], dDacc);
-      dlu[i] = dl[i] * uu[i]; tl += dl[i];
+    for (int j = 0; j < ITEMS / 2; ++j) {
+      dl2[j] = f32x2{dl[2 * j], dl[2 * j + 1]};
+      dy2[j] = f32x2{dy[2 * j], dy[2 * j + 1]};
+      ddl2[j] = f32x2{0.f, 0.f}; gB2[j] = f32x2{0.f, 0.f}; y2[j] = f32x2{0.f, 0.f};
+      dlu2[j] = dl2[j] * f32x2{uu[2 * j], uu[2 * j + 1]};
     }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) { dDacc = fmaf(dy[i], uu[i], dDacc); tl += dl[i]; }
     // one state's share of the backward (its dB / dC accumulator row is this wave's alone in the
     // current step)
     auto state = [&](const int n) __attribute__((always_inline)) {
-      float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS], xs[ITEMS];
+      float Bv[ITEMS], Cv[ITEMS];
       lds8f(Bs + n * CHUNK, lane, Bv);
       lds8f(Cs + n * CHUNK, lane, Cv);
+      f32x2 Bv2[ITEMS / 2], Cv2[ITEMS / 2], aa2[ITEMS / 2], bb2[ITEMS / 2], xs2[ITEMS / 2];
+#pragma unroll
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        Bv2[j] = f32x2{Bv[2 * j], Bv[2 * j + 1]};
+        Cv2[j] = f32x2{Cv[2 * j], Cv[2 * j + 1]};
+      }
       // the state's dB / dC accumulator rows, read up front so the LDS round trips overlap the
       // scans instead of serialising read -> fma -> write at the end (occupancy is LDS-bound at
       // 2 waves / SIMD, so the 16 extra VGPRs are free)
       float* aB = accw + n * CHUNK + lane;
       float* aC = aB + N * CHUNK;
-      float rB[ITEMS], rC[ITEMS];
+      f32x2 rB2[ITEMS / 2], rC2[ITEMS / 2];
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) { rB[i] = aB[i * 64]; rC[i] = aC[i * 64]; }
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        rB2[j] = f32x2{aB[(2 * j) * 64], aB[(2 * j + 1) * 64]};
+        rC2[j] = f32x2{aC[(2 * j) * 64], aC[(2 * j + 1) * 64]};
+      }
       const float An = bcast(Al, n), An2 = An * LOG2E;
       const float Pt = ex2(tl * An2);  // prod_i a_i, for both directions
+#pragma unroll
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        const f32x2 t = dl2[j] * An2;
+        aa2[j] = f32x2{ex2(t.x), ex2(t.y)};
+        bb2[j] = dlu2[j] * Bv2[j];
+      }
       float P = Pt, S = 0.f;
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        aa[i] = ex2(dl[i] * An2);
-        bb[i] = dlu[i] * Bv[i];
-        S = fmaf(aa[i], S, bb[i]);
-      }
+      for (int i = 0; i < ITEMS; ++i) S = fmaf(aa2[i >> 1][i & 1], S, bb2[i >> 1][i & 1]);
       float Pr = Pt, Sr = 0.f;
 #pragma unroll
-      for (int i = ITEMS - 1; i >= 0; --i) Sr = aa[i] * fmaf(Cv[i], dy[i], Sr);
+      for (int i = ITEMS - 1; i >= 0; --i)
+        Sr = aa2[i >> 1][i & 1] * fmaf(Cv2[i >> 1][i & 1], dy2[i >> 1][i & 1], Sr);
       scan_both(P, S, Pr, Sr, lane);
       const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
       const float xprev = fmaf(Pe, bcast(xcl, n), Se);
       float x = xprev;
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        x = fmaf(aa[i], x, bb[i]);
-        xs[i] = x;
-        y[i] = fmaf(Cv[i], x, y[i]);
+        x = fmaf(aa2[i >> 1][i & 1], x, bb2[i >> 1][i & 1]);
+        xs2[i >> 1][i & 1] = x;
       }
+#pragma unroll
+      for (int j = 0; j < ITEMS / 2; ++j) y2[j] = Cv2[j] * xs2[j] + y2[j];
       const float Pn = shl1(Pr, 1.f), Sn = shl1(Sr, 0.f);
       float h = fmaf(Pn, bcast(hcl, n), Sn);
-      float dAn = 0.f;
+      // the reverse chain (g_i = C_i dy_i + h_{i+1}, h_i = a_i g_i) is serial; everything that
+      // consumes g runs packed after it. a_i x_{i-1} = x_i - b_i (x_i = a_i x_{i-1} + b_i)
+      f32x2 g2[ITEMS / 2];
 #pragma unroll
       for (int i = ITEMS - 1; i >= 0; --i) {
-        const float g = fmaf(Cv[i], dy[i], h);
-        const float xm1 = i > 0 ? xs[i - 1] : xprev;
-        const float da = g * xm1 * aa[i];
-        ddl[i] = fmaf(da, An, ddl[i]);
-        dAn = fmaf(da, dl[i], dAn);
-        gB[i] = fmaf(g, Bv[i], gB[i]);   // d/dδ and d/du through B: g B (u resp. δ) after the loop
-        rB[i] = fmaf(g, dlu[i], rB[i]);   // rows exclusive this step (state rotation above)
-        rC[i] = fmaf(dy[i], xs[i], rC[i]);
-        h = aa[i] * g;
+        const float g = fmaf(Cv2[i >> 1][i & 1], dy2[i >> 1][i & 1], h);
+        g2[i >> 1][i & 1] = g;
+        h = aa2[i >> 1][i & 1] * g;
+      }
+      f32x2 dAn2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        const f32x2 da = g2[j] * (xs2[j] - bb2[j]);
+        ddl2[j] = da * An + ddl2[j];
+        dAn2 = da * dl2[j] + dAn2;
+        gB2[j] = g2[j] * Bv2[j] + gB2[j];  // d/dδ and d/du through B: g B (u resp. δ) after the loop
+        rB2[j] = g2[j] * dlu2[j] + rB2[j];  // rows exclusive this step (state rotation above)
+        rC2[j] = dy2[j] * xs2[j] + rC2[j];
       }
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) { aB[i * 64] = rB[i]; aC[i * 64] = rC[i]; }
-      const float dAs = wsum(dAn);
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        aB[(2 * j) * 64] = rB2[j].x; aB[(2 * j + 1) * 64] = rB2[j].y;
+        aC[(2 * j) * 64] = rC2[j].x; aC[(2 * j + 1) * 64] = rC2[j].y;
+      }
+      const float dAs = wsum(dAn2.x + dAn2.y);
       if (lane == n) dAl = dAs;
     };
     if constexpr (R == 1 && N / 2 >= CW) {
@@ -1119,8 +1150,9 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
     float dd[ITEMS], du[ITEMS], dbacc = 0.f;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      du[i] = fmaf(gB[i], dl[i], Dd * dy[i]);
-      float g = fmaf(gB[i], uu[i], ddl[i]);
+      const float gBi = gB2[i >> 1][i & 1];
+      du[i] = fmaf(gBi, dl[i], Dd * dy[i]);
+      float g = fmaf(gBi, uu[i], ddl2[i >> 1][i & 1]);
       if (a.softplus) g *= sigmoidf(dr[i] + bias);
       dd[i] = (pos + i < a.len) ? g : 0.f;
       dbacc += dd[i];
@@ -1132,7 +1164,7 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
         const float s = sigmoidf(zz[i]);
-        const float pre = fmaf(Dd, uu[i], y[i]);
+        const float pre = fmaf(Dd, uu[i], y2[i >> 1][i & 1]);
         dzv[i] = go[i] * pre * s * (1.f + zz[i] * (1.f - s));
       }
       store8x<VEC>((T*)a.dz + off, pos, a.len, dzv);
