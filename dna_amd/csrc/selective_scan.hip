@@ -699,8 +699,14 @@ __global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
       lds8f(Bs + n * CHUNK, lane, Bv);
       const float An = bcast(Al, n), An2 = An * LOG2E;
       float x = 0.f;
+      f32x2 e2[ITEMS / 2], b2[ITEMS / 2];  // packed fp32 pairs for the non-chain products
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) x = fmaf(ex2(dl[i] * An2), x, uu[i] * Bv[i]);
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        e2[j] = f32x2{dl[2 * j], dl[2 * j + 1]} * An2;
+        b2[j] = f32x2{uu[2 * j], uu[2 * j + 1]} * f32x2{Bv[2 * j], Bv[2 * j + 1]};
+      }
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) x = fmaf(ex2(e2[i >> 1][i & 1]), x, b2[i >> 1][i & 1]);
       Sv[n] = x * ex2(An2 * suf);
       // keep the unrolled states' LDS reads from all being hoisted (VGPRs -> occupancy)
       if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
@@ -764,8 +770,11 @@ __global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
       lds8f(Cs + n * CHUNK, lane, Cv);
       const float An = bcast(Al, n), An2 = An * LOG2E;
       float r = 0.f;
+      f32x2 e2[ITEMS / 2];
 #pragma unroll
-      for (int i = ITEMS - 1; i >= 0; --i) r = ex2(dl[i] * An2) * fmaf(Cv[i], dy[i], r);
+      for (int j = 0; j < ITEMS / 2; ++j) e2[j] = f32x2{dl[2 * j], dl[2 * j + 1]} * An2;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) r = ex2(e2[i >> 1][i & 1]) * fmaf(Cv[i], dy[i], r);
       Rv[n] = r * ex2(An2 * pre);
       if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
@@ -904,38 +913,55 @@ __global__ __launch_bounds__(CT) void chunk_fwd_kernel(Args a, Chunked q) {
     const int ch = b * a.dim + d;
     const size_t off = (size_t)ch * a.len;
     const float Al = nx.Al, Dd = nx.Dd, bias = nx.bias, xcl = nx.xcl;
-    float uu[ITEMS], dl[ITEMS], y[ITEMS], zz[ITEMS];
+    float uu[ITEMS], dl[ITEMS], zz[ITEMS];
     nx.u.get(uu);
     nx.dl.get(dl);
     if (a.z) nx.z.get(zz);
     if constexpr (VEC) fetch(nx, j + 1 < q.k ? j + 1 : j);
     else if (j + 1 < q.k) fetch(nx, j + 1);
     prep_delta(dl, bias, a.softplus, pos, a.len);
-    float du_[ITEMS], tl = 0.f;  // delta * u and the lane's delta sum (state-independent)
+    // delta * u and the lane's delta sum (state-independent); per-position pairs as packed fp32
+    // (see chunk_bwd_kernel)
+    f32x2 du2[ITEMS / 2], dl2[ITEMS / 2], y2[ITEMS / 2];
+    float tl = 0.f;
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) { y[i] = 0.f; du_[i] = dl[i] * uu[i]; tl += dl[i]; }
+    for (int j = 0; j < ITEMS / 2; ++j) {
+      dl2[j] = f32x2{dl[2 * j], dl[2 * j + 1]};
+      du2[j] = dl2[j] * f32x2{uu[2 * j], uu[2 * j + 1]};
+      y2[j] = f32x2{0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) tl += dl[i];
 #pragma unroll 2
     for (int n = 0; n < N; ++n) {
-      float Bv[ITEMS], Cv[ITEMS], aa[ITEMS], bb[ITEMS];
+      float Bv[ITEMS], Cv[ITEMS];
       lds8f(Bs + n * CHUNK, lane, Bv);
       lds8f(Cs + n * CHUNK, lane, Cv);
+      f32x2 aa2[ITEMS / 2], bb2[ITEMS / 2], xs2[ITEMS / 2];
       const float An = bcast(Al, n), An2 = An * LOG2E;
       float P = ex2(tl * An2), S = 0.f;  // prod_i exp(dl_i A) = exp(A sum_i dl_i)
 #pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        aa[i] = ex2(dl[i] * An2);
-        bb[i] = du_[i] * Bv[i];
-        S = fmaf(aa[i], S, bb[i]);
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        const f32x2 t = dl2[j] * An2;
+        aa2[j] = f32x2{ex2(t.x), ex2(t.y)};
+        bb2[j] = du2[j] * f32x2{Bv[2 * j], Bv[2 * j + 1]};
       }
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) S = fmaf(aa2[i >> 1][i & 1], S, bb2[i >> 1][i & 1]);
       scan_fwd(P, S, lane);
       const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
       float x = fmaf(Pe, bcast(xcl, n), Se);
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        x = fmaf(aa[i], x, bb[i]);
-        y[i] = fmaf(Cv[i], x, y[i]);
+        x = fmaf(aa2[i >> 1][i & 1], x, bb2[i >> 1][i & 1]);
+        xs2[i >> 1][i & 1] = x;
       }
+#pragma unroll
+      for (int j = 0; j < ITEMS / 2; ++j) y2[j] = f32x2{Cv[2 * j], Cv[2 * j + 1]} * xs2[j] + y2[j];
     }
+    float y[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) y[i] = y2[i >> 1][i & 1];
     float o[ITEMS];
     if (a.z) {
 #pragma unroll
