@@ -692,22 +692,35 @@ __global__ __launch_bounds__(CT) void sum_fwd_kernel(Args a, Chunked q) {
     for (int i = 0; i < ITEMS; ++i) { tl += dl[i]; uu[i] *= dl[i]; }  // uu <- δ u
     float pre, suf, tot;
     delta_sums(tl, lane, pre, suf, tot);
+    // The chunk summary S_n = sum_p exp(A_n sd_p) δ_p u_p B_n,p, sd_p = the δ summed over the
+    // chunk positions after p: the product of the a_j after p is the exp of their δ sum, so each
+    // position's term takes one exp (as the a_p of the chain form did) and no recurrence -- every
+    // product runs on packed fp32 pairs of positions.
+    f32x2 sd2[ITEMS / 2], du2[ITEMS / 2];
+    {
+      float sd[ITEMS], run = suf;
+#pragma unroll
+      for (int i = ITEMS - 1; i >= 0; --i) { sd[i] = run; run += dl[i]; }
+#pragma unroll
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        sd2[j] = f32x2{sd[2 * j], sd[2 * j + 1]};
+        du2[j] = f32x2{uu[2 * j], uu[2 * j + 1]};
+      }
+    }
     float Sv[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       float Bv[ITEMS];
       lds8f(Bs + n * CHUNK, lane, Bv);
-      const float An = bcast(Al, n), An2 = An * LOG2E;
-      float x = 0.f;
-      f32x2 e2[ITEMS / 2], b2[ITEMS / 2];  // packed fp32 pairs for the non-chain products
+      const float An2 = bcast(Al, n) * LOG2E;
+      f32x2 acc = f32x2{0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < ITEMS / 2; ++j) {
-        e2[j] = f32x2{dl[2 * j], dl[2 * j + 1]} * An2;
-        b2[j] = f32x2{uu[2 * j], uu[2 * j + 1]} * f32x2{Bv[2 * j], Bv[2 * j + 1]};
+        const f32x2 t = sd2[j] * An2;
+        const f32x2 e = f32x2{ex2(t.x), ex2(t.y)};
+        acc = e * (du2[j] * f32x2{Bv[2 * j], Bv[2 * j + 1]}) + acc;
       }
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) x = fmaf(ex2(e2[i >> 1][i & 1]), x, b2[i >> 1][i & 1]);
-      Sv[n] = x * ex2(An2 * suf);
+      Sv[n] = acc.x + acc.y;
       // keep the unrolled states' LDS reads from all being hoisted (VGPRs -> occupancy)
       if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
@@ -763,19 +776,33 @@ __global__ __launch_bounds__(CT) void sum_bwd_kernel(Args a, Chunked q) {
     for (int i = 0; i < ITEMS; ++i) tl += dl[i];
     float pre, suf, tot;
     delta_sums(tl, lane, pre, suf, tot);
+    // R_n = sum_p exp(A_n pd_p) C_n,p dy_p, pd_p = the δ summed over the chunk positions up to
+    // and including p (see sum_fwd_kernel: one exp per position and state, no recurrence)
+    f32x2 pd2[ITEMS / 2], dy2[ITEMS / 2];
+    {
+      float pd[ITEMS], run = pre;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) { run += dl[i]; pd[i] = run; }
+#pragma unroll
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        pd2[j] = f32x2{pd[2 * j], pd[2 * j + 1]};
+        dy2[j] = f32x2{dy[2 * j], dy[2 * j + 1]};
+      }
+    }
     float Rv[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       float Cv[ITEMS];
       lds8f(Cs + n * CHUNK, lane, Cv);
-      const float An = bcast(Al, n), An2 = An * LOG2E;
-      float r = 0.f;
-      f32x2 e2[ITEMS / 2];
+      const float An2 = bcast(Al, n) * LOG2E;
+      f32x2 acc = f32x2{0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < ITEMS / 2; ++j) e2[j] = f32x2{dl[2 * j], dl[2 * j + 1]} * An2;
-#pragma unroll
-      for (int i = ITEMS - 1; i >= 0; --i) r = ex2(e2[i >> 1][i & 1]) * fmaf(Cv[i], dy[i], r);
-      Rv[n] = r * ex2(An2 * pre);
+      for (int j = 0; j < ITEMS / 2; ++j) {
+        const f32x2 t = pd2[j] * An2;
+        const f32x2 e = f32x2{ex2(t.x), ex2(t.y)};
+        acc = (e * f32x2{Cv[2 * j], Cv[2 * j + 1]}) * dy2[j] + acc;
+      }
+      Rv[n] = acc.x + acc.y;
       if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     const float R = reduce_states<N>(Rv, lane);
