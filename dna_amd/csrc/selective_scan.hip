@@ -251,6 +251,19 @@ __device__ __forceinline__ float prefix_sum(float v) {
   return v;
 }
 __device__ __forceinline__ float wsum(float v) { return bcast(prefix_sum(v), 63); }
+// two wave sums at once: one permlane32 exchange leaves the partial sums of a in lanes 0-31 and
+// of b in lanes 32-63, then one 32-lane reduction serves both (9 instructions instead of 14)
+__device__ __forceinline__ void wsum2(float a, float b, float& ta, float& tb) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  v += dpp<0x111>(0.f, v);
+  v += dpp<0x112>(0.f, v);
+  v += dpp<0x114>(0.f, v);
+  v += dpp<0x118>(0.f, v);
+  v += dpp<0x142, 0xA>(0.f, v);  // rows 1, 3 += lane 15 / 47
+  ta = bcast(v, 31);
+  tb = bcast(v, 63);
+}
 
 // N per-lane values v[n] (one per state) summed over the wave at once, transposed: each
 // exchange step halves the values a lane carries by pairing value k with k + half across lane
@@ -1107,7 +1120,8 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
     for (int i = 0; i < ITEMS; ++i) { dDacc = fmaf(dy[i], uu[i], dDacc); tl += dl[i]; }
     // one state's share of the backward (its dB / dC accumulator row is this wave's alone in the
     // current step)
-    auto state = [&](const int n) __attribute__((always_inline)) {
+    // dAp: this lane's share of dA for state n (summed over the wave by the caller)
+    auto state = [&](const int n, float& dAp) __attribute__((always_inline)) {
       float Bv[ITEMS], Cv[ITEMS];
       lds8f(Bs + n * CHUNK, lane, Bv);
       lds8f(Cs + n * CHUNK, lane, Cv);
@@ -1180,8 +1194,7 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
         aB[(2 * j) * 64] = rB2[j].x; aB[(2 * j + 1) * 64] = rB2[j].y;
         aC[(2 * j) * 64] = rC2[j].x; aC[(2 * j + 1) * 64] = rC2[j].y;
       }
-      const float dAs = wsum(dAn2.x + dAn2.y);
-      if (lane == n) dAl = dAs;
+      dAp = dAn2.x + dAn2.y;
     };
     if constexpr (R == 1 && N / 2 >= CW) {
       // two states per step (wave w: states 2((st + w) mod N/2) and + 1, still one writer per
@@ -1189,14 +1202,22 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
 #pragma unroll 1
       for (int st = 0; st < N / 2; ++st) {
         const int n0 = 2 * ((st + w) % (N / 2));
-        state(n0);
-        state(n0 + 1);
+        float p0, p1, s0, s1;
+        state(n0, p0);
+        state(n0 + 1, p1);
+        wsum2(p0, p1, s0, s1);
+        if (lane == n0) dAl = s0;
+        if (lane == n0 + 1) dAl = s1;
         __syncthreads();
       }
     } else {
 #pragma unroll 1
       for (int st = 0; st < N; ++st) {
-        state((st + w) % N);
+        const int n = (st + w) % N;
+        float p;
+        state(n, p);
+        const float sn = wsum(p);
+        if (lane == n) dAl = sn;
         __syncthreads();
       }
     }
@@ -1223,8 +1244,7 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
       store8x<VEC>((T*)a.dz + off, pos, a.len, dzv);
     }
     if (lane < N) atomicAdd(a.dA + d * N + lane, dAl);
-    dDacc = wsum(dDacc);
-    dbacc = wsum(dbacc);
+    wsum2(dDacc, dbacc, dDacc, dbacc);
     if (lane == 0) {
       if (a.dD) atomicAdd(a.dD + d, dDacc);
       if (a.ddelta_bias) atomicAdd(a.ddelta_bias + d, dbacc);
