@@ -46,6 +46,13 @@ _SIGS = {
     "dna_hyena_gate_out_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _sz, _vp, _vp, _vp]),
     "dna_hyena_modulate_t_fwd": (_i, [_vp, _i, _vp, _vp, _f, _i, _i, _i, _vp, _vp]),
     "dna_hyena_modulate_t_bwd": (_i, [_vp, _vp, _vp, _f, _i, _i, _i, _vp, _i, _vp]),
+    "dna_hyena_filter_part_elems": (_i, [_i, _i, _i, _i]),
+    "dna_hyena_filter_part_stride": (_i, [_i, _i, _i]),
+    "dna_hyena_filter_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _f, _i, _i, _i, _i,
+                                  _vp, _vp]),
+    "dna_hyena_filter_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _f, _i, _i, _i, _i,
+                                  _vp, _vp, _vp, _vp]),
+    "dna_hyena_filter_finish": (_i, [_vp, _i, _i, _i, _vp, _vp]),
     "dna_ln_fwd": (_i, [_vp, _i, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _i, _i, _f, _vp, _vp,
                         _vp, _vp, _vp]),
     "dna_ln_bwd_workspace": (_sz, [_i, _i]),

@@ -8,6 +8,7 @@ Mirrors `fftconv_ref(u, k, D, dropout_mask, gelu=True, k_rev=None, bidirectional
 kernels of dna_amd/csrc/fftconv.hip (four-step FFT of size 2L, fp32 internally); there is no CPU
 or torch.fft fallback -- without the native library or a GPU tensor this raises.
 """
+import ctypes
 import math
 import os
 
@@ -346,6 +347,103 @@ class ModulateT(torch.autograd.Function):
         return dh, None, None, None, None
 
 
+_FILTER_FUSED = os.environ.get("DNA_HYENA_FILTER_FUSED", "1") != "0"  # A/B switch
+
+
+def _ptr_array(ts):
+    arr = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+    return arr, ctypes.addressof(arr)
+
+
+class FilterMLP(torch.autograd.Function):
+    """HyenaFilter.filter_t under bf16 autocast as two kernels (csrc/hyena_filter.hip): the
+    positional MLP Linear(E, 64) -> Sin -> [Linear(64, 64) -> Sin] x 2 -> Linear(64, C), the
+    ExponentialModulation and the transpose to the long convolution's k [O][C / O][L] in one
+    forward launch; the backward recomputes the MLP per 64-position tile and leaves per-block
+    weight-gradient partials for one dna_sum_slices. Same dtype flow as the module path under
+    autocast (reference hyena.py:162-247 with torch's autocast casts): bf16 Linear operands and
+    outputs, fp32 Sin, dW / db rounded to bf16 once after the fp32 sum, the freq gradient fp32."""
+
+    @staticmethod
+    def forward(ctx, z, tpos, deltas, shift, O, w1, b1, w4, freq, *inner):
+        _gpu(z, w1, w4)
+        L, E = z.shape
+        C = w4.shape[0]
+        wi, bi = list(inner[0::2]), list(inner[1::2])
+        NI = len(wi)
+        k = torch.empty(O, C // O, L, device=z.device, dtype=torch.float32)
+        wa, wp = _ptr_array(wi)
+        ba, bp = _ptr_array(bi)
+        with _timed("hyena_filter_fwd", L * (E + C) * 4, "byte"):
+            N.call("dna_hyena_filter_fwd", z.data_ptr(), w1.data_ptr(), b1.data_ptr(), wp, bp, NI,
+                   w4.data_ptr(), freq.data_ptr(), tpos.data_ptr(), deltas.data_ptr(), float(shift), L,
+                   E, C, O, k.data_ptr(), N.stream_ptr())
+        ctx.save_for_backward(z, tpos, deltas, w1, b1, w4, freq, *inner)
+        ctx.cfg = (float(shift), O, NI)
+        return k
+
+    @staticmethod
+    def backward(ctx, dk):
+        z, tpos, deltas, w1, b1, w4, freq, *inner = ctx.saved_tensors
+        shift, O, NI = ctx.cfg
+        wi, bi = list(inner[0::2]), list(inner[1::2])
+        L, E = z.shape
+        C = w4.shape[0]
+        F_ = w1.shape[0]
+        dk = dk.contiguous().float()
+        lib = N.lib()
+        total = int(lib.dna_hyena_filter_part_elems(L, E, NI, C))
+        P = int(lib.dna_hyena_filter_part_stride(E, NI, C))
+        part = torch.empty(total, device=dk.device, dtype=torch.float32)
+        dz = torch.empty(L, E, device=dk.device, dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        wa, wp = _ptr_array(wi)
+        ba, bp = _ptr_array(bi)
+        with _timed("hyena_filter_bwd", L * (E + C) * 4, "byte"):
+            N.call("dna_hyena_filter_bwd", z.data_ptr(), w1.data_ptr(), b1.data_ptr(), wp, bp, NI,
+                   w4.data_ptr(), freq.data_ptr(), tpos.data_ptr(), deltas.data_ptr(), shift, L, E, C,
+                   O, dk.data_ptr(), part.data_ptr(), _p(dz), N.stream_ptr())
+            # slice sum; the weight / bias entries (all but the trailing freq) rounded to bf16, the
+            # grad of autocast's bf16 copies
+            g = torch.empty(P, device=dk.device, dtype=torch.float32)
+            N.call("dna_hyena_filter_finish", part.data_ptr(), total // P, P, P - F_, g.data_ptr(),
+                   N.stream_ptr())
+        o = 0
+        dw4 = g[o:o + C * F_].view(C, F_); o += C * F_
+        dwi = [g[o + i * F_ * F_:o + (i + 1) * F_ * F_].view(F_, F_) for i in range(NI)]; o += NI * F_ * F_
+        dbi = [g[o + i * F_:o + (i + 1) * F_] for i in range(NI)]; o += NI * F_
+        dw1 = g[o:o + F_ * E].view(F_, E); o += F_ * E
+        db1 = g[o:o + F_]; o += F_
+        dfreq = g[o:o + F_].view_as(freq)
+        dinner = []
+        for a_, b_ in zip(dwi, dbi):
+            dinner += [a_, b_]
+        return (dz, None, None, None, None, dw1, db1, dw4, dfreq, *dinner)
+
+
+def _fused_filter_ok(f, h0, L, O):
+    """The implicit filter runs as FilterMLP: CUDA, bf16 autocast, the reference layout
+    (Linear(E, 64), then two Linear(64, 64), Linear(64, C, no bias), one shared Sin), C in
+    {64, 128, 256, 512}, L % 64 == 0, modulation with a constant deltas, not normalized."""
+    if not (_FILTER_FUSED and h0.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    mods = list(f.implicit_filter)
+    if len(mods) != 7 or L % 64 or not f.modulate or f.normalized or f.modulation.deltas.requires_grad:
+        return False
+    lins, acts = mods[0::2], mods[1::2]
+    if not all(isinstance(m, nn.Linear) for m in lins) or not all(a is acts[0] for a in acts):
+        return False
+    if not isinstance(acts[0], Sin) or not isinstance(acts[0].freq, torch.Tensor) or acts[0].freq.numel() != 64:
+        return False
+    E = lins[0].in_features
+    C = lins[-1].out_features
+    return (E <= 8 and lins[0].out_features == 64 and all(m.in_features == 64 and m.out_features == 64
+                                                           for m in lins[1:-1])
+            and lins[-1].in_features == 64 and lins[-1].bias is None and C in (64, 128, 256, 512)
+            and C % O == 0 and all(m.bias is not None for m in lins[:-1])
+            and all(p.dtype == torch.float32 for m in lins for p in m.parameters()))
+
+
 def _split_k_linear(x, lin):
     """nn.Linear over the L positions of the implicit filter MLP ([1, L, K] -> [1, L, N], K 3-5
     and N 64-256) on the strided MFMA GEMM (`functional.strided_linear`). As one library GEMM
@@ -407,6 +505,16 @@ class HyenaFilter(_OptimModule):
         k[o][v][l] = filter(L)[0][l][v * O + o]. On the GPU the modulation and the transpose are
         one kernel (ModulateT); otherwise the reshape / permute of the reference."""
         z, t = self.pos_emb(L)
+        if z.dim() == 3 and z.shape[0] == 1 and _fused_filter_ok(self, z, L, O):
+            lins = list(self.implicit_filter)[0::2]
+            act = self.implicit_filter[1]
+            inner = []
+            for m in lins[1:-1]:
+                inner += [m.weight, m.bias]
+            return FilterMLP.apply(z[0], t.reshape(-1).float().contiguous(),
+                                   self.modulation.deltas.reshape(-1).float().contiguous(),
+                                   self.modulation.shift, O, lins[0].weight, lins[0].bias,
+                                   lins[-1].weight, act.freq.reshape(-1), *inner)
         h = z
         for layer in self.implicit_filter:
             h = _split_k_linear(h, layer) if isinstance(layer, nn.Linear) else layer(h)

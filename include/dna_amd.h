@@ -388,6 +388,29 @@ int dna_hyena_modulate_t_fwd(const void* h, int dtype, const float* tpos, const 
 int dna_hyena_modulate_t_bwd(const float* dk, const float* tpos, const float* delta, float shift,
                              int L, int C, int O, void* dh, int dtype, void* stream);
 
+/* HyenaFilter's implicit filter whole (reference hyena.py:162-247 filter() + the modulation and
+ * transpose above): k = modulate(Linear_out(Sin(... Sin(Linear_1(z)) ...))) under the bf16
+ * autocast dtype flow (each Linear on bf16-rounded input / weight / bias, bf16 output; Sin in
+ * fp32; one shared freq). z [L][E] fp32 (E <= 8), w1 [64][E], b1 [64], wi / bi: NI <= 4 host
+ * arrays of device pointers to [64][64] / [64] fp32, w4 [C][64] (C in {64, 128, 256, 512}),
+ * freq [64], tpos [L], delta [C]; L % 64 == 0; k [O][C / O][L] fp32. Backward: per-block
+ * partial gradients part [grid][dna_hyena_filter_part_stride()] (dna_hyena_filter_part_elems()
+ * floats in all; layout w4 [C][64], wi [NI][64][64], bi [NI][64], w1 [64][E], b1 [64], freq [64])
+ * for dna_sum_slices, and dz [L][E] (bf16-rounded) when dz is non-null. csrc/hyena_filter.hip. */
+int dna_hyena_filter_part_elems(int L, int E, int NI, int C);
+int dna_hyena_filter_part_stride(int E, int NI, int C);
+int dna_hyena_filter_fwd(const float* z, const float* w1, const float* b1, const float* const* wi,
+                         const float* const* bi, int NI, const float* w4, const float* freq,
+                         const float* tpos, const float* delta, float shift, int L, int E, int C, int O,
+                         float* k, void* stream);
+int dna_hyena_filter_bwd(const float* z, const float* w1, const float* b1, const float* const* wi,
+                         const float* const* bi, int NI, const float* w4, const float* freq,
+                         const float* tpos, const float* delta, float shift, int L, int E, int C, int O,
+                         const float* dk, float* part, float* dz, void* stream);
+/* the backward's gradient: out[i] = sum_g part[g * P + i] over the G = part_elems / P slices in
+ * order, rounded to bf16 (and back) for i < nround -- the weight / bias entries -- fp32 after */
+int dna_hyena_filter_finish(const float* part, int G, int P, int nround, float* out, void* stream);
+
 /* ------------------------------------------------------------------ causal depthwise conv1d (+ SiLU)
  * Mamba.forward's x = silu(conv1d(x)[..., :L]) (depthwise, kernel K = d_conv, padding K-1;
  * mamba_ssm via modeling_caduceus.py:88-91): x [B, C, L] (batch stride x_bstride elements,

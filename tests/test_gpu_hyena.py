@@ -103,10 +103,13 @@ def _op_state(d_model, l_max, order, seed, **kw):
 
 
 @pytest.mark.parametrize("order,autocast", [(2, True), (3, False), (2, False)])
-def test_filter_t_equals_filter_permuted(order, autocast):
+def test_filter_t_equals_filter_permuted(order, autocast, monkeypatch):
     """HyenaFilter.filter_t (ModulateT: modulation + transpose in one kernel) against the
     reference layout filter(L)[0].reshape(L, v, o).permute(2, 1, 0): forward and the gradients of
-    the implicit-filter MLP parameters."""
+    the implicit-filter MLP parameters. (The whole-filter kernels are off here; they have their
+    own test below.)"""
+    from dna_amd import hyena as HY
+    monkeypatch.setattr(HY, "_FILTER_FUSED", False)
     op, _ = _op_state(64, 2048, order, 5, emb_dim=5)
     f = op.filter_fn.to(DEV)
     L, O = 2048, order - 1
@@ -130,6 +133,50 @@ def test_filter_t_equals_filter_permuted(order, autocast):
     for n in g1:
         sc = g2[n].abs().max().item()
         assert (g1[n] - g2[n]).abs().max().item() <= 2e-5 * max(sc, 1e-3), n
+
+
+@pytest.mark.parametrize("C,O,L,lr_pos,w", [(256, 1, 65536, 0.0, 10), (256, 1, 4096, 1e-5, 10),
+                                          (256, 1, 4096, 1e-5, 1), (128, 2, 2048, 1e-5, 1),
+                                          (64, 1, 1024, 1e-5, 10), (512, 1, 1024, 0.0, 1)])
+def test_filter_whole_kernels_vs_module_path(C, O, L, lr_pos, w, monkeypatch):
+    """The implicit filter as two kernels (FilterMLP, csrc/hyena_filter.hip) against the module
+    path (strided-GEMM Linears, torch Sin, ModulateT) under bf16 autocast, at the config-D shape
+    (emb_dim 5, filter_order 64, Sin frequency w = 10) and others: k, and the gradients of every
+    MLP parameter, the shared Sin frequency and (lr_pos_emb > 0) the positional features. Both
+    run the same bf16 dtype flow and differ only in fp32 accumulation order, so a bf16 rounding
+    may land one ulp apart -- and sin(w y) turns a one-ulp change of y into w times that. Relative
+    Frobenius error: k < 4e-3 at w = 1 and < 2e-2 at w = 10, each gradient < 2e-2 / 5e-2."""
+    from dna_amd import hyena as HY
+    tk, tg = (4e-3, 2e-2) if w == 1 else (2e-2, 5e-2)
+    torch.manual_seed(C + L)
+    f = HY.HyenaFilter(C, emb_dim=5, order=64, seq_len=L, w=w, lr_pos_emb=lr_pos, modulate=True).to(DEV)
+    with torch.no_grad():  # trained-looking weights (default init keeps the Sin arguments small)
+        for n, p in f.named_parameters():
+            if "implicit_filter" in n:
+                p.mul_(1.5)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    dk = torch.randn(O, C // O, L, generator=g).to(DEV)
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(HY, "_FILTER_FUSED", fused)
+        f.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            k = f.filter_t(L, O)
+        (k * dk).sum().backward()
+        outs.append((k.detach().clone(),
+                     {n: p.grad.detach().clone() for n, p in f.named_parameters() if p.grad is not None}))
+    (k1, g1), (k2, g2) = outs
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()
+    assert k1.shape == k2.shape == (O, C // O, L)
+    assert rel(k1, k2) < tk, rel(k1, k2)
+    expect = {"implicit_filter.0.weight", "implicit_filter.0.bias", "implicit_filter.1.freq",
+              "implicit_filter.2.weight", "implicit_filter.2.bias", "implicit_filter.4.weight",
+              "implicit_filter.4.bias", "implicit_filter.6.weight"}
+    assert expect <= set(g1) and set(g1) == set(g2), (set(g1), set(g2))
+    if lr_pos > 0:
+        assert "pos_emb.z" in g1
+    for n in g1:
+        assert rel(g1[n], g2[n]) < tg, (n, rel(g1[n], g2[n]))
 
 
 def test_hyena_operator_matches_reference_fixture():
