@@ -473,9 +473,14 @@ __global__ __launch_bounds__(256) void finish_kernel(const float* __restrict__ p
                                                      float* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= P) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(size_t)g * P + i];
-  out[i] = i < nround ? rb(s) : s;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 slices in flight, fixed order
+  int g = 0;
+  for (; g + 8 <= G; g += 8)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] += part[(size_t)(g + q) * P + i];
+  for (; g < G; ++g) s[0] += part[(size_t)g * P + i];
+  const float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  out[i] = i < nround ? rb(t) : t;
 }
 
 inline size_t bwd_lds(int NI) { return (size_t)(2 + 2 * (NI + 1) + 4) * TILE * 2 + TP * MAXE * 4; }

@@ -416,11 +416,13 @@ int dispatch_cols(int cols, F&& f) {
   return DNA_ERR_UNSUPPORTED;
 }
 
-inline int bwd_blocks(int rows) {
+inline int bwd_blocks(int rows, int cols) {
   // DNA_LN_BWD_BLOCKS: A/B switch for the grid cap (more blocks = more rows in flight, more
-  // [3][cols] partials for reduce_partials)
-  static const int cap = getenv("DNA_LN_BWD_BLOCKS") ? atoi(getenv("DNA_LN_BWD_BLOCKS")) : BWD_BLOCKS;
-  const int lim = cap >= 64 ? cap : BWD_BLOCKS;
+  // [3][cols] partials for reduce_partials). Rows below 768 columns get twice the blocks: a
+  // wave's row is then too short to keep enough bytes in flight (d = 256, config D: 0.200 ->
+  // 0.126 ms per call at 1024 blocks; 768 columns: 512 stays best, profiles/r05)
+  static const int cap = getenv("DNA_LN_BWD_BLOCKS") ? atoi(getenv("DNA_LN_BWD_BLOCKS")) : 0;
+  const int lim = cap >= 64 ? cap : (cols < 768 ? 2 * BWD_BLOCKS : BWD_BLOCKS);
   int nb = (rows + WAVES - 1) / WAVES;
   return nb < lim ? nb : lim;
 }
@@ -432,7 +434,7 @@ using namespace dna;
 using namespace dna::ln;
 
 extern "C" size_t dna_ln_bwd_workspace(int rows, int cols) {
-  return (size_t)bwd_blocks(rows) * 3 * cols * sizeof(float);
+  return (size_t)bwd_blocks(rows, cols) * 3 * cols * sizeof(float);
 }
 
 extern "C" int dna_ln_fwd(const void* x, int x_dtype, const float* bias, int act, float p_drop,
@@ -473,7 +475,7 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
   DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
                 "dna_ln_bwd: workspace too small (%zu < %zu)", workspace_bytes,
                 dna_ln_bwd_workspace(rows, cols));
-  const int nb = bwd_blocks(rows);
+  const int nb = bwd_blocks(rows, cols);
   BwdArgs a{dy, (const bf16*)dy_bf16, x, bias, act, p_drop, dropout_threshold(p_drop),
             1.f / (1.f - p_drop), seed, offset, residual, gamma, mean, rstd, rows, cols,
             dresidual, dx, (float*)workspace, 0, nullptr};
@@ -540,7 +542,7 @@ extern "C" int dna_add_ln_bwd(const float* dy, const void* dy_bf16, const float*
   DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
                 "dna_add_ln_bwd: workspace too small (%zu < %zu)", workspace_bytes,
                 dna_ln_bwd_workspace(rows, cols));
-  const int nb = bwd_blocks(rows);
+  const int nb = bwd_blocks(rows, cols);
   BwdArgs a{dy, (const bf16*)dy_bf16, x, nullptr, 0, 0.f, 0u, 1.f, 0, 0, residual, gamma,
             rms ? nullptr : mean, rstd, rows, cols, dresidual, dx, (float*)workspace, rms ? 1 : 0, dsum};
   hipStream_t s = as_stream(stream);
@@ -596,7 +598,7 @@ static int embed_ln_bwd_impl(const float* dy, const void* dy_bf16, const int64_t
   if (rows == 0) return DNA_OK;
   DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
                 "dna_embed_ln_bwd: workspace too small");
-  const int nb = bwd_blocks(rows);
+  const int nb = bwd_blocks(rows, cols);
   EmbBwdArgs a{dy, (const bf16*)dy_bf16, ids, word_emb, type_row, gamma, mean, rstd, rows, cols,
                vocab, padding_idx, p_drop, dropout_threshold(p_drop), 1.f / (1.f - p_drop), seed,
                offset, dword_emb, (float*)workspace, drows};
@@ -675,7 +677,7 @@ extern "C" int dna_rms_bwd(const float* dy, const void* dy_bf16, const void* x, 
   DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
                 "dna_rms_bwd: workspace too small (%zu < %zu)", workspace_bytes,
                 dna_ln_bwd_workspace(rows, cols));
-  const int nb = bwd_blocks(rows);
+  const int nb = bwd_blocks(rows, cols);
   BwdArgs a{dy, (const bf16*)dy_bf16, x, nullptr, DNA_ACT_NONE, 0.f, 0u, 1.f, 0, 0, nullptr, gamma,
             nullptr, rstd, rows, cols, nullptr, dx, (float*)workspace, 1};
   hipStream_t s = as_stream(stream);
