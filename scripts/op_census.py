@@ -23,6 +23,15 @@ WATCH = ("aten::copy_", "aten::to", "aten::_to_copy", "aten::fill_", "aten::zero
 
 
 def build(model, L):
+    if model == "bert":  # bench.py's DNABERT-2 step (MLMTrainer), at a small per-GPU batch
+        import bench
+        from dna_amd.bert_layers import BertForMaskedLM
+        from dna_amd.trainer import MLMTrainer
+        dev = torch.device("cuda", 0)
+        m = BertForMaskedLM(bench.MODEL_CFG, precision="bf16")
+        tr = MLMTrainer(m, dev, lr=5e-4, weight_decay=1e-5, max_grad_norm=1.0)
+        batches = bench.make_batches(1, 64, 0, dev)
+        return lambda: tr.step(batches[0])
     if model == "hyena":
         from dna_amd.hyena_lm import BertLMHeadModel
         layer = {"_name_": "hyena", "emb_dim": 5, "filter_order": 64, "short_filter_order": 3,
@@ -60,11 +69,12 @@ def build(model, L):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="hyena", choices=["hyena", "caduceus"])
+    ap.add_argument("--model", default="hyena", choices=["hyena", "caduceus", "bert"])
     ap.add_argument("--L", type=int, default=0)
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
     L = a.L or (65536 if a.model == "hyena" else 131072)
+    os.environ.setdefault("DNA_STRICT_NATIVE", "1")
     torch.manual_seed(0)
     step = build(a.model, L)
     for _ in range(2):
