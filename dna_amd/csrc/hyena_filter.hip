@@ -10,7 +10,10 @@
 // sin(freq * y) in fp32 from the bf16 y; the modulation multiplies the bf16 h in fp32. Backward:
 // dh = bf16(dk * mod), each Linear's dx in bf16, dW / db summed in fp32 and rounded to bf16 once
 // (the grad of the bf16 weight copy), Sin: darg = dx * cos(freq y), dfreq += darg * y (fp32),
-// dy = bf16(darg * freq).
+// dy = bf16(darg * freq). The forward's sin and every exp are the hardware forms (v_sin / v_exp
+// after the range scaling, ~1e-6 absolute; each result is rounded to bf16 next, 4e-3 relative); the
+// backward keeps the library sin / cos (with the hardware forms its register allocation spills
+// and hipcc 7.2's AGPR-copy rewrite crashes).
 //
 // Layout: a block = 4 waves works on tiles of 64 positions. The 64-wide GEMMs run on
 // v_mfma_f32_16x16x32_bf16 with the positions as M: a lane ends with 4 consecutive positions of
@@ -65,6 +68,16 @@ struct Off {
 };
 
 __device__ __forceinline__ float rb(float x) { return (float)(bf16)x; }
+// sin / cos on the hardware unit (v_sin_f32 / v_cos_f32 take revolutions): the argument reduced to
+// [-0.5, 0.5] revolutions first; ~1e-6 absolute against the library forms
+__device__ __forceinline__ float hsin(float x) {
+  const float r = x * 0.15915494309189535f;
+  return __builtin_amdgcn_sinf(r - rintf(r));
+}
+__device__ __forceinline__ float hcos(float x) {
+  const float r = x * 0.15915494309189535f;
+  return __builtin_amdgcn_cosf(r - rintf(r));
+}
 __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -90,12 +103,12 @@ __device__ __forceinline__ float lane_sum4(float v) {  // over lanes l, l^16, l^
   return v;
 }
 
-// Linear(E, F) + Sin on the VALU for a tile: thread -> position tid / 4, channels 16 (tid % 4) ..
-// +15. Writes y (bf16 values, pre-sin) to ytile[j][pos] if given, the bf16 sin output to
+// Linear(E, F) + Sin on the VALU for a tile: lane -> position, wave -> channels 16 w .. +15 (the
+// [j][pos] row writes of a wave are then 128 contiguous bytes: no LDS bank conflicts). Writes y (bf16 values, pre-sin) to ytile[j][pos] if given, the bf16 sin output to
 // xrow[pos][j] and, if given, xcol[j][pos]. zt[pos][e]: the tile's rounded features.
 __device__ __forceinline__ void first_layer(const float* w1s, const float* b1s, const float* frs,
                                            const float* zt, int E, bf16* xrow, bf16* xcol, bf16* ytile) {
-  const int tid = threadIdx.x, pos = tid >> 2, cg = (tid & 3) * 16;
+  const int tid = threadIdx.x, pos = tid & 63, cg = (tid >> 6) * 16;
   float zz[MAXE];
 #pragma unroll
   for (int e = 0; e < MAXE; ++e) zz[e] = e < E ? zt[pos * MAXE + e] : 0.f;
@@ -108,7 +121,7 @@ __device__ __forceinline__ void first_layer(const float* w1s, const float* b1s, 
     for (int e = 0; e < MAXE; ++e)
       if (e < E) acc = fmaf(zz[e], w1s[j * MAXE + e], acc);
     const float y = rb(acc + b1s[j]);
-    const float s = sinf(frs[j] * y);
+    const float s = hsin(frs[j] * y);
     o[jj >> 3][jj & 7] = (bf16)s;
     if (xcol) xcol[j * RS + pos] = (bf16)s;
     if (ytile) ytile[j * RS + pos] = (bf16)y;
@@ -191,7 +204,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float y = rb(acc[i] + bb);
-          dst[(ms * 16 + 4 * lg + i) * RS + 16 * w + l16] = (bf16)sinf(fr * y);
+          dst[(ms * 16 + 4 * lg + i) * RS + 16 * w + l16] = (bf16)hsin(fr * y);
         }
       }
       __syncthreads();
@@ -210,7 +223,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(Args a) {
         const int c = w * 16 * CTW + ct * 16 + l16;
         f32x4 o;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = rb(acc[i]) * (expf(-tv[i] * ad[ct]) + a.shift);
+        for (int i = 0; i < 4; ++i) o[i] = rb(acc[i]) * (__expf(-tv[i] * ad[ct]) + a.shift);
         *reinterpret_cast<f32x4*>(a.k + ((size_t)(c % a.O) * V + c / a.O) * a.L + pos) = o;
       }
     }
@@ -335,7 +348,7 @@ __global__ __launch_bounds__(NT) void bwd_kernel(Args a) {
           const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * q);
           const f32x4 tv = *reinterpret_cast<const f32x4*>(a.tpos + p0 + pg + 4 * q);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) d[4 * q + i] = rb(v[i] * (expf(-tv[i] * ad[cc]) + a.shift));
+          for (int i = 0; i < 4; ++i) d[4 * q + i] = rb(v[i] * (__expf(-tv[i] * ad[cc]) + a.shift));
         }
         bf16x8 h0, h1;
 #pragma unroll
