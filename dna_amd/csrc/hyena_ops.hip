@@ -14,6 +14,8 @@
 // Tiles: 64 positions x 32 channels per block of 256 threads (small LDS footprint -> several
 // blocks per CU); tiles load with 16-byte vectors; for the conv, lane = position (coalesced
 // channel-major rows) and wave = an 8-channel slice. All math in fp32; HBM-bound.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace dna {
@@ -69,6 +71,7 @@ __device__ __forceinline__ void load_tok_tiles(float* lds, const T* src, int L, 
 struct Fwd {
   const void* u; const float* w; const float* bias; int B, L, d, order, K;
   void* xs; void* vx;
+  int nct;  // channel tiles per block, run one after the other (see nct_for)
 };
 
 template <typename T, int K, int ORD>
@@ -76,9 +79,12 @@ __global__ __launch_bounds__(256) void shortconv_fwd_kernel(Fwd a) {
   extern __shared__ float smem[];
   constexpr int G = ORD + 1;  // channel groups x_0 .. x_{order-1}, v (compile-time: exact unrolls)
   const int C = G * a.d;
-  const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
+  const int t0 = blockIdx.x * TP, b = blockIdx.z;
   const int R = TP + K - 1;  // rows incl. halo
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
+  for (int ct = 0; ct < a.nct; ++ct) {
+  const int c0 = (blockIdx.y * a.nct + ct) * TC;
+  if (ct > 0) __syncthreads();  // the previous tile's LDS reads are done
   load_tok_tiles<T, K - 1, 0, G>(smem, u, a.L, C, t0, a.d, c0);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -101,6 +107,7 @@ __global__ __launch_bounds__(256) void shortconv_fwd_kernel(Fwd a) {
           ((T*)a.vx)[((size_t)b * a.d + c) * a.L + t] = cvt<T>(acc * last);
       }
     }
+  }
   }
 }
 
@@ -224,6 +231,7 @@ __global__ __launch_bounds__(256) void modulate_t_bwd_kernel(const float* __rest
 struct Bwd {
   const void* u; const float* w; const float* bias; int B, L, d, order, K;
   const void* dxs; const void* dvx; void* du; float* part;  // part [B * nL][C][K + 1]
+  int nct;  // channel tiles per block
 };
 
 // duc (d of the conv outputs) at positions [t0, t0 + TP + K - 1), then
@@ -239,7 +247,10 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   extern __shared__ float smem[];
   constexpr int G = ORD + 1;
   const int C = G * a.d;
-  const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
+  const int t0 = blockIdx.x * TP, b = blockIdx.z;
+  for (int ct = 0; ct < a.nct; ++ct) {
+  const int c0 = (blockIdx.y * a.nct + ct) * TC;
+  if (ct > 0) __syncthreads();  // the previous tile's LDS reads are done
   constexpr int RU = TP + 2 * (K - 1);  // u rows: [t0 - (K-1), t0 + TP + K - 1)
   constexpr int RD = TP + K - 1;        // duc rows: [t0, t0 + TP + K - 1)
   constexpr int LW = TC + PAD;
@@ -431,6 +442,16 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
                     red[3 * G * TC * (K + 1) + e];
     prow[(size_t)(g * a.d + c0 + j) * (K + 1) + k] = v;
   }
+  }
+}
+
+// Channel tiles per block for the short-conv backward: the two 32-channel tiles of a 128-B
+// token-major line run in one block, so the second tile's u rows are L2 hits (PMC: the one-tile
+// kernel fetched 2x its algorithmic bytes); 0.365 -> 0.354 ms at config D. DNA_HYENA_NCT=1: the
+// one-tile blocks (A/B).
+inline int nct_for(int d) {
+  static const int env = getenv("DNA_HYENA_NCT") ? atoi(getenv("DNA_HYENA_NCT")) : 2;
+  return (env == 2 && (d / TC) % 2 == 0) ? 2 : 1;
 }
 
 template <typename F>
@@ -475,8 +496,8 @@ extern "C" int dna_hyena_shortconv_fwd(const void* u, int dtype, const float* w,
   if (st) return st;
   DNA_CHECK_ARG(u && w && bias && vx && (order == 2 || xs), "dna_hyena_shortconv_fwd: null pointer");
   DNA_CHECK_ARG(((uintptr_t)u & 15) == 0, "dna_hyena_shortconv_fwd: u must be 16-byte aligned");
-  Fwd a{u, w, bias, B, L, d, order, K, xs, vx};
-  const dim3 grid((L + TP - 1) / TP, d / TC, B);
+  Fwd a{u, w, bias, B, L, d, order, K, xs, vx, 1};  // two tiles per block: 2 % slower here
+  const dim3 grid((L + TP - 1) / TP, d / TC / a.nct, B);
   const size_t lds = (size_t)(order + 1) * (TP + K - 1) * (TC + PAD) * sizeof(float);
   hipStream_t s = as_stream(stream);
   dispatch_k_ord(K, order, [&](auto kk, auto oo) {
@@ -502,8 +523,8 @@ extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w,
   DNA_CHECK_ARG(u && w && bias && dvx && du && part && (order == 2 || dxs),
                 "dna_hyena_shortconv_bwd: null pointer");
   DNA_CHECK_ARG(((uintptr_t)u & 15) == 0, "dna_hyena_shortconv_bwd: u must be 16-byte aligned");
-  Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part};
-  const dim3 grid((L + TP - 1) / TP, d / TC, B);
+  Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part, nct_for(d)};
+  const dim3 grid((L + TP - 1) / TP, d / TC / a.nct, B);
   const size_t lds = (size_t)(order + 1) * (((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) + 4 * TC * (K + 1)) *
                      sizeof(float);
   DNA_CHECK_ARG(lds <= 160 * 1024, "dna_hyena_shortconv_bwd: order %d needs %zu B of LDS", order, lds);
