@@ -235,7 +235,9 @@ __global__ __launch_bounds__(NT) void fwd_kernel(Args a) {
 //   xa[2]            forward recompute, [pos][k] rows (MFMA A operands)
 //   xT[NI + 1]       inputs of the inner layers and of the output layer, [k][pos] rows (dW B)
 //   yv[NI + 1]       pre-sin values of L1 and the inner layers, [j][pos] rows
-//   dhc, dhp         one 64-channel chunk of dh as [c][pos] (dW4 A) and [pos][c] (dX4 A)
+//   dhc, dhp         one 64-channel chunk of dh as [c][pos] (dW4 A) and [pos][c] (dX4 A); dhp's
+//                    8-column chunks XOR-swizzled by 2 * (pos / 16 % 4): the staging threads of a
+//                    wave write 4 rows 16 apart (the same banks) at once -- 4-way conflicts else
 //   dyt, dyp         dy of the current layer as [j][pos] (dW A) and [pos][j] (dX A)
 //   zt (fp32)        the tile's features
 template <int CTW, int NI>
@@ -356,7 +358,8 @@ __global__ __launch_bounds__(NT) void bwd_kernel(Args a) {
         *reinterpret_cast<bf16x8*>(dhc + cl * RS + pg) = h0;
         *reinterpret_cast<bf16x8*>(dhc + cl * RS + pg + 8) = h1;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dhp[(pg + i) * RS + cl] = (bf16)d[i];
+        for (int i = 0; i < 16; ++i)
+          dhp[(pg + i) * RS + (((cl >> 3) ^ (2 * ((pg >> 4) & 3))) << 3) + (cl & 7)] = (bf16)d[i];
       }
       __syncthreads();
       {  // dW4[c][j] += sum_pos dh[pos][c] x4[pos][j]: rows c = 16 w + (chunk), column tiles nt
@@ -371,9 +374,9 @@ __global__ __launch_bounds__(NT) void bwd_kernel(Args a) {
         // dX4[pos][j] += sum_c dh[pos][c] W4[c][j]: column tile w, row tiles ms
 #pragma unroll
         for (int ms = 0; ms < 4; ++ms) {
-          const bf16* pr = dhp + (ms * 16 + l16) * RS + 8 * lg;
-          dx[ms] = mfma(lds8(pr), w4t[cc][0], dx[ms]);
-          dx[ms] = mfma(lds8(pr + 32), w4t[cc][1], dx[ms]);
+          const bf16* pr = dhp + (ms * 16 + l16) * RS;  // row ms * 16 + l16: swizzle 2 * ms
+          dx[ms] = mfma(lds8(pr + ((lg ^ (2 * ms)) << 3)), w4t[cc][0], dx[ms]);
+          dx[ms] = mfma(lds8(pr + (((lg + 4) ^ (2 * ms)) << 3)), w4t[cc][1], dx[ms]);
         }
       }
       __syncthreads();
