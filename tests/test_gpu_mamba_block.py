@@ -19,7 +19,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,C,L,K,silu", [(2, 64, 1000, 4, True), (1, 3, 2500, 3, False),
-                                          (3, 128, 64, 2, True), (1, 16, 4096, 4, True)])
+                                          (3, 128, 64, 2, True), (1, 16, 4096, 4, True),
+                                          (2, 8, 5128, 4, True), (1, 4, 8200, 3, False)])
 def test_causal_conv1d_vs_torch(dtype, tol, B, C, L, K, silu):
     from dna_amd.mamba import CausalConv1d
     g = torch.Generator(device="cpu").manual_seed(B * C + L)
