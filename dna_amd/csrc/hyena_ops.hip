@@ -35,37 +35,56 @@ __device__ __forceinline__ T cvt(float v) { return from_f32<T>(v); }
 // along the channels. Every load of a thread (all groups) is issued before the first LDS store:
 // these kernels are memory-latency bound (PMC: 78-92 % of wave cycles in s_waitcnt), and a
 // load -> convert -> store loop kept one 16-B load per thread in flight.
+template <typename T, int LO, int HI>
+struct TokTile {
+  static constexpr int VE = 16 / sizeof(T);      // elements per vector
+  static constexpr int VPR = TC / VE;            // vectors per row
+  static constexpr int ROWS = TP + LO + HI;
+  static constexpr int NIT = (ROWS * VPR + 255) / 256;  // per group and thread (256-thread blocks)
+};
+template <typename T, int LO, int HI, int G, int NIT = TokTile<T, LO, HI>::NIT>
+__device__ __forceinline__ void tok_fetch(uint4 (&raw)[G][NIT], const T* src,
+                                          int L, int ldc, int t0, int d, int col0) {
+  using TT = TokTile<T, LO, HI>;
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int it = 0; it < TT::NIT; ++it) {
+      const int i = threadIdx.x + it * 256;
+      const int r = i / TT::VPR, cv = (i - r * TT::VPR) * TT::VE;
+      const int t = t0 - LO + r;
+      raw[g][it] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < TT::ROWS * TT::VPR && t >= 0 && t < L)
+        raw[g][it] = *reinterpret_cast<const uint4*>(src + (size_t)t * ldc + g * d + col0 + cv);
+    }
+}
+template <typename T, int LO, int HI, int G, int NIT = TokTile<T, LO, HI>::NIT>
+__device__ __forceinline__ void tok_store(float* lds, const uint4 (&raw)[G][NIT]) {
+  using TT = TokTile<T, LO, HI>;
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int it = 0; it < TT::NIT; ++it) {
+      const int i = threadIdx.x + it * 256;
+      if (i >= TT::ROWS * TT::VPR) continue;
+      const int r = i / TT::VPR, cv = (i - r * TT::VPR) * TT::VE;
+      float* dst = lds + (g * TT::ROWS + r) * (TC + PAD) + cv;
+      const T* e = reinterpret_cast<const T*>(&raw[g][it]);
+#pragma unroll
+      for (int q = 0; q < TT::VE; ++q) dst[q] = to_f32(e[q]);
+    }
+}
+// Load rows [t0 - LO, t0 + TP + HI) x channels [g*d + col0, + TC) of the G channel groups of a
+// token-major [L, ldc] matrix into lds[g][row][TC + PAD] (zero outside [0, L)), 16-byte vectors
+// along the channels. Every load of a thread (all groups) is issued before the first LDS store:
+// these kernels are memory-latency bound (PMC: 78-92 % of wave cycles in s_waitcnt), and a
+// load -> convert -> store loop kept one 16-B load per thread in flight.
 template <typename T, int LO, int HI, int G>
 __device__ __forceinline__ void load_tok_tiles(float* lds, const T* src, int L, int ldc, int t0,
                                                int d, int col0) {
-  constexpr int VE = 16 / sizeof(T);      // elements per vector
-  constexpr int VPR = TC / VE;            // vectors per row
-  constexpr int ROWS = TP + LO + HI;
-  constexpr int NIT = (ROWS * VPR + 255) / 256;  // per group and thread (256-thread blocks)
-  uint4 raw[G][NIT];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int i = threadIdx.x + it * 256;
-      const int r = i / VPR, cv = (i - r * VPR) * VE;
-      const int t = t0 - LO + r;
-      raw[g][it] = make_uint4(0u, 0u, 0u, 0u);
-      if (i < ROWS * VPR && t >= 0 && t < L)
-        raw[g][it] = *reinterpret_cast<const uint4*>(src + (size_t)t * ldc + g * d + col0 + cv);
-    }
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int i = threadIdx.x + it * 256;
-      if (i >= ROWS * VPR) continue;
-      const int r = i / VPR, cv = (i - r * VPR) * VE;
-      float* dst = lds + (g * ROWS + r) * (TC + PAD) + cv;
-      const T* e = reinterpret_cast<const T*>(&raw[g][it]);
-#pragma unroll
-      for (int q = 0; q < VE; ++q) dst[q] = to_f32(e[q]);
-    }
+  uint4 raw[G][TokTile<T, LO, HI>::NIT];
+  tok_fetch<T, LO, HI, G>(raw, src, L, ldc, t0, d, col0);
+  tok_store<T, LO, HI, G>(lds, raw);
 }
 
 struct Fwd {
@@ -231,7 +250,6 @@ __global__ __launch_bounds__(256) void modulate_t_bwd_kernel(const float* __rest
 struct Bwd {
   const void* u; const float* w; const float* bias; int B, L, d, order, K;
   const void* dxs; const void* dvx; void* du; float* part;  // part [B * nL][C][K + 1]
-  int nct;  // channel tiles per block
 };
 
 // duc (d of the conv outputs) at positions [t0, t0 + TP + K - 1), then
@@ -242,91 +260,73 @@ struct Bwd {
 // du is written as channel pairs (4-B bf16 / 8-B fp32 stores, 16 pairs x 4 rows per wave pass);
 // the dw / dbias tile sums are split into 4 row quarters per (group, channel) and combined in LDS
 // in a fixed order before the per-tile partial is written (deterministic).
-template <typename T, int K, int ORD>
+// A block runs NCT channel tiles of one position tile, software-pipelined: every HBM load of tile
+// ct + 1 (its u rows and its d(x) / d(v x) rows, into registers) is issued right after tile ct's
+// u rows reach LDS, so it is in flight during tile ct's compute and stores; the first tile's
+// d(x) and u loads are issued together (one round trip before the first barrier).
+template <typename T, int K, int ORD, int NCT>
 __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   extern __shared__ float smem[];
   constexpr int G = ORD + 1;
-  const int C = G * a.d;
-  const int t0 = blockIdx.x * TP, b = blockIdx.z;
-  for (int ct = 0; ct < a.nct; ++ct) {
-  const int c0 = (blockIdx.y * a.nct + ct) * TC;
-  if (ct > 0) __syncthreads();  // the previous tile's LDS reads are done
   constexpr int RU = TP + 2 * (K - 1);  // u rows: [t0 - (K-1), t0 + TP + K - 1)
   constexpr int RD = TP + K - 1;        // duc rows: [t0, t0 + TP + K - 1)
   constexpr int LW = TC + PAD;
+  // duc for a tile's positions plus the K-1 after it (0 at t >= L: cropped conv outputs). A lane
+  // takes (channel jj of the wave's 8, chunk of 8 positions): its d(x_g) / d(v x) loads are 16-B
+  // vectors of the channel-major rows (when L % 8 == 0: every row 16-B aligned); rows past the
+  // duc tile (RD) or past L are dropped / zero.
+  constexpr int NCH = (RD + 7) / 8;                 // position chunks per channel
+  constexpr int NQ = (CPW * NCH + 63) / 64;         // items per lane
+  constexpr int DW = sizeof(T) == 2 ? 1 : 2;        // 16-B words per 8 elements
+  constexpr int NIT = TokTile<T, K - 1, K - 1>::NIT;
+  const int C = G * a.d;
+  const int t0 = blockIdx.x * TP, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float* us = smem;                  // [G][RU][LW]
   float* ds = smem + G * RU * LW;    // [G][RD][LW]
   float* red = ds + G * RD * LW;     // [4][G * TC][K + 1] row-quarter sums
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
-  load_tok_tiles<T, K - 1, K - 1, G>(us, u, a.L, C, t0, a.d, c0);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // duc for this tile's positions plus the K-1 after it (0 at t >= L: cropped conv outputs).
-  // A lane takes (channel jj of the wave's 8, chunk of 8 positions): its d(x_g) / d(v x) loads are
-  // 16-B vectors of the channel-major rows (when L % 8 == 0: every row 16-B aligned), all issued
-  // before the conv recompute; rows past the duc tile (RD) or past L are dropped / zero.
-  constexpr int NCH = (RD + 7) / 8;                 // position chunks per channel
-  constexpr int NQ = (CPW * NCH + 63) / 64;         // items per lane
-  constexpr int NX = ORD - 1 > 0 ? ORD - 1 : 1;
   const bool vec = (a.L & 7) == 0;
-  bf16x8 lxv[NQ][NX], lvv[NQ];
-  float4 lxf[NQ][NX][2], lvf[NQ][2];
+  struct Regs {
+    uint4 raw[G][NIT];      // u tile rows (token-major, 16-B vectors)
+    uint4 dg[NQ][ORD][DW];  // [g < ORD-1]: d(x_g), [ORD-1]: d(v x); 8 positions per item
+  };
+  auto fetch = [&](Regs& r, int c0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int n = 0; n < NQ; ++n) {
-    const int q = lane + 64 * n;
-    const int jj = q / NCH, pc = q - jj * NCH;
-    const int c = c0 + wv * CPW + jj, t = t0 + 8 * pc;
-    const bool okq = q < CPW * NCH;
-    const size_t ov = ((size_t)b * a.d + c) * a.L + t;
-    if constexpr (sizeof(T) == 2) {
-      lvv[n] = bf16x8{};
+    for (int n = 0; n < NQ; ++n) {
+      const int q = lane + 64 * n;
+      const int jj = q / NCH, pc = q - jj * NCH;
+      const int c = c0 + wv * CPW + jj, t = t0 + 8 * pc;
+      const bool okq = q < CPW * NCH;
 #pragma unroll
-      for (int g = 0; g < NX; ++g) lxv[n][g] = bf16x8{};
-      if (okq && vec && t + 8 <= a.L) {
-        lvv[n] = *reinterpret_cast<const bf16x8*>((const bf16*)a.dvx + ov);
+      for (int g = 0; g < ORD; ++g) {
+        const T* row = g < ORD - 1 ? (const T*)a.dxs + ((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L
+                                   : (const T*)a.dvx + ((size_t)b * a.d + c) * a.L;
 #pragma unroll
-        for (int g = 0; g < ORD - 1; ++g)
-          lxv[n][g] = *reinterpret_cast<const bf16x8*>(
-              (const bf16*)a.dxs + ((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t);
-      } else if (okq) {
+        for (int h = 0; h < DW; ++h) r.dg[n][g][h] = make_uint4(0u, 0u, 0u, 0u);
+        if (okq && vec && t + 8 <= a.L) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (t + i >= a.L) break;
-          lvv[n][i] = ((const bf16*)a.dvx)[ov + i];
+          for (int h = 0; h < DW; ++h) r.dg[n][g][h] = *reinterpret_cast<const uint4*>(row + t + h * (8 / DW));
+        } else if (okq) {
+          T* e = reinterpret_cast<T*>(&r.dg[n][g][0]);
 #pragma unroll
-          for (int g = 0; g < ORD - 1; ++g)
-            lxv[n][g][i] = ((const bf16*)a.dxs)[((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t + i];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        lvf[n][h] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int g = 0; g < NX; ++g) lxf[n][g][h] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      if (okq && vec && t + 8 <= a.L) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          lvf[n][h] = *reinterpret_cast<const float4*>((const float*)a.dvx + ov + 4 * h);
-#pragma unroll
-          for (int g = 0; g < ORD - 1; ++g)
-            lxf[n][g][h] = *reinterpret_cast<const float4*>(
-                (const float*)a.dxs + ((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t + 4 * h);
-        }
-      } else if (okq) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (t + i >= a.L) break;
-          reinterpret_cast<float*>(&lvf[n][0])[i] = ((const float*)a.dvx)[ov + i];
-#pragma unroll
-          for (int g = 0; g < ORD - 1; ++g)
-            reinterpret_cast<float*>(&lxf[n][g][0])[i] =
-                ((const float*)a.dxs)[((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t + i];
+          for (int i = 0; i < 8; ++i)
+            if (t + i < a.L) e[i] = row[t + i];
         }
       }
     }
-  }
+    tok_fetch<T, K - 1, K - 1, G>(r.raw, u, a.L, C, t0, a.d, c0);
+  };
+  Regs cur;
+  fetch(cur, blockIdx.y * NCT * TC);
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+  const int c0 = (blockIdx.y * NCT + ct) * TC;
+  if (ct > 0) __syncthreads();  // the previous tile's LDS reads are done
+  tok_store<T, K - 1, K - 1, G>(us, cur.raw);
+  __syncthreads();
+  Regs nxt;
+  if (ct + 1 < NCT) fetch(nxt, c0 + TC);
 #pragma unroll
   for (int n = 0; n < NQ; ++n) {
     const int q = lane + 64 * n;
@@ -356,20 +356,11 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
           conv_v = fmaf(wvv[k], tl_v[(rr + k) * LW + j], conv_v);
         }
       }
-      float dvx, xg[NX];
-      if constexpr (sizeof(T) == 2) {
-        dvx = (float)lvv[n][i];
-#pragma unroll
-        for (int g = 0; g < NX; ++g) xg[g] = (float)lxv[n][g][i];
-      } else {
-        dvx = reinterpret_cast<const float*>(&lvf[n][0])[i];
-#pragma unroll
-        for (int g = 0; g < NX; ++g) xg[g] = reinterpret_cast<const float*>(&lxf[n][g][0])[i];
-      }
+      const float dvx = to_f32(reinterpret_cast<const T*>(&cur.dg[n][ORD - 1][0])[i]);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float v;
-        if (g < ORD - 1) v = xg[g < NX ? g : 0];
+        if (g < ORD - 1) v = to_f32(reinterpret_cast<const T*>(&cur.dg[n][g < ORD - 1 ? g : 0][0])[i]);
         else v = g == ORD - 1 ? dvx * conv_v : dvx * conv_last;
         ds[(g * RD + rr) * LW + j] = v;
       }
@@ -442,16 +433,20 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
                     red[3 * G * TC * (K + 1) + e];
     prow[(size_t)(g * a.d + c0 + j) * (K + 1) + k] = v;
   }
+  if (ct + 1 < NCT) cur = nxt;
   }
 }
 
-// Channel tiles per block for the short-conv backward: the two 32-channel tiles of a 128-B
-// token-major line run in one block, so the second tile's u rows are L2 hits (PMC: the one-tile
-// kernel fetched 2x its algorithmic bytes); 0.365 -> 0.354 ms at config D. DNA_HYENA_NCT=1: the
-// one-tile blocks (A/B).
+// Channel tiles per block for the short-conv backward: the 32-channel tiles of a 128-B
+// token-major line run in one block, so the later tiles' u rows are L2 hits (PMC: the one-tile
+// kernel fetched 2x its algorithmic bytes), software-pipelined (above): 4 tiles per block
+// (0.347 -> 0.334 ms at config D, profiles/r05/ab_shortconv_pipelined.txt).
+// DNA_HYENA_NCT = 1 | 2 | 4 (A/B; default 4); fewer when d / 32 does not divide.
 inline int nct_for(int d) {
-  static const int env = getenv("DNA_HYENA_NCT") ? atoi(getenv("DNA_HYENA_NCT")) : 2;
-  return (env == 2 && (d / TC) % 2 == 0) ? 2 : 1;
+  static const int env = getenv("DNA_HYENA_NCT") ? atoi(getenv("DNA_HYENA_NCT")) : 4;
+  for (int n = env >= 4 ? 4 : env >= 2 ? 2 : 1; n > 1; n /= 2)
+    if ((d / TC) % n == 0) return n;
+  return 1;
 }
 
 template <typename F>
@@ -523,23 +518,25 @@ extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w,
   DNA_CHECK_ARG(u && w && bias && dvx && du && part && (order == 2 || dxs),
                 "dna_hyena_shortconv_bwd: null pointer");
   DNA_CHECK_ARG(((uintptr_t)u & 15) == 0, "dna_hyena_shortconv_bwd: u must be 16-byte aligned");
-  Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part, nct_for(d)};
-  const dim3 grid((L + TP - 1) / TP, d / TC / a.nct, B);
+  Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part};
+  const int nct = nct_for(d);
+  const dim3 grid((L + TP - 1) / TP, d / TC / nct, B);
   const size_t lds = (size_t)(order + 1) * (((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) + 4 * TC * (K + 1)) *
                      sizeof(float);
   DNA_CHECK_ARG(lds <= 160 * 1024, "dna_hyena_shortconv_bwd: order %d needs %zu B of LDS", order, lds);
   hipStream_t s = as_stream(stream);
   dispatch_k_ord(K, order, [&](auto kk, auto oo) {
     constexpr int KK = decltype(kk)::value, OO = decltype(oo)::value;
-    if (dtype == DNA_F32) {
-      auto k = shortconv_bwd_kernel<float, KK, OO>;
+    auto go = [&](auto k) {
       if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
-    } else {
-      auto k = shortconv_bwd_kernel<bf16, KK, OO>;
-      if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
-    }
+    };
+    if (dtype == DNA_F32)
+      nct == 4 ? go(shortconv_bwd_kernel<float, KK, OO, 4>) : nct == 2 ? go(shortconv_bwd_kernel<float, KK, OO, 2>)
+                                                            : go(shortconv_bwd_kernel<float, KK, OO, 1>);
+    else
+      nct == 4 ? go(shortconv_bwd_kernel<bf16, KK, OO, 4>) : nct == 2 ? go(shortconv_bwd_kernel<bf16, KK, OO, 2>)
+                                                           : go(shortconv_bwd_kernel<bf16, KK, OO, 1>);
   });
   DNA_LAUNCH_CHECK("dna_hyena_shortconv_bwd");
   return DNA_OK;
