@@ -284,7 +284,10 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float* us = smem;                  // [G][RU][LW]
   float* ds = smem + G * RU * LW;    // [G][RD][LW]
-  float* red = ds + G * RD * LW;     // [4][G * TC][K + 1] row-quarter sums
+  // [4][G * TC][K + 1] row-quarter sums, over the u tile once the dw phase has read it (one more
+  // barrier; 53 KB per block instead of 59: three blocks per CU instead of two)
+  float* red = smem;
+  static_assert(4 * G * TC * (K + 1) <= G * RU * LW, "red must fit in the u tile");
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
   const bool vec = (a.L & 7) == 0;
   struct Regs {
@@ -404,24 +407,35 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
     }
   }
   // dw / dbias: (row quarter, group, channel) per thread, 16 rows each
-  const int items = 4 * G * TC;
-  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+  constexpr int items = 4 * G * TC;
+  constexpr int NH = (items + 255) / 256;  // items per thread
+  float sw[NH][K + 1];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int it = threadIdx.x + 256 * h;
+#pragma unroll
+    for (int k = 0; k <= K; ++k) sw[h][k] = 0.f;
+    if (it >= items) continue;
     const int qr = it / (G * TC), gc = it - qr * (G * TC);
     const int g = gc / TC, j = gc - g * TC;
     const float* dl = ds + g * RD * LW;
     const float* ul = us + g * RU * LW;
-    float sw[K + 1];
-#pragma unroll
-    for (int k = 0; k <= K; ++k) sw[k] = 0.f;
 #pragma unroll 4
     for (int r = 16 * qr; r < 16 * qr + 16; ++r) {
       const float dv = dl[r * LW + j];  // duc at t0 + r (0 past L)
 #pragma unroll
-      for (int k = 0; k < K; ++k) sw[k] = fmaf(dv, ul[(r + k) * LW + j], sw[k]);  // u[t - (K-1-k)]
-      sw[K] += dv;
+      for (int k = 0; k < K; ++k) sw[h][k] = fmaf(dv, ul[(r + k) * LW + j], sw[h][k]);  // u[t - (K-1-k)]
+      sw[h][K] += dv;
     }
+  }
+  __syncthreads();  // every read of the u tile is done: red overwrites it
 #pragma unroll
-    for (int k = 0; k <= K; ++k) red[(qr * G * TC + gc) * (K + 1) + k] = sw[k];
+  for (int h = 0; h < NH; ++h) {
+    const int it = threadIdx.x + 256 * h;
+    if (it < items) {
+#pragma unroll
+      for (int k = 0; k <= K; ++k) red[it * (K + 1) + k] = sw[h][k];
+    }
   }
   __syncthreads();
   const int nL = gridDim.x;
@@ -440,7 +454,8 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
 // Channel tiles per block for the short-conv backward: the 32-channel tiles of a 128-B
 // token-major line run in one block, so the later tiles' u rows are L2 hits (PMC: the one-tile
 // kernel fetched 2x its algorithmic bytes), software-pipelined (above): 4 tiles per block
-// (0.347 -> 0.334 ms at config D, profiles/r05/ab_shortconv_pipelined.txt).
+// (0.347 -> 0.334 ms at config D, profiles/r05/ab_shortconv_pipelined.txt; with the dw partials over
+// the u tile 0.287 ms).
 // DNA_HYENA_NCT = 1 | 2 | 4 (A/B; default 4); fewer when d / 32 does not divide.
 inline int nct_for(int d) {
   static const int env = getenv("DNA_HYENA_NCT") ? atoi(getenv("DNA_HYENA_NCT")) : 4;
@@ -521,8 +536,7 @@ extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w,
   Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part};
   const int nct = nct_for(d);
   const dim3 grid((L + TP - 1) / TP, d / TC / nct, B);
-  const size_t lds = (size_t)(order + 1) * (((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) + 4 * TC * (K + 1)) *
-                     sizeof(float);
+  const size_t lds = (size_t)(order + 1) * ((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) * sizeof(float);
   DNA_CHECK_ARG(lds <= 160 * 1024, "dna_hyena_shortconv_bwd: order %d needs %zu B of LDS", order, lds);
   hipStream_t s = as_stream(stream);
   dispatch_k_ord(K, order, [&](auto kk, auto oo) {
