@@ -30,11 +30,6 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 template <typename T>
 __device__ __forceinline__ T cvt(float v) { return from_f32<T>(v); }
 
-// Load rows [t0 - LO, t0 + TP + HI) x channels [g*d + col0, + TC) of the G channel groups of a
-// token-major [L, ldc] matrix into lds[g][row][TC + PAD] (zero outside [0, L)), 16-byte vectors
-// along the channels. Every load of a thread (all groups) is issued before the first LDS store:
-// these kernels are memory-latency bound (PMC: 78-92 % of wave cycles in s_waitcnt), and a
-// load -> convert -> store loop kept one 16-B load per thread in flight.
 template <typename T, int LO, int HI>
 struct TokTile {
   static constexpr int VE = 16 / sizeof(T);      // elements per vector
@@ -72,6 +67,27 @@ __device__ __forceinline__ void tok_store(float* lds, const uint4 (&raw)[G][NIT]
       const T* e = reinterpret_cast<const T*>(&raw[g][it]);
 #pragma unroll
       for (int q = 0; q < TT::VE; ++q) dst[q] = to_f32(e[q]);
+    }
+}
+// The u tile in the backward's LDS: bf16 rows kept as bf16 (68-B rows: 34 elements), fp32 as fp32
+// (TC + PAD); the raw 16-B vectors stored as 4-B words (rows are 4-B aligned).
+template <typename T> struct UTile {
+  typedef T type;
+  static constexpr int LW = sizeof(T) == 2 ? TC + 2 : TC + PAD;
+};
+template <typename T, int LO, int HI, int G, int NIT = TokTile<T, LO, HI>::NIT>
+__device__ __forceinline__ void tok_store_raw(T* lds, const uint4 (&raw)[G][NIT]) {
+  using TT = TokTile<T, LO, HI>;
+  constexpr int LW = UTile<T>::LW;
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = threadIdx.x + it * 256;
+      if (i >= TT::ROWS * TT::VPR) continue;
+      const int r = i / TT::VPR, cv = (i - r * TT::VPR) * TT::VE;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(lds + (g * TT::ROWS + r) * LW + cv);
+      dst[0] = raw[g][it].x; dst[1] = raw[g][it].y; dst[2] = raw[g][it].z; dst[3] = raw[g][it].w;
     }
 }
 // Load rows [t0 - LO, t0 + TP + HI) x channels [g*d + col0, + TC) of the G channel groups of a
@@ -265,7 +281,7 @@ struct Bwd {
 // u rows reach LDS, so it is in flight during tile ct's compute and stores; the first tile's
 // d(x) and u loads are issued together (one round trip before the first barrier).
 template <typename T, int K, int ORD, int NCT>
-__global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
+__global__ __launch_bounds__(256, sizeof(T) == 2 && NCT <= 2 && ORD == 2 && K <= 3 ? 4 : 1) void shortconv_bwd_kernel(Bwd a) {
   extern __shared__ float smem[];
   constexpr int G = ORD + 1;
   constexpr int RU = TP + 2 * (K - 1);  // u rows: [t0 - (K-1), t0 + TP + K - 1)
@@ -282,12 +298,14 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   const int C = G * a.d;
   const int t0 = blockIdx.x * TP, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float* us = smem;                  // [G][RU][LW]
-  float* ds = smem + G * RU * LW;    // [G][RD][LW]
+  constexpr int LU = UTile<T>::LW;
+  T* us = reinterpret_cast<T*>(smem);                                  // [G][RU][LU], T
+  float* ds = reinterpret_cast<float*>(us + G * RU * LU);             // [G][RD][LW]
   // [4][G * TC][K + 1] row-quarter sums, over the u tile once the dw phase has read it (one more
-  // barrier; 53 KB per block instead of 59: three blocks per CU instead of two)
+  // barrier; with the bf16 u tile 40 KB per block: four blocks per CU)
   float* red = smem;
-  static_assert(4 * G * TC * (K + 1) <= G * RU * LW, "red must fit in the u tile");
+  static_assert(4 * G * TC * (K + 1) * 4 <= G * RU * LU * (int)sizeof(T), "red must fit in the u tile");
+  static_assert((G * RU * LU * sizeof(T)) % 4 == 0, "ds must be 4-B aligned");
   const T* u = (const T*)a.u + (size_t)b * a.L * C;
   const bool vec = (a.L & 7) == 0;
   struct Regs {
@@ -326,7 +344,7 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
   for (int ct = 0; ct < NCT; ++ct) {
   const int c0 = (blockIdx.y * NCT + ct) * TC;
   if (ct > 0) __syncthreads();  // the previous tile's LDS reads are done
-  tok_store<T, K - 1, K - 1, G>(us, cur.raw);
+  tok_store_raw<T, K - 1, K - 1, G>(us, cur.raw);
   __syncthreads();
   Regs nxt;
   if (ct + 1 < NCT) fetch(nxt, c0 + TC);
@@ -342,8 +360,8 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
 #pragma unroll
     for (int k = 0; k < K; ++k) { wl[k] = a.w[chl * K + k]; wvv[k] = a.w[chv * K + k]; }
     const float bl = a.bias[chl], bv = a.bias[chv];
-    const float* tl_l = us + (ORD - 1) * RU * LW;
-    const float* tl_v = us + ORD * RU * LW;
+    const T* tl_l = us + (ORD - 1) * RU * LU;
+    const T* tl_v = us + ORD * RU * LU;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int rr = 8 * pc + i;
@@ -355,8 +373,8 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
         conv_v = bv;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          conv_last = fmaf(wl[k], tl_l[(rr + k) * LW + j], conv_last);
-          conv_v = fmaf(wvv[k], tl_v[(rr + k) * LW + j], conv_v);
+          conv_last = fmaf(wl[k], to_f32(tl_l[(rr + k) * LU + j]), conv_last);
+          conv_v = fmaf(wvv[k], to_f32(tl_v[(rr + k) * LU + j]), conv_v);
         }
       }
       const float dvx = to_f32(reinterpret_cast<const T*>(&cur.dg[n][ORD - 1][0])[i]);
@@ -419,12 +437,12 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
     const int qr = it / (G * TC), gc = it - qr * (G * TC);
     const int g = gc / TC, j = gc - g * TC;
     const float* dl = ds + g * RD * LW;
-    const float* ul = us + g * RU * LW;
+    const T* ul = us + g * RU * LU;
 #pragma unroll 4
     for (int r = 16 * qr; r < 16 * qr + 16; ++r) {
       const float dv = dl[r * LW + j];  // duc at t0 + r (0 past L)
 #pragma unroll
-      for (int k = 0; k < K; ++k) sw[h][k] = fmaf(dv, ul[(r + k) * LW + j], sw[h][k]);  // u[t - (K-1-k)]
+      for (int k = 0; k < K; ++k) sw[h][k] = fmaf(dv, to_f32(ul[(r + k) * LU + j]), sw[h][k]);  // u[t - (K-1-k)]
       sw[h][K] += dv;
     }
   }
@@ -453,13 +471,15 @@ __global__ __launch_bounds__(256) void shortconv_bwd_kernel(Bwd a) {
 
 // Channel tiles per block for the short-conv backward: the 32-channel tiles of a 128-B
 // token-major line run in one block, so the later tiles' u rows are L2 hits (PMC: the one-tile
-// kernel fetched 2x its algorithmic bytes), software-pipelined (above): 4 tiles per block
-// (0.347 -> 0.334 ms at config D, profiles/r05/ab_shortconv_pipelined.txt; with the dw partials over
-// the u tile 0.287 ms).
-// DNA_HYENA_NCT = 1 | 2 | 4 (A/B; default 4); fewer when d / 32 does not divide.
-inline int nct_for(int d) {
-  static const int env = getenv("DNA_HYENA_NCT") ? atoi(getenv("DNA_HYENA_NCT")) : 4;
-  for (int n = env >= 4 ? 4 : env >= 2 ? 2 : 1; n > 1; n /= 2)
+// kernel fetched 2x its algorithmic bytes), software-pipelined (above). bf16: 2 tiles per block
+// (the bf16 u tile + fp32 duc tile are 40 KB and 119 VGPRs: four blocks per CU); fp32: 4 tiles
+// (three blocks per CU). Config D 0.347 -> 0.237 ms per call over the round-5 steps
+// (profiles/r05/ab_shortconv_pipelined.txt). DNA_HYENA_NCT = 1 | 2 | 4 overrides (A/B); fewer
+// when d / 32 does not divide.
+inline int nct_for(int d, int dtype) {
+  static const int env = getenv("DNA_HYENA_NCT") ? atoi(getenv("DNA_HYENA_NCT")) : 0;
+  const int want = env > 0 ? env : (dtype == DNA_BF16 ? 2 : 4);
+  for (int n = want >= 4 ? 4 : want >= 2 ? 2 : 1; n > 1; n /= 2)
     if ((d / TC) % n == 0) return n;
   return 1;
 }
@@ -534,9 +554,11 @@ extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w,
                 "dna_hyena_shortconv_bwd: null pointer");
   DNA_CHECK_ARG(((uintptr_t)u & 15) == 0, "dna_hyena_shortconv_bwd: u must be 16-byte aligned");
   Bwd a{u, w, bias, B, L, d, order, K, dxs, dvx, du, part};
-  const int nct = nct_for(d);
+  const int nct = nct_for(d, dtype);
   const dim3 grid((L + TP - 1) / TP, d / TC / nct, B);
-  const size_t lds = (size_t)(order + 1) * ((TP + 2 * (K - 1)) + (TP + K - 1)) * (TC + PAD) * sizeof(float);
+  const size_t es = dtype == DNA_BF16 ? 2 : 4;
+  const size_t lu = dtype == DNA_BF16 ? TC + 2 : TC + PAD;
+  const size_t lds = (size_t)(order + 1) * ((TP + 2 * (K - 1)) * lu * es + (TP + K - 1) * (TC + PAD) * sizeof(float));
   DNA_CHECK_ARG(lds <= 160 * 1024, "dna_hyena_shortconv_bwd: order %d needs %zu B of LDS", order, lds);
   hipStream_t s = as_stream(stream);
   dispatch_k_ord(K, order, [&](auto kk, auto oo) {
