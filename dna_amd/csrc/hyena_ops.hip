@@ -122,25 +122,58 @@ __global__ __launch_bounds__(256) void shortconv_fwd_kernel(Fwd a) {
   if (ct > 0) __syncthreads();  // the previous tile's LDS reads are done
   load_tok_tiles<T, K - 1, 0, G>(smem, u, a.L, C, t0, a.d, c0);
   __syncthreads();
+  // lane = (channel jj of the wave's 8, chunk pc of 8 positions): the lane's 8 outputs of a group
+  // come from K + 7 LDS reads of one column and leave as one 16-B (bf16) / two 16-B (fp32) store
+  // of the channel-major row (when L % 8 == 0); bank = 8 pc + jj: conflict-free
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int t = t0 + lane;
-  for (int j = wv * CPW; j < wv * CPW + CPW; ++j) {
-    const int c = c0 + j;
-    float last = 0.f;  // conv of group order-1 (x_{order-1})
-    for (int g = 0; g < G; ++g) {
-      const int ch = g * a.d + c;
-      const float* tl = smem + g * R * (TC + PAD);
-      float acc = a.bias[ch];
+  const int jj = lane >> 3, pc = lane & 7;
+  const int j = wv * CPW + jj, c = c0 + j, tl0 = t0 + 8 * pc;
+  const bool full = (a.L & 7) == 0 && tl0 + 8 <= a.L;
+  float last[8];  // conv of group order-1 (x_{order-1})
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc = fmaf(a.w[ch * K + k], tl[(lane + k) * (TC + PAD) + j], acc);
-      if (t < a.L) {
-        if (g < ORD - 1)
-          ((T*)a.xs)[((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L + t] = cvt<T>(acc);
-        else if (g == ORD - 1)
-          last = acc;
-        else
-          ((T*)a.vx)[((size_t)b * a.d + c) * a.L + t] = cvt<T>(acc * last);
+  for (int g = 0; g < G; ++g) {
+    const int ch = g * a.d + c;
+    const float* tl = smem + g * R * (TC + PAD) + j;
+    float xv[8 + K - 1];
+#pragma unroll
+    for (int i = 0; i < 8 + K - 1; ++i) xv[i] = tl[(8 * pc + i) * (TC + PAD)];
+    float wk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[k] = a.w[ch * K + k];
+    const float bc = a.bias[ch];
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float acc = bc;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc = fmaf(wk[k], xv[i + k], acc);
+      o[i] = acc;
+    }
+    if (g == ORD - 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) last[i] = o[i];
+      continue;
+    }
+    if (g == ORD) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] *= last[i];
+    }
+    T* row = g < ORD - 1 ? (T*)a.xs + ((size_t)b * (ORD - 1) * a.d + g * a.d + c) * a.L
+                         : (T*)a.vx + ((size_t)b * a.d + c) * a.L;
+    if (full) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8 v;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (bf16)o[i];
+        *reinterpret_cast<bf16x8*>(row + tl0) = v;
+      } else {
+        *reinterpret_cast<float4*>(row + tl0) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(row + tl0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
       }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (tl0 + i < a.L) row[tl0 + i] = cvt<T>(o[i]);
     }
   }
   }
