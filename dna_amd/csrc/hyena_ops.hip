@@ -179,76 +179,118 @@ __global__ __launch_bounds__(256) void shortconv_fwd_kernel(Fwd a) {
   }
 }
 
-// y[b, t, c] = yc[b, c, t] * x0[b, c, t]
+// 8 consecutive elements <-> fp32 (one 16-B bf16 / two 16-B fp32 accesses; p 16-B aligned)
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 q = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)q[i];
+  } else {
+    const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 q;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = (bf16)v[i];
+    *reinterpret_cast<bf16x8*>(p) = q;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+// bounded forms (the tail of a row, or rows not 16-B aligned)
+template <typename T>
+__device__ __forceinline__ void ld8b(const T* p, int n, float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = i < n ? to_f32(p[i]) : 0.f;
+}
+template <typename T>
+__device__ __forceinline__ void st8b(T* p, int n, const float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < n) p[i] = cvt<T>(v[i]);
+}
+
+// y[b, t, c] = yc[b, c, t] * x0[b, c, t]. Channel-major side: lane = (channel of the wave's 8,
+// chunk of 8 positions), 16-B accesses; token-major side: lane = (row of 16, 8-channel chunk of
+// 4), one 16-B access per row (vec: L, d and the batch stride multiples of 8, aligned rows).
+// LDS rows of TP + 2 floats: both phases conflict-free or 2-way.
+constexpr int GW = TP + 2;
 template <typename T>
 __global__ __launch_bounds__(256) void gate_out_fwd_kernel(const T* yc, const T* x0, int L, int d,
-                                                           size_t x0_bstride, T* y) {
-  __shared__ float tile[TC][TP + PAD];
+                                                           size_t x0_bstride, int vec, T* y) {
+  __shared__ float tile[TC][GW];
   const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  {  // the 8 channel rows of this wave: all 16 loads issued before the products
-    constexpr int NJ = TC / 4;
-    T ly[NJ], lx[NJ];
-    const int t = t0 + lane;
+  {
+    const int j = wv * CPW + (lane >> 3), pc = lane & 7, t = t0 + 8 * pc;
+    const T* py = yc + ((size_t)b * d + c0 + j) * L + t;
+    const T* px = x0 + (size_t)b * x0_bstride + (size_t)(c0 + j) * L + t;
+    float vy[8], vx[8];
+    if (vec && t + 8 <= L) { ld8(py, vy); ld8(px, vx); }
+    else { ld8b(py, L - t, vy); ld8b(px, L - t, vx); }
 #pragma unroll
-    for (int n = 0; n < NJ; ++n) {
-      const int j = wv + 4 * n;
-      const size_t o = ((size_t)b * d + c0 + j) * L + t;
-      ly[n] = t < L ? yc[o] : T(0.f);
-      lx[n] = t < L ? x0[(size_t)b * x0_bstride + (size_t)(c0 + j) * L + t] : T(0.f);
-    }
-#pragma unroll
-    for (int n = 0; n < NJ; ++n) tile[wv + 4 * n][lane] = to_f32(ly[n]) * to_f32(lx[n]);
+    for (int i = 0; i < 8; ++i) tile[j][8 * pc + i] = vy[i] * vx[i];
   }
   __syncthreads();
-  // token-major rows of TC channels: a wave covers 64 / TC rows per pass
-  constexpr int RPW = 64 / TC;
-  const int cl = lane % TC, rsub = lane / TC;
-  for (int r = wv * RPW + rsub; r < TP; r += 4 * RPW) {
+  const int cc8 = 8 * (lane & 3), rsub = lane >> 2;
+  for (int r = wv * 16 + rsub; r < TP; r += 64) {
     const int t = t0 + r;
-    if (t < L) y[((size_t)b * L + t) * d + c0 + cl] = cvt<T>(tile[cl][r]);
+    if (t >= L) break;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = tile[cc8 + e][r];
+    T* o = y + ((size_t)b * L + t) * d + c0 + cc8;
+    if (vec) st8(o, v);
+    else st8b(o, 8, v);
   }
 }
 
-// dyc = dy * x0, dx0 = dy * yc (channel-major outputs; dy token-major)
+// dyc = dy * x0, dx0 = dy * yc (channel-major outputs; dy token-major); the same two lane maps
 template <typename T>
 __global__ __launch_bounds__(256) void gate_out_bwd_kernel(const T* dy, const T* yc, const T* x0,
-                                                           int L, int d, size_t x_bstride, T* dyc,
-                                                           T* dx0) {
+                                                           int L, int d, size_t x_bstride, int vec,
+                                                           T* dyc, T* dx0) {
   __shared__ float tile[TP][TC + PAD];
   const int t0 = blockIdx.x * TP, c0 = blockIdx.y * TC, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  constexpr int RPW = 64 / TC;
-  const int cl = lane % TC, rsub = lane / TC;
-  for (int r = wv * RPW + rsub; r < TP; r += 4 * RPW) {
+  const int j = wv * CPW + (lane >> 3), pc = lane & 7, tl0 = t0 + 8 * pc;
+  const size_t o = ((size_t)b * d + c0 + j) * L + tl0;
+  const size_t ox = (size_t)b * x_bstride + (size_t)(c0 + j) * L + tl0;
+  const bool full = vec && tl0 + 8 <= L;
+  // the channel-major loads first (registers), then dy through LDS
+  float vx[8], vy[8];
+  if (full) { ld8(x0 + ox, vx); ld8(yc + o, vy); }
+  else { ld8b(x0 + ox, L - tl0, vx); ld8b(yc + o, L - tl0, vy); }
+  const int cc8 = 8 * (lane & 3), rsub = lane >> 2;
+  for (int r = wv * 16 + rsub; r < TP; r += 64) {
     const int t = t0 + r;
-    tile[r][cl] = t < L ? to_f32(dy[((size_t)b * L + t) * d + c0 + cl]) : 0.f;
+    float v[8];
+    const T* p = dy + ((size_t)b * L + t) * d + c0 + cc8;
+    if (t >= L) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    } else if (vec) ld8(p, v);
+    else ld8b(p, 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[r][cc8 + e] = v[e];
   }
   __syncthreads();
-  {  // the 8 channel rows of this wave: all 16 loads issued before the products and stores
-    constexpr int NJ = TC / 4;
-    T lx[NJ], ly[NJ];
-    const int t = t0 + lane;
+  if (tl0 >= L) return;
+  float g[8], a[8], c[8];
 #pragma unroll
-    for (int n = 0; n < NJ; ++n) {
-      const int j = wv + 4 * n;
-      const size_t o = ((size_t)b * d + c0 + j) * L + t;
-      const size_t ox = (size_t)b * x_bstride + (size_t)(c0 + j) * L + t;
-      lx[n] = t < L ? x0[ox] : T(0.f);
-      ly[n] = t < L ? yc[o] : T(0.f);
-    }
-    if (t < L) {
-#pragma unroll
-      for (int n = 0; n < NJ; ++n) {
-        const int j = wv + 4 * n;
-        const float g = tile[lane][j];
-        const size_t o = ((size_t)b * d + c0 + j) * L + t;
-        const size_t ox = (size_t)b * x_bstride + (size_t)(c0 + j) * L + t;
-        dyc[o] = cvt<T>(g * to_f32(lx[n]));
-        dx0[ox] = cvt<T>(g * to_f32(ly[n]));
-      }
-    }
+  for (int i = 0; i < 8; ++i) {
+    g[i] = tile[8 * pc + i][j];
+    a[i] = g[i] * vx[i];
+    c[i] = g[i] * vy[i];
   }
+  if (full) { st8(dyc + o, a); st8(dx0 + ox, c); }
+  else { st8b(dyc + o, L - tl0, a); st8b(dx0 + ox, L - tl0, c); }
 }
 
 // The implicit filter's ExponentialModulation fused with the [L, C] -> [O][C/O][L] transpose the
@@ -611,17 +653,25 @@ extern "C" int dna_hyena_shortconv_bwd(const void* u, int dtype, const float* w,
   return DNA_OK;
 }
 
+// the 16-B paths of the gate kernels: every row start 16-B aligned (d % 32 == 0 already)
+static int gate_vec(int L, size_t bstride, std::initializer_list<const void*> ptrs) {
+  int ok = L % 8 == 0 && bstride % 8 == 0;
+  for (const void* p : ptrs) ok = ok && ((uintptr_t)p & 15) == 0;
+  return ok;
+}
+
 extern "C" int dna_hyena_gate_out_fwd(const void* yc, const void* x0, int dtype, int B, int L, int d,
                                       size_t x0_bstride, void* y, void* stream) {
   DNA_CHECK_ARG(yc && x0 && y && B > 0 && L > 0 && d % TC == 0, "dna_hyena_gate_out_fwd: bad args");
   const dim3 grid((L + TP - 1) / TP, d / TC, B);
   hipStream_t s = as_stream(stream);
+  const int vec = gate_vec(L, x0_bstride, {yc, x0, y});
   if (dtype == DNA_F32)
     hipLaunchKernelGGL(gate_out_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)yc,
-                       (const float*)x0, L, d, x0_bstride, (float*)y);
+                       (const float*)x0, L, d, x0_bstride, vec, (float*)y);
   else if (dtype == DNA_BF16)
     hipLaunchKernelGGL(gate_out_fwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)yc,
-                       (const bf16*)x0, L, d, x0_bstride, (bf16*)y);
+                       (const bf16*)x0, L, d, x0_bstride, vec, (bf16*)y);
   else
     DNA_CHECK_ARG(false, "dna_hyena_gate_out_fwd: bad dtype");
   DNA_LAUNCH_CHECK("dna_hyena_gate_out_fwd");
@@ -635,12 +685,13 @@ extern "C" int dna_hyena_gate_out_bwd(const void* dy, const void* yc, const void
                 "dna_hyena_gate_out_bwd: bad args");
   const dim3 grid((L + TP - 1) / TP, d / TC, B);
   hipStream_t s = as_stream(stream);
+  const int vec = gate_vec(L, x_bstride, {dy, yc, x0, dyc, dx0});
   if (dtype == DNA_F32)
     hipLaunchKernelGGL(gate_out_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)dy,
-                       (const float*)yc, (const float*)x0, L, d, x_bstride, (float*)dyc, (float*)dx0);
+                       (const float*)yc, (const float*)x0, L, d, x_bstride, vec, (float*)dyc, (float*)dx0);
   else if (dtype == DNA_BF16)
     hipLaunchKernelGGL(gate_out_bwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)dy,
-                       (const bf16*)yc, (const bf16*)x0, L, d, x_bstride, (bf16*)dyc, (bf16*)dx0);
+                       (const bf16*)yc, (const bf16*)x0, L, d, x_bstride, vec, (bf16*)dyc, (bf16*)dx0);
   else
     DNA_CHECK_ARG(false, "dna_hyena_gate_out_bwd: bad dtype");
   DNA_LAUNCH_CHECK("dna_hyena_gate_out_bwd");
