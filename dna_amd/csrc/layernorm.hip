@@ -59,6 +59,38 @@ __device__ __forceinline__ void store_row(T* p, int lane, const float (&v)[NV]) 
   }
 }
 
+// A row's NV values of a lane as loaded (bf16 kept packed until used), so loads issued for the
+// next row are not waited for by a conversion right after them.
+template <typename T, int NV, bool VEC>
+struct RawRow {
+  static constexpr bool PK = VEC && sizeof(T) == 2;
+  typename std::conditional<PK, bf16x4, T>::type q[PK ? NV / 4 : NV];
+  __device__ __forceinline__ void load(const T* p, int lane) {
+    if constexpr (PK) {
+#pragma unroll
+      for (int k = 0; k < NV; k += 4) q[k / 4] = *reinterpret_cast<const bf16x4*>(p + col_of<VEC>(k, lane));
+    } else if constexpr (VEC) {
+#pragma unroll
+      for (int k = 0; k < NV; k += 4) {
+        f32x4 t = *reinterpret_cast<const f32x4*>(p + col_of<VEC>(k, lane));
+        q[k] = t[0]; q[k + 1] = t[1]; q[k + 2] = t[2]; q[k + 3] = t[3];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) q[k] = p[col_of<VEC>(k, lane)];
+    }
+  }
+  __device__ __forceinline__ void get(float (&v)[NV]) const {
+    if constexpr (PK) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] = (float)q[k / 4][k & 3];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] = to_f32(q[k]);
+    }
+  }
+};
+
 // dropout keep bits for the NV values of a lane in row `row`
 template <int NV, bool VEC>
 __device__ __forceinline__ void keep_bits(bool (&keep)[NV], int row, int cols, int lane,
@@ -174,6 +206,9 @@ __device__ __forceinline__ void block_partials(float (&acc0)[NV], float (&acc1)[
   }
 }
 
+// The row loop is software-pipelined for short rows: the next row's inputs (x, residual, dy, the
+// sum's gradient, mean / rstd) are loaded into raw registers before this row is computed, so each
+// wave keeps two rows' loads in flight (the optional inputs under wave-uniform branches).
 template <typename TX, int NV, bool VEC>
 __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
   const int lane = threadIdx.x & 63;
@@ -184,10 +219,97 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
   load_row<float, NV, VEC>(a.gamma, lane, gam);
   if (a.bias) load_row<float, NV, VEC>(a.bias, lane, bias);
   const float inv_cols = 1.f / a.cols;
+  struct In {
+    RawRow<TX, NV, VEC> x;
+    RawRow<float, NV, VEC> r, dy, ds;
+    RawRow<bf16, NV, VEC> dyb;
+    float mu, rs;
+  };
+  auto fetch = [&](In& f, int row) __attribute__((always_inline)) {
+    const size_t ro = (size_t)row * a.cols;
+    f.x.load(reinterpret_cast<const TX*>(a.x) + ro, lane);
+    if (a.res) f.r.load(a.res + ro, lane);
+    if (a.dy) f.dy.load(a.dy + ro, lane);
+    if (a.dyb) f.dyb.load(a.dyb + ro, lane);
+    if (a.dsum) f.ds.load(a.dsum + ro, lane);
+    f.mu = a.rms ? 0.f : a.mean[row];
+    f.rs = a.rstd[row];
+  };
+  // rows of up to 512 columns; at 768 (DNABERT-2) the second row set takes the kernel past 256
+  // VGPRs and the plain loop below is faster (0.58 vs 0.61 ms, profiles/r05/ab_ln_bwd_prefetch.txt)
+  constexpr bool PF = NV <= 8;
+  if constexpr (!PF) {
+    for (int row = gw; row < a.rows; row += nw) {
+      const size_t ro = (size_t)row * a.cols;
+      float u[NV], v[NV];
+      load_row<TX, NV, VEC>(reinterpret_cast<const TX*>(a.x) + ro, lane, u);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) { u[k] += bias[k]; v[k] = a.act == DNA_ACT_GELU ? gelu_erf(u[k]) : u[k]; }
+      bool keep[NV];
+      if (a.p > 0.f) {
+        keep_bits<NV, VEC>(keep, row, a.cols, lane, a.seed, a.off, a.th);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = keep[k] ? v[k] * a.kscale : 0.f;
+      }
+      if (a.res) {
+        float r[NV];
+        load_row<float, NV, VEC>(a.res + ro, lane, r);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] += r[k];
+      }
+      const float mu = a.rms ? 0.f : a.mean[row], rs = a.rstd[row];
+      float g[NV];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) g[k] = 0.f;
+      if (a.dy) load_row<float, NV, VEC>(a.dy + ro, lane, g);
+      if (a.dyb) {
+        float t[NV];
+        load_row<bf16, NV, VEC>(a.dyb + ro, lane, t);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) g[k] += t[k];
+      }
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const float xh = (v[k] - mu) * rs;
+        v[k] = xh;
+        acc_g[k] += g[k] * xh;
+        acc_b[k] += g[k];
+        const float gy = g[k] * gam[k];
+        g[k] = gy;
+        s1 += gy;
+        s2 += gy * xh;
+      }
+      const float c1 = a.rms ? 0.f : wave_sum(s1) * inv_cols, c2 = wave_sum(s2) * inv_cols;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) g[k] = rs * (g[k] - c1 - v[k] * c2);  // d(pre-LN sum)
+      if (a.dsum) {  // the sum's other consumers (the residual stream): total gradient of the sum
+        float t[NV];
+        load_row<float, NV, VEC>(a.dsum + ro, lane, t);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) g[k] += t[k];
+      }
+      if (a.dres) store_row<float, NV, VEC>(a.dres + ro, lane, g);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        float d = g[k];
+        if (a.p > 0.f) d = keep[k] ? d * a.kscale : 0.f;
+        if (a.act == DNA_ACT_GELU) d *= gelu_erf_grad(u[k]);
+        g[k] = d;
+        acc_x[k] += d;
+      }
+      store_row<TX, NV, VEC>(reinterpret_cast<TX*>(a.dx) + ro, lane, g);
+    }
+  } else {
+  In nx;
+  if (gw < a.rows) fetch(nx, gw);
   for (int row = gw; row < a.rows; row += nw) {
     const size_t ro = (size_t)row * a.cols;
+    const In cur = nx;
+    // the next row (the last row again past the end: an L2 hit, no branch around the loads)
+    fetch(nx, row + nw < a.rows ? row + nw : row);
     float u[NV], v[NV];
-    load_row<TX, NV, VEC>(reinterpret_cast<const TX*>(a.x) + ro, lane, u);
+    cur.x.get(u);
 #pragma unroll
     for (int k = 0; k < NV; ++k) { u[k] += bias[k]; v[k] = a.act == DNA_ACT_GELU ? gelu_erf(u[k]) : u[k]; }
     bool keep[NV];
@@ -198,18 +320,18 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
     }
     if (a.res) {
       float r[NV];
-      load_row<float, NV, VEC>(a.res + ro, lane, r);
+      cur.r.get(r);
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[k] += r[k];
     }
-    const float mu = a.rms ? 0.f : a.mean[row], rs = a.rstd[row];
+    const float mu = cur.mu, rs = cur.rs;
     float g[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) g[k] = 0.f;
-    if (a.dy) load_row<float, NV, VEC>(a.dy + ro, lane, g);
+    if (a.dy) cur.dy.get(g);
     if (a.dyb) {
       float t[NV];
-      load_row<bf16, NV, VEC>(a.dyb + ro, lane, t);
+      cur.dyb.get(t);
 #pragma unroll
       for (int k = 0; k < NV; ++k) g[k] += t[k];
     }
@@ -230,7 +352,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
     for (int k = 0; k < NV; ++k) g[k] = rs * (g[k] - c1 - v[k] * c2);  // d(pre-LN sum)
     if (a.dsum) {  // the sum's other consumers (the residual stream): total gradient of the sum
       float t[NV];
-      load_row<float, NV, VEC>(a.dsum + ro, lane, t);
+      cur.ds.get(t);
 #pragma unroll
       for (int k = 0; k < NV; ++k) g[k] += t[k];
     }
@@ -244,6 +366,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
       acc_x[k] += d;
     }
     store_row<TX, NV, VEC>(reinterpret_cast<TX*>(a.dx) + ro, lane, g);
+  }
   }
   block_partials<NV, VEC>(acc_g, acc_b, acc_x, a.cols, a.part);
 }

@@ -95,7 +95,9 @@ def main():
                 frames = [f"{os.path.basename(fr.filename)}:{fr.lineno}"
                           for fr in traceback.extract_stack()[:-1]
                           if "dna_amd" in fr.filename or "scripts" in fr.filename]
-                sites[(name, " <- ".join(reversed(frames[-3:])))] += 1
+                shp = "x".join(str(v) for v in args[0].shape) if args and hasattr(args[0], "shape") else ""
+                dt = str(args[0].dtype).replace("torch.", "") if args and hasattr(args[0], "dtype") else ""
+                sites[(name, (" <- ".join(reversed(frames[-3:])) or "(autograd)") + f" [{shp} {dt}]")] += 1
             return func(*args, **(kwargs or {}))
 
     with Census():
