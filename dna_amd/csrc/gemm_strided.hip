@@ -111,7 +111,7 @@ __device__ __forceinline__ bf16x8 frag(const bf16* img, int base, int lane) {
 }
 
 template <bool AKC, bool BKC, bool F32>
-__global__ __launch_bounds__(NT) void sgemm_kernel(Args a) {
+__global__ __launch_bounds__(NT, 4) void sgemm_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2][2][IMG];  // [buffer][A, B]
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
