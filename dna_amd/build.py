@@ -32,6 +32,11 @@ HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-I", INCLU
 # turns the per-score multiplies into v_pk_mul_f32 on odd register pairs (v_mov/v_alignbit
 # shuffles around every pair, and packed f32 beside MFMAs is slower anyway)
 FILE_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize"]}
+# experiment hook: DNA_AMD_FILE_FLAGS="gemm.hip:-fno-slp-vectorize -DX=1;other.hip:..." adds flags
+# per file (the object is rebuilt whenever its command line changes)
+for _item in filter(None, os.environ.get("DNA_AMD_FILE_FLAGS", "").split(";")):
+    _f, _, _fl = _item.partition(":")
+    FILE_FLAGS[_f.strip()] = FILE_FLAGS.get(_f.strip(), []) + _fl.split()
 CXX_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-I", INCLUDE, "-I", CSRC, "-Wall",
              "-Wno-unused-function"]
 
@@ -43,15 +48,21 @@ def _headers_mtime():
 
 def _compile(src):
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
-        return obj, None
     if src.endswith(".hip"):
         cmd = [HIPCC] + HIP_FLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     else:
         cmd = ["g++"] + CXX_FLAGS + ["-c", src, "-o", obj]
+    stamp = obj + ".cmd"
+    line = " ".join(cmd)
+    prev = open(stamp).read() if os.path.exists(stamp) else None
+    if (os.path.exists(obj) and (prev == line or (prev is None and not os.environ.get("DNA_AMD_FILE_FLAGS")))
+            and os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime())):
+        return obj, None
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+        return obj, f"$ {line}\n{r.stdout}\n{r.stderr}"
+    with open(stamp, "w") as f:
+        f.write(line)
     return obj, None
 
 

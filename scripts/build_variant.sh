@@ -10,6 +10,7 @@ TMP=$(mktemp -d /tmp/dna_variant.XXXXXX)
 git -C "$ROOT" archive "$REV" | tar -x -C "$TMP"
 mkdir -p "$TMP/build/native"
 # reuse object files of unchanged sources (same content => same object)
+# (DNA_AMD_FILE_FLAGS in the environment adds per-file compiler flags: dna_amd/build.py)
 (cd "$TMP" && python -m dna_amd.build > /dev/null)
 cp "$TMP/dna_amd/lib/libdna_amd.so" "$ROOT/dna_amd/lib/libdna_amd_$NAME.so"
 rm -rf "$TMP"

@@ -136,7 +136,8 @@ pmc)
       -- "$@" > $OUT/set_$i.log 2>&1
   done
   python $ROOT/scripts/pmc_table.py $OUT --kernel "$KRE" > $OUT/summary.txt 2>&1 || true
-  cat $OUT/summary.txt
+  python $ROOT/scripts/pmc_table.py $OUT --kernel "$KRE" --per-kernel > $OUT/per_kernel.txt 2>&1 || true
+  cat $OUT/per_kernel.txt
   ;;
 *)
   sed -n 2,20p "$0"

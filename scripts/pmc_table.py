@@ -14,19 +14,24 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--kernel", default="dna|gemm|attn")
+    ap.add_argument("--per-kernel", action="store_true",
+                    help="one table per (job, kernel name) instead of one per job")
     a = ap.parse_args()
     pat = re.compile(a.kernel)
     jobs = collections.defaultdict(dict)
     for f in sorted(glob.glob(os.path.join(a.root, "*", "run_counter_collection.csv"))):
-        job = os.path.basename(os.path.dirname(f)).rsplit("_", 1)[0]
+        job0 = os.path.basename(os.path.dirname(f)).rsplit("_", 1)[0]
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if not pat.search(row["Kernel_Name"]):
                     continue
-                per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
-        for c, d in per.items():
+                key = row["Kernel_Name"].split("(")[0][:60] if a.per_kernel else ""
+                per[(key, row["Counter_Name"])][row["Dispatch_Id"]] += float(row["Counter_Value"])
+        for (key, c), d in per.items():
+            job = f"{key}" if a.per_kernel else job0
             jobs[job][c] = sum(d.values()) / len(d)
+            jobs[job]["dispatches"] = max(jobs[job].get("dispatches", 0), len(d))
     for job, cs in jobs.items():
         print(f"== {job}")
         for c in sorted(cs):
