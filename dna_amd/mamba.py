@@ -332,14 +332,17 @@ class InProj(torch.autograd.Function):
             if not halves:
                 if not acc:
                     dh.zero_()
-            elif len(halves) == 2 and dt == torch.bfloat16:
+            elif len(halves) == 2 and dt == torch.bfloat16 and E % 32 == 0:
+                # the two-operand contraction splits K at E, which must be a whole number of
+                # the kernel's 32-deep K-steps (dna_gemm_bf16_strided_cat); other E take the
+                # concatenated operand below
                 with _timed("mamba_proj", (2 * T * E + (3 if acc else 1) * T * d) * es, "byte"):
                     N.call("dna_gemm_bf16_strided_cat", halves[0][1].data_ptr(),
                            halves[1][1].data_ptr(), E, 1, L, E * L, w.data_ptr(), d, 1, 0,
                            cbase.data_ptr(), ldc, L * d, 2 if acc else 0, None, None, L, d, E2,
                            b, 1, N.stream_ptr())
             else:
-                if len(halves) == 2:  # fp32 parity mode: one operand of both halves
+                if len(halves) == 2:  # fp32 parity mode / E % 32 != 0: one operand of both halves
                     g, wi = torch.cat([halves[0][1], halves[1][1]], 1), w
                 else:
                     i, g = halves[0]

@@ -43,6 +43,32 @@ def test_caduceus_vs_oracle(rms, strategy):
         assert _rel(p.grad, sd[n].grad) < 2e-3, n
 
 
+@pytest.mark.parametrize("d_model", [24, 40])
+def test_caduceus_odd_d_inner_autocast(d_model):
+    """d_inner = 2 * d_model not a multiple of 32 (48, 80): in_proj's data gradient cannot take
+    the two-operand contraction (it splits K at d_inner in 32-deep steps), so it runs on the
+    concatenated operand. bf16-autocast gradients vs the fp32 run of the same model."""
+    from dna_amd.caduceus import CaduceusForMaskedLM
+    torch.manual_seed(11)
+    m = CaduceusForMaskedLM(d_model=d_model, n_layer=2, vocab_size=12,
+                            ssm_cfg={"d_state": 16}).to(DEV)
+    ids = torch.randint(0, 12, (2, 256), device=DEV, generator=torch.Generator(DEV).manual_seed(2))
+    grads = []
+    for ac in (False, True):
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=ac):
+            _, logits = m(ids)
+        loss = torch.nn.functional.cross_entropy(logits.float().reshape(-1, logits.shape[-1]),
+                                                 ids.reshape(-1))
+        loss.backward()
+        grads.append({n: p.grad.detach().float().clone() for n, p in m.named_parameters()
+                      if p.grad is not None})
+    assert any("in_proj" in n for n in grads[1])
+    for n, g in grads[0].items():
+        assert torch.isfinite(grads[1][n]).all(), n
+        assert _rel(grads[1][n], g) < 6e-2, n
+
+
 @pytest.mark.parametrize("autocast", [True, False])
 def test_caduceus_model_has_no_library_gemm(autocast, monkeypatch):
     """Config E's model (bidirectional Mamba mixer: in_proj, x_proj, dt_proj, out_proj, the LM

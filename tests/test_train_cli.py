@@ -110,6 +110,11 @@ def test_train_config_a_runs_on_gpu(data_root, monkeypatch, tmp_path):
     # (monitor test/loss, mode min) writes checkpoints/test/loss.ckpt
     ev = [l for l in logs if "val/loss" in l]
     assert len(ev) == 1 and ev[0]["step"] == 6
+    # Timer callback (configs/callbacks/base.yaml: step, epoch, val) and trainer/epoch
+    assert all(l["trainer/epoch"] == l["epoch"] for l in train_logs)
+    assert ev[0]["timer/validation"] > 0
+    te = [l for l in logs if "timer/epoch" in l]
+    assert len(te) == 1 and te[0]["timer/epoch"] >= ev[0]["timer/validation"]
     for k in ("val/loss", "val/perplexity", "test/loss", "test/perplexity"):
         assert math.isfinite(ev[0][k]), k
     assert abs(ev[0]["val/perplexity"] - math.exp(ev[0]["val/loss"])) < 1e-3 * ev[0]["val/perplexity"]
@@ -268,6 +273,16 @@ def test_mid_epoch_resume_replays_the_uninterrupted_run(data_root, monkeypatch, 
     ck = torch.load(tmp_path / "b" / "checkpoints" / "last.ckpt", map_location="cpu",
                     weights_only=True)
     assert ck["loops"]["fit_loop"]["epoch_loop.batch_progress"]["current"]["completed"] == 2
-    rest = run(tmp_path / "b", 4, resume=str(tmp_path / "b" / "checkpoints" / "last.ckpt"))
+    ck_path = tmp_path / "b" / "checkpoints" / "last.ckpt"
+    if fault_tolerant:
+        # a reference / Lightning checkpoint has the loop counters but not this engine's
+        # batches_done: the data module's load_state_dict fast-forwards from the counters
+        lt = dict(ck, dna_amd={k: v for k, v in ck["dna_amd"].items() if k != "batches_done"})
+        (tmp_path / "c").mkdir()
+        torch.save(lt, tmp_path / "c" / "loops_only.ckpt")
+    rest = run(tmp_path / "b", 4, resume=str(ck_path))
     assert first == {1: full[1], 2: full[2]}
     assert rest == {3: full[3], 4: full[4]}, (rest, full)
+    if fault_tolerant:
+        rest2 = run(tmp_path / "c", 4, resume=str(tmp_path / "c" / "loops_only.ckpt"))
+        assert rest2 == {3: full[3], 4: full[4]}, (rest2, full)

@@ -64,10 +64,17 @@ def test_params_log():
 
 
 def test_model_checkpoint_state_key_and_resume(tmp_path):
-    best = train.BestCheckpoint(str(tmp_path), "test/loss", mode="min", every_n_train_steps=0)
+    # Lightning 1.8 __init_triggers: every_n_epochs = 1 only when no trigger is given at all
+    best = train.BestCheckpoint(str(tmp_path), "test/loss", mode="min")
     assert best.state_key == ("ModelCheckpoint{'monitor': 'test/loss', 'mode': 'min', "
                               "'every_n_train_steps': 0, 'every_n_epochs': 1, "
                               "'train_time_interval': None}")
+    assert "'every_n_train_steps': 1000, 'every_n_epochs': 0," in train.BestCheckpoint(
+        str(tmp_path), "test/loss", every_n_train_steps=1000).state_key
+    assert "'every_n_train_steps': 0, 'every_n_epochs': 2," in train.BestCheckpoint(
+        str(tmp_path), "test/loss", every_n_epochs=2).state_key
+    assert "'every_n_train_steps': 0, 'every_n_epochs': 0," in train.BestCheckpoint(
+        str(tmp_path), "test/loss", every_n_train_steps=0).state_key
     best.score = 1.25
     st = best.state_dict()
     assert isinstance(st["best_model_score"], torch.Tensor) and float(st["best_model_score"]) == 1.25
@@ -84,6 +91,22 @@ def test_model_checkpoint_state_key_and_resume(tmp_path):
     b4 = train.BestCheckpoint(str(tmp_path), "val/loss")  # another monitor: not restored
     b4.load_from_checkpoint(torch.load(path, weights_only=True))
     assert b4.score is None
+
+
+def test_checkpoint_loops_are_whole_lightning_progress_states():
+    """The fit-loop counters are complete Lightning 1.8 Progress / BatchProgress states: every
+    tracker of `total` and `current` (Progress.load_state_dict indexes both) and is_last_batch
+    (BatchProgress) -- ADVICE r5; the reference's data module reads current.completed."""
+    ep = train._progress(3)
+    bp = dict(train._progress(11), is_last_batch=False)
+    for st in (ep, bp):
+        for part in ("total", "current"):
+            assert set(st[part]) == {"ready", "started", "processed", "completed"}
+    from dna_amd.hg38 import BertHG38
+    d = BertHG38(fault_tolerant=True, ddp=True, shuffle=True)
+    d.load_state_dict({"loops": {"fit_loop": {"epoch_progress": ep,
+                                              "epoch_loop.batch_progress": bp}}})
+    assert (d.fast_forward_epochs, d.fast_forward_batches) == (3, 11)
 
 
 def _shard(n, world, rank, epoch, seed=0):

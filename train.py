@@ -79,6 +79,14 @@ def load_lightning_state(model, path, strict):
     return missing, unexpected
 
 
+def _progress(n):
+    """A Lightning 1.8 `Progress` state dict whose trackers all stand at n (ready == started ==
+    processed == completed: the counted units finished); `total` = `current` here, since the
+    run's earlier epochs are not kept per batch."""
+    t = {"ready": int(n), "started": int(n), "processed": int(n), "completed": int(n)}
+    return {"total": dict(t), "current": dict(t)}
+
+
 def save_checkpoint(path, trainer, epoch, batches_done=0, metrics=None, best=None):
     """Lightning-1.8 checkpoint layout: state_dict with the "model." prefix, torch AdamW
     optimizer state, timm scheduler state, epoch / global_step; plus this engine's dropout-stream
@@ -93,10 +101,11 @@ def save_checkpoint(path, trainer, epoch, batches_done=0, metrics=None, best=Non
           "dna_amd": {"dropout_rng": trainer.rng_state(), "batches_done": int(batches_done),
                       "metrics": metrics or {}},
           # the two Lightning loop counters the reference's fault-tolerant data modules read on
-          # resume (genomics.py:1249-1253)
-          "loops": {"fit_loop": {"epoch_progress": {"current": {"completed": int(epoch)}},
-                                 "epoch_loop.batch_progress": {"current": {"completed":
-                                                                           int(batches_done)}}}}}
+          # resume (genomics.py:1249-1253), as whole Lightning 1.8 Progress / BatchProgress
+          # states (total + current trackers), so Loop._load_from_state_dict can restore them
+          "loops": {"fit_loop": {"epoch_progress": _progress(epoch),
+                                 "epoch_loop.batch_progress": dict(_progress(batches_done),
+                                                                   is_last_batch=False)}}}
     if best is not None:  # ModelCheckpoint state, keyed and typed as Lightning 1.8 keeps it
         ck["callbacks"] = {best.state_key: best.state_dict()}
     os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
@@ -135,8 +144,13 @@ class BestCheckpoint:
             raise NotImplementedError(f"model_checkpoint.save_top_k={save_top_k} (1 or 0)")
         self.path = os.path.join(dirpath, (filename or monitor or "best") + ".ckpt")
         self.dirpath = dirpath
-        self.every_n_train_steps = int(every_n_train_steps or 0)
-        self.every_n_epochs = int(every_n_epochs if every_n_epochs is not None else 1)
+        # Lightning 1.8 ModelCheckpoint.__init_triggers: every_n_epochs defaults to 1 only when
+        # no trigger at all is given, otherwise a missing one counts as 0
+        if every_n_train_steps is None and every_n_epochs is None:
+            self.every_n_epochs, self.every_n_train_steps = 1, 0
+        else:
+            self.every_n_epochs = int(every_n_epochs or 0)
+            self.every_n_train_steps = int(every_n_train_steps or 0)
         self.score = None
 
     @property
@@ -340,6 +354,7 @@ def train(cfg, dry_run=False, out=sys.stdout):
                           "global_batch": int(cfg.dataset.get("batch_size", 0) or 0) * world}),
               file=out, flush=True)
     ck_cfg = cfg.get("callbacks", {}) or {}
+    timer_cfg = (ck_cfg.get("timer") if ck_cfg else None) or {}  # configs/callbacks/base.yaml
     if rank == 0 and ck_cfg and ck_cfg.get("params") is not None:
         print(json.dumps(dict({"event": "params"}, **params_log(model, ck_cfg.params))),
               file=out, flush=True)
@@ -369,6 +384,13 @@ def train(cfg, dry_run=False, out=sys.stdout):
                 trainer.model.dropout_rng.seed = (trainer.model.dropout_rng.seed + rank) & (2 ** 63 - 1)
             skip_batches = int(extra.get("batches_done", 0))
             restored = extra.get("metrics") or {}
+            if "batches_done" not in extra and "loops" in ck and \
+                    getattr(ds, "fault_tolerant", False) and hasattr(ds, "load_state_dict"):
+                # a reference / Lightning checkpoint: the data module reads the fit loop's
+                # counters (genomics.py:1249-1253) and the sampler fast-forwards from them
+                ds.load_state_dict(ck)
+                start_epoch = int(ds.fast_forward_epochs)
+                skip_batches = int(ds.fast_forward_batches)
         else:
             warnings.warn(f"resume checkpoint {resume} not found; training from scratch")
 
@@ -446,7 +468,7 @@ def train(cfg, dry_run=False, out=sys.stdout):
         now = time.perf_counter()
         if rank == 0:
             print(json.dumps({"step": step, "epoch": epoch, "train/loss": round(lv, 5),
-                              "trainer/loss": round(lv, 5),
+                              "trainer/loss": round(lv, 5), "trainer/epoch": epoch,
                               "train/perplexity": round(math.exp(sums[0] / max(sums[1], 1)), 4),
                               "train/num_tokens": int(sums[2]),
                               "trainer/lr": trainer.opt.param_groups[0]["lr"],
@@ -463,8 +485,12 @@ def train(cfg, dry_run=False, out=sys.stdout):
         lim = limit_test if final else limit_val
         if lim is not None and not isinstance(lim, bool) and float(lim) == 0.0:
             return {}  # limit_{val,test}_batches=0: the evaluation loop is disabled
+        t_val = time.perf_counter()
         res = evaluate(trainer, loaders, device, pad_id,
                        limit=limit_test if final else limit_val, tokens=eval_tokens)
+        if res and not final and timer_cfg.get("val", True):
+            # Timer.on_validation_epoch_end (src/callbacks/timer.py:91-96)
+            res = dict(res, **{"timer/validation": round(time.perf_counter() - t_val, 5)})
         if rank == 0 and res:
             print(json.dumps(dict({"step": trainer.global_step, "epoch": epoch},
                                   **{k: (round(v, 6) if isinstance(v, float) else v)
@@ -492,6 +518,7 @@ def train(cfg, dry_run=False, out=sys.stdout):
         run_eval()
 
     for epoch in range(start_epoch, max_epochs):
+        t_epoch = time.perf_counter()  # Timer.on_train_epoch_start (src/callbacks/timer.py:38-41)
         if hasattr(loader.sampler, "set_epoch"):
             loader.sampler.set_epoch(epoch)  # EpochSampler: forwarded to the DistributedSampler
         else:
@@ -537,6 +564,12 @@ def train(cfg, dry_run=False, out=sys.stdout):
         # end of the epoch (or of the run at max_steps): the validation epoch (val + test
         # loaders), then ModelCheckpoint on its metrics; a resume starts at the next batch
         metrics = run_eval()
+        if rank == 0 and timer_cfg.get("epoch", True):
+            # Timer.on_train_epoch_end (src/callbacks/timer.py:80-86); Lightning 1.8 calls it
+            # after the epoch-end validation loop, so the epoch time includes it
+            print(json.dumps({"step": trainer.global_step, "epoch": epoch,
+                              "timer/epoch": round(time.perf_counter() - t_epoch, 5)}),
+                  file=out, flush=True)
         checkpoint(epoch + 1, 0, metrics) if not done else checkpoint(epoch, bi + 1, metrics)
         if done:
             break
