@@ -44,13 +44,22 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 // ---------------------------------------------------------------------------------------- RNG
 // Philox4x32-10 (Salmon et al., SC'11): counter-based, so the backward pass regenerates the
 // forward dropout mask from (seed, offset, element index) instead of storing it.
+// Timing-only diagnostic builds (scripts/build_variant.sh with DNA_AMD_FILE_FLAGS): DNA_DBG_EPI
+// bit 0 replaces erf by the identity, DNA_PHILOX_ROUNDS changes the round count. Never set in
+// the product build (results change).
+#ifndef DNA_DBG_EPI
+#define DNA_DBG_EPI 0
+#endif
+#ifndef DNA_PHILOX_ROUNDS
+#define DNA_PHILOX_ROUNDS 10
+#endif
 struct Philox {
   __device__ __forceinline__ static uint4 gen(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1) {
     // each round's two 32x32 -> 64-bit products as one 64-bit multiply apiece (the pair
     // v_mul_hi_u32 + v_mul_lo_u32 per product otherwise; same bits either way)
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < DNA_PHILOX_ROUNDS; ++r) {
       const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
       const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
       const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
@@ -108,6 +117,10 @@ __host__ __device__ __forceinline__ uint32_t dropout_threshold(float p) {
 // largest VALU cost of the GeGLU kernels. GELU from it: |error| < 5e-7 on [-10, 10] (checked
 // against math.erf), below bf16 resolution of every tensor it feeds.
 __device__ __forceinline__ float erf_fast(float z, float& e) {
+  if constexpr (DNA_DBG_EPI & 1) {
+    e = z;
+    return z;
+  }
   const float az = fabsf(z);
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
   float p = fmaf(1.061405429f, t, -1.453152027f);

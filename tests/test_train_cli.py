@@ -216,26 +216,30 @@ def test_train_devices_2_starts_two_ranks(data_root, tmp_path):
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_real_model(tmp_path):
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_bench_multi_rank_real_model(tmp_path, ranks):
     """bench.py's own world > 1 path with the real DNABERT-2 step (not the --dist-dry-run
     skeleton): process group init, the model step with GradBucketReducer, max-over-ranks timing,
-    one JSON line from rank 0 -- two gloo ranks on the test box's GPU."""
+    one JSON line from rank 0 -- gloo ranks on the test box's GPU. ranks=8 rehearses the
+    driver's SCALE command (`bench.py --gpus 8`: the launcher, 8 children, the port, the
+    rank -> device binding) with every rank bound to the one visible GPU."""
     dump = str(tmp_path / "dump")
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(ranks), "--steps", "2",
            "--warmup", "1", "--batch", "8", "--no-cpu-baseline", "--no-b64", "--no-data-pipeline",
            "--dump-params", dump]
     env = _two_rank_env("", dump)
     env.pop("DNA_DUMP_PARAMS")
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     line = lines[0]
-    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
-    assert line["config"]["global_batch"] == 16 and line["value"] > 0
+    assert line["n_gpus"] == ranks and line["config"]["parallelism"] == f"dp{ranks}"
+    assert line["config"]["global_batch"] == 8 * ranks and line["value"] > 0
     assert math.isfinite(line["final_loss"])
-    d0, d1 = _digests(dump, 2)
-    assert d0["sha256"] == d1["sha256"], (d0, d1)
+    ds = _digests(dump, ranks)
+    assert len({d["sha256"] for d in ds}) == 1, ds
+    assert all(d["global_step"] == ds[0]["global_step"] for d in ds)
 
 
 @pytest.mark.gpu
