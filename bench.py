@@ -244,6 +244,8 @@ def main():
     if data_pipeline is not None:
         data_pipeline["bench_batch_prep_seq_per_s"] = round(4 * args.batch / t_data, 1)
 
+    if rank == 0:  # progress on stderr (the stdout line is the result)
+        print(f"bench.py: {world} rank(s), model and batches ready", file=sys.stderr, flush=True)
     for i in range(args.warmup):
         trainer.step(batches[i % len(batches)])
     if world > 1:

@@ -58,6 +58,8 @@ _SIGS = {
     "dna_ln_bwd_workspace": (_sz, [_i, _i]),
     "dna_ln_bwd": (_i, [_vp, _vp, _vp, _i, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _vp, _i, _i,
                         _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dna_ln_bwd_from_y": (_i, [_vp, _vp, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _i, _i, _vp,
+                               _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dna_add_ln_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dna_add_ln_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp,
                             _vp, _vp, _sz, _vp]),
@@ -73,8 +75,8 @@ _SIGS = {
     "dna_embed_grad_segsum": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "dna_sum_slices_accum": (_i, [_vp, _i, _sz, _vp, _vp]),
     "dna_sum_slices": (_i, [_vp, _i, _sz, _vp, _vp]),
-    "dna_geglu_fwd": (_i, [_vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
-    "dna_geglu_bwd": (_i, [_vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
+    "dna_geglu_fwd": (_i, [_vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
+    "dna_geglu_bwd": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_linear_dgrad": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_linear_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
@@ -94,8 +96,8 @@ _SIGS = {
                                   _vp, _i, _i, _i, _i, _i, _vp]),
     "dna_linear_wgrad_p": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_geglu_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
-    "dna_geglu_linear_dgrad": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
-    "dna_geglu_linear_dgrad_p": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp]),
+    "dna_geglu_linear_dgrad": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
+    "dna_geglu_linear_dgrad_p": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_gelu_linear_dgrad_p": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_fftconv_workspace": (_sz, [_i, _i, _i]),
     "dna_fftconv_kspec_elems": (_sz, [_i]),

@@ -142,6 +142,25 @@ __device__ __forceinline__ void gelu_erf_and_grad(float x, float& g, float& dg) 
   g = x * cdf;
   dg = fmaf(x * 0.3989422804014327f, e, cdf);  // e = exp(-x^2 / 2)
 }
+// GeGLU forward and its backward factors (bert_layers.py:292-296), for h1 = g[:, :F], h2 =
+// g[:, F:] (the bf16-rounded gated_layers outputs), the element's dropout keep bit and
+// ks = 1 / (1 - p) (p = 0: kept, ks = 1):
+//   s    = kept ? ks : 0
+//   fac2 = gelu(h1) s                    (= d a / d h2)
+//   a    = fac2 h2
+//   fac1 = gelu'(h1) s h2                (= d a / d h1)
+// The forward stores fac = [fac1 | fac2] where g would have gone (same bytes), so the backward is
+// dg = da * fac: no erf and no keep-bit draws there (csrc/gemm.hip, csrc/geglu.hip).
+__device__ __forceinline__ void geglu_fwd_fac(float h1, float h2, bool kept, float ks, float& a,
+                                              float& f1, float& f2) {
+  float ge, dge;
+  gelu_erf_and_grad(h1, ge, dge);
+  const float s = kept ? ks : 0.f;
+  f2 = ge * s;
+  a = f2 * h2;
+  f1 = dge * s * h2;
+}
+
 // d/dx of the tanh-approximation GELU 0.5 x (1 + tanh(k (x + 0.044715 x^3))), k = sqrt(2/pi),
 // in the operation order of torch's GeluBackward (approximate="tanh")
 __device__ __forceinline__ float gelu_tanh_grad(float x) {

@@ -1,8 +1,12 @@
 // GeGLU (+ dropout) of BertGatedLinearUnitMLP (bert_layers.py:292-296), fwd and bwd.
 //   a = dropout( gelu_erf(g[:, :F]) * g[:, F:] ),  g = gated_layers(x) with F = intermediate_size.
+// The forward also writes the backward factors fac = [d a / d g1 | d a / d g2] (common.h
+// geglu_fwd_fac: dropout and 1/(1-p) folded in), optionally over g itself, so the backward is
+// dg = da * fac -- the same arithmetic as the fused GEMM epilogues (csrc/gemm.hip).
 // HBM-bound elementwise: 8 consecutive outputs per thread (16-B bf16 vectors), grid-stride,
 // U rows per thread per iteration.
-// Algorithmic bytes per output element: fwd 2*s (read g1, g2) + s (write a); bwd 3*s + 2*s.
+// Algorithmic bytes per output element: fwd 2*s (read g1, g2) + s (write a) [+ 2*s fac];
+// bwd 3*s + 2*s.
 // Dropout bits: dropout_keep8 (16-bit slices of one Philox draw per 8 elements).
 #include "common.h"
 
@@ -42,9 +46,10 @@ __device__ __forceinline__ uint32_t keep8(uint64_t seed, uint64_t off, uint64_t 
 // keeps U*2 (fwd) / U*3 (bwd) 16-B vectors per lane in flight instead of 2 / 3 (the U=1 kernels
 // reached only 66 % of HBM bandwidth at the bench shape).
 template <typename T, int U>
-__global__ __launch_bounds__(128) void fwd_kernel(const T* __restrict__ g, int rows, int F,
+__global__ __launch_bounds__(128) void fwd_kernel(const T* g, int rows, int F,
                                                   float p, uint32_t th, float ks, uint64_t seed,
-                                                  uint64_t off, T* __restrict__ a) {
+                                                  uint64_t off, T* __restrict__ a, T* fac) {
+  // fac may alias g (each thread reads its g1 / g2 vectors before writing the same places)
   // 2-D launch: blockIdx.y walks row groups, x covers one row's F/8 vectors (no 64-bit div/mod)
   const int f8 = F / 8;
   for (int r0 = blockIdx.y * U; r0 < rows; r0 += gridDim.y * U)
@@ -62,22 +67,23 @@ __global__ __launch_bounds__(128) void fwd_kernel(const T* __restrict__ g, int r
       const int r = r0 + u;
       if (U > 1 && r >= rows) break;
       const size_t e = (size_t)r * F + c;
-      float o[8];
+      float o[8], f1[8], f2[8];
       uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = gelu_erf(g1[u][j]) * g2[u][j];
-        o[j] = p > 0.f ? (((keep >> j) & 1) ? v * ks : 0.f) : v;
-      }
+      for (int j = 0; j < 8; ++j) geglu_fwd_fac(g1[u][j], g2[u][j], (keep >> j) & 1, ks, o[j], f1[j], f2[j]);
       Vec8<T>::store(a + e, o);
+      if (fac) {
+        Vec8<T>::store(fac + (size_t)r * 2 * F + c, f1);
+        Vec8<T>::store(fac + (size_t)r * 2 * F + F + c, f2);
+      }
     }
   }
 }
 
 template <typename T, int U>
 __global__ __launch_bounds__(128) void bwd_kernel(const T* __restrict__ da, const T* __restrict__ g,
-                                                  int rows, int F, float p, uint32_t th, float ks,
-                                                  uint64_t seed, uint64_t off, T* __restrict__ dg) {
+                                                  int rows, int F, T* __restrict__ dg) {
+  // g = the forward's factors fac: dg = [da * fac1 | da * fac2]
   const int f8 = F / 8;
   for (int r0 = blockIdx.y * U; r0 < rows; r0 += gridDim.y * U)
   for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < f8; v += gridDim.x * blockDim.x) {
@@ -94,17 +100,11 @@ __global__ __launch_bounds__(128) void bwd_kernel(const T* __restrict__ da, cons
     for (int u = 0; u < U; ++u) {
       const int r = r0 + u;
       if (U > 1 && r >= rows) break;
-      const size_t e = (size_t)r * F + c;
-      uint32_t keep = p > 0.f ? keep8(seed, off, e, th) : 0xFFu;
       float o1[8], o2[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float dd = d[u][j];
-        if (p > 0.f) dd = ((keep >> j) & 1) ? dd * ks : 0.f;
-        float ge, dge;
-        gelu_erf_and_grad(g1[u][j], ge, dge);
-        o1[j] = dd * g2[u][j] * dge;
-        o2[j] = dd * ge;
+        o1[j] = d[u][j] * g1[u][j];
+        o2[j] = d[u][j] * g2[u][j];
       }
       Vec8<T>::store(dg + (size_t)r * 2 * F + c, o1);
       Vec8<T>::store(dg + (size_t)r * 2 * F + F + c, o2);
@@ -133,7 +133,7 @@ inline dim3 grid_for(int rows, int F, int u = 1) {
 using namespace dna;
 
 extern "C" int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, float p_drop,
-                             uint64_t seed, uint64_t offset, void* a, void* stream) {
+                             uint64_t seed, uint64_t offset, void* a, void* fac, void* stream) {
   DNA_CHECK_ARG(g && a, "dna_geglu_fwd: null pointer");
   DNA_CHECK_ARG(inter % 8 == 0 && rows >= 0, "dna_geglu_fwd: intermediate %% 8 != 0");
   DNA_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "dna_geglu_fwd: bad p");
@@ -145,44 +145,43 @@ extern "C" int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, floa
   const dim3 grid = geglu::grid_for(rows, inter, u);
   if (dtype == DNA_BF16 && u == 4)
     hipLaunchKernelGGL((geglu::fwd_kernel<bf16, 4>), grid, dim3(128), 0, s, (const bf16*)g,
-                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a);
+                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a, (bf16*)fac);
   else if (dtype == DNA_BF16 && u == 2)
     hipLaunchKernelGGL((geglu::fwd_kernel<bf16, 2>), grid, dim3(128), 0, s, (const bf16*)g,
-                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a);
+                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a, (bf16*)fac);
   else if (dtype == DNA_BF16)
     hipLaunchKernelGGL((geglu::fwd_kernel<bf16, 1>), grid, dim3(128), 0, s, (const bf16*)g,
-                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a);
+                       rows, inter, p_drop, th, ks, seed, offset, (bf16*)a, (bf16*)fac);
   else if (dtype == DNA_F32)
     hipLaunchKernelGGL((geglu::fwd_kernel<float, 1>), grid, dim3(128), 0, s, (const float*)g,
-                       rows, inter, p_drop, th, ks, seed, offset, (float*)a);
+                       rows, inter, p_drop, th, ks, seed, offset, (float*)a, (float*)fac);
   else
     DNA_CHECK_ARG(false, "dna_geglu_fwd: bad dtype");
   DNA_LAUNCH_CHECK("dna_geglu_fwd");
   return DNA_OK;
 }
 
-extern "C" int dna_geglu_bwd(const void* da, const void* g, int dtype, int rows, int inter,
-                             float p_drop, uint64_t seed, uint64_t offset, void* dg, void* stream) {
-  DNA_CHECK_ARG(da && g && dg, "dna_geglu_bwd: null pointer");
+extern "C" int dna_geglu_bwd(const void* da, const void* fac, int dtype, int rows, int inter,
+                             void* dg, void* stream) {
+  DNA_CHECK_ARG(da && fac && dg, "dna_geglu_bwd: null pointer");
   DNA_CHECK_ARG(inter % 8 == 0 && rows >= 0, "dna_geglu_bwd: intermediate %% 8 != 0");
   if (rows == 0) return DNA_OK;
   hipStream_t s = as_stream(stream);
-  const uint32_t th = dropout_threshold16(p_drop);
-  const float ks = 1.f / (1.f - p_drop);
+  const void* g = fac;
   const int u = dtype == DNA_BF16 ? geglu::unroll_rows(rows) : 1;
   const dim3 grid = geglu::grid_for(rows, inter, u);
   if (dtype == DNA_BF16 && u == 4)
     hipLaunchKernelGGL((geglu::bwd_kernel<bf16, 4>), grid, dim3(128), 0, s, (const bf16*)da,
-                       (const bf16*)g, rows, inter, p_drop, th, ks, seed, offset, (bf16*)dg);
+                       (const bf16*)g, rows, inter, (bf16*)dg);
   else if (dtype == DNA_BF16 && u == 2)
     hipLaunchKernelGGL((geglu::bwd_kernel<bf16, 2>), grid, dim3(128), 0, s, (const bf16*)da,
-                       (const bf16*)g, rows, inter, p_drop, th, ks, seed, offset, (bf16*)dg);
+                       (const bf16*)g, rows, inter, (bf16*)dg);
   else if (dtype == DNA_BF16)
     hipLaunchKernelGGL((geglu::bwd_kernel<bf16, 1>), grid, dim3(128), 0, s, (const bf16*)da,
-                       (const bf16*)g, rows, inter, p_drop, th, ks, seed, offset, (bf16*)dg);
+                       (const bf16*)g, rows, inter, (bf16*)dg);
   else if (dtype == DNA_F32)
     hipLaunchKernelGGL((geglu::bwd_kernel<float, 1>), grid, dim3(128), 0, s, (const float*)da,
-                       (const float*)g, rows, inter, p_drop, th, ks, seed, offset, (float*)dg);
+                       (const float*)g, rows, inter, (float*)dg);
   else
     DNA_CHECK_ARG(false, "dna_geglu_bwd: bad dtype");
   DNA_LAUNCH_CHECK("dna_geglu_bwd");

@@ -440,23 +440,27 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
           const bf16x4 h1 = bf16x4{(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
           const bf16x4 h2 = bf16x4{(bf16)v2[0], (bf16)v2[1], (bf16)v2[2], (bf16)v2[3]};
           const uint32_t og = (uint32_t)((r * 2 * a.F + c) * 2);
-          store_b64h(rg, og, h1);
-          store_b64h(rg, og + a.F * 2, h2);
           const size_t e = (size_t)(m0 + r) * a.F + c;
           // c % 4 == 0: this lane's 4 columns are one half of a keep8 group
           const uint32_t keep = a.p > 0.f ? (dropout_keep8(a.seed, a.off, e >> 3, a.th) >> (e & 4)) & 0xFu : 0xFu;
-          f32x4 o;
+          f32x4 o, f1, f2;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float x = gelu_erf((float)h1[q]) * (float)h2[q];
-            o[q] = a.p > 0.f ? (((keep >> q) & 1) ? x * a.ks : 0.f) : x;
+            float x, y1, y2;
+            geglu_fwd_fac((float)h1[q], (float)h2[q], (keep >> q) & 1, a.ks, x, y1, y2);
+            o[q] = x;
+            f1[q] = y1;
+            f2[q] = y2;
           }
+          store_b64(rg, og, f1);  // the backward factors where g would go
+          store_b64(rg, og + a.F * 2, f2);
           store_b64(ra, (uint32_t)((r * a.F + c) * 2), o);
         }
       }
   } else {  // EPI_GEGLU_BWD
     // da tile -> LDS (bf16, [256][256], 16-B chunks XOR-swizzled by row&15), then row-contiguous
-    // 8-element chunks per thread: 16-B loads of g, 16-B stores of dg, one keep8 Philox draw.
+    // 8-element chunks per thread: 16-B loads of the forward's factors fac, 16-B stores of
+    // dg = bf16(da) * fac.
     __syncthreads();
     char* T = smem;
 #pragma unroll
@@ -496,19 +500,12 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(Args a) {
         const int r = idx >> 5, c = idx & 31;
         const int m = m0 + r, n = n0 + c * 8;
         const bf16x8 d = *reinterpret_cast<const bf16x8*>(T + r * 512 + ((c ^ (r & 15)) << 4));
-        const size_t e = (size_t)m * a.F + n;
-        uint32_t keep = 0xFFu;
-        if (a.p > 0.f) keep = dropout_keep8(a.seed, a.off, e >> 3, a.th);
+        (void)m;
         bf16x8 o1, o2;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          float dd = (float)d[q];
-          if (a.p > 0.f) dd = ((keep >> q) & 1) ? dd * a.ks : 0.f;
-          const float x = (float)g1[u][q];
-          float ge, dge;
-          gelu_erf_and_grad(x, ge, dge);
-          o1[q] = (bf16)(dd * (float)g2[u][q] * dge);
-          o2[q] = (bf16)(dd * ge);
+          o1[q] = (bf16)((float)d[q] * (float)g1[u][q]);
+          o2[q] = (bf16)((float)d[q] * (float)g2[u][q]);
         }
         store_b128h(rdg, offs[u], o1);
         store_b128h(rdg, offs[u] + a.F * 2, o2);
@@ -586,7 +583,7 @@ static_assert(pend_stores<EPI_BF16>(1, 0) == 16 && pend_stores<EPI_BF16>(1, 3) =
 template <int EPI, int ABL = 0, int SCH = 0>
 __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU ||
-                    (EPI == EPI_GEGLU_BWD && SCH == 2 && (ABL == 0 || ABL == 64 || ABL == 128)) ||
+                    (EPI == EPI_GEGLU_BWD && SCH == 2 && (ABL == 0 || ABL == 128)) ||
                     (EPI == EPI_GELU_BWD && SCH == 2 && ABL == 0),
                 "persistent kernel: bf16 / GeGLU epilogues (GeGLU backward: lean body only)");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
@@ -756,9 +753,10 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   };
 
   // GeGLU: the rows of half mq are final once both column quadrants (mq, 0) = g1 and (mq, 1) = g2
-  // are (phase 1 for mq = 0, phase 3 for mq = 1 of a unit's last K-step): bias, bf16 g1 / g2
-  // stores, then a = dropout(gelu(g1) * g2) from the rounded values -- all three widened to
-  // 16-B stores by the same permlane16 exchange; one Philox keep8 draw per 8 columns.
+  // are (phase 1 for mq = 0, phase 3 for mq = 1 of a unit's last K-step): bias, bf16 rounding of
+  // g1 / g2, then a = dropout(gelu(g1) * g2) and the backward factors fac1 / fac2 (common.h
+  // geglu_fwd_fac; stored where g would go) from the rounded values -- all three widened to 16-B
+  // stores by the same permlane16 exchange; one Philox keep8 draw per 8 columns.
   const auto rAux = out_rsrc(a.aux, (uint32_t)((size_t)a.M * a.F * 2));
   const int colq = wc * 32 + (((lane >> 4) & 1) << 4) + (((lane >> 4) & 2) << 2);  // after the swap
   const uint32_t voG = (uint32_t)(((wr * 64 + (lane & 15)) * 2 * a.F + colq) * 2);
@@ -783,17 +781,20 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       // row-block offsets added per lane (soffset 0): keeps this epilogue's scalar footprint small
       const uint32_t og = voG + (uint32_t)((row * 2 * a.F + c.n0) * 2);
       const uint32_t oa = voAx + (uint32_t)((row * a.F + c.n0) * 2);
-      __builtin_amdgcn_raw_buffer_store_b128(g1, rC, og, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(g2, rC, og + a.F * 2, 0, 0);
       const bf16x8 h1 = __builtin_bit_cast(bf16x8, g1), h2 = __builtin_bit_cast(bf16x8, g2);
       const size_t e = (size_t)(row + wr * 64 + (lane & 15)) * a.F + c.n0 + colq;  // e % 8 == 0
       const uint32_t keep = a.p > 0.f ? dropout_keep8(a.seed, a.off, e >> 3, a.th) : 0xFFu;
-      bf16x8 o;
+      bf16x8 o, f1, f2;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const float x = gelu_erf((float)h1[q]) * (float)h2[q];
-        o[q] = (bf16)(a.p > 0.f ? (((keep >> q) & 1) ? x * a.ks : 0.f) : x);
+        float x, y1, y2;
+        geglu_fwd_fac((float)h1[q], (float)h2[q], (keep >> q) & 1, a.ks, x, y1, y2);
+        o[q] = (bf16)x;
+        f1[q] = (bf16)y1;
+        f2[q] = (bf16)y2;
       }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f1), rC, og, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f2), rC, og + a.F * 2, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rAux, oa, 0, 0);
 #pragma unroll
       for (int nq = 0; nq < 2; ++nq)
@@ -1157,27 +1158,13 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rC, off, 0, 0);
           continue;
         }
-        // element index within the launch's row block (< 2^31: the launcher's row blocks keep
-        // M * 2F * 2 bytes below 2^31); e % 8 == 0
-        const uint32_t e = (uint32_t)(row + wr * 64 + l16) * (uint32_t)a.F + (uint32_t)(c.n0 + nq * 128 + colq);
-        const uint32_t keep = a.p > 0.f ? dropout_keep8(a.seed, a.off, (uint64_t)(e >> 3), a.th) : 0xFFu;
+        // dg = bf16(da) * fac (the forward's factors: GELU derivative, g2, keep bit and 1/(1-p)
+        // folded in, common.h geglu_fwd_fac)
         bf16x8 o1, o2;
-        if constexpr ((ABL & 64) != 0) {  // diagnostics (timing only): no GeGLU math
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            o1[q] = (bf16)((float)d[q] * (float)gv[i][1][q]);
-            o2[q] = (bf16)((float)d[q] * (float)gv[i][0][q]);
-          }
-        } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          float dd = (float)d[q];
-          if (a.p > 0.f) dd = ((keep >> q) & 1) ? dd * a.ks : 0.f;
-          float ge, dge;
-          gelu_erf_and_grad((float)gv[i][0][q], ge, dge);
-          o1[q] = (bf16)(dd * (float)gv[i][1][q] * dge);
-          o2[q] = (bf16)(dd * ge);
-        }
+          o1[q] = (bf16)((float)d[q] * (float)gv[i][0][q]);
+          o2[q] = (bf16)((float)d[q] * (float)gv[i][1][q]);
         }
         const uint32_t off = voGB + (uint32_t)__builtin_amdgcn_readfirstlane(
                                         (row * 2 * a.F + c.n0 + nq * 128) * 2);
@@ -1988,9 +1975,10 @@ extern "C" int dna_linear_wgrad(const void* dy, const void* x, int M, int N, int
 }
 
 extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* bias, int M, int F,
-                                    int K, float p_drop, uint64_t seed, uint64_t offset, void* g,
+                                    int K, float p_drop, uint64_t seed, uint64_t offset, void* fac,
                                     void* out, void* stream) {
-  DNA_CHECK_ARG(x && w && g && out, "dna_geglu_linear_fwd: null pointer");
+  DNA_CHECK_ARG(x && w && fac && out, "dna_geglu_linear_fwd: null pointer");
+  void* g = fac;  // the backward factors take g's place (same layout, [M][2F])
   DNA_CHECK_ARG(M >= 0 && K % BK == 0 && F % (BN / 2) == 0,
                 "dna_geglu_linear_fwd: K %% 64 and F %% 128 required (K=%d F=%d)", K, F);
   DNA_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "dna_geglu_linear_fwd: bad p");
@@ -2024,10 +2012,10 @@ extern "C" int dna_geglu_linear_fwd(const void* x, const void* w, const float* b
   return launch<true, true, EPI_GEGLU>(a, 1, as_stream(stream), "dna_geglu_linear_fwd");
 }
 
-extern "C" int dna_geglu_linear_dgrad(const void* dy, const void* w, const void* g, int M, int F,
-                                      int N, float p_drop, uint64_t seed, uint64_t offset,
-                                      void* dg, void* stream) {
-  DNA_CHECK_ARG(dy && w && g && dg, "dna_geglu_linear_dgrad: null pointer");
+extern "C" int dna_geglu_linear_dgrad(const void* dy, const void* w, const void* fac, int M, int F,
+                                      int N, void* dg, void* stream) {
+  DNA_CHECK_ARG(dy && w && fac && dg, "dna_geglu_linear_dgrad: null pointer");
+  const void* g = fac;
   DNA_CHECK_ARG(M >= 0 && N % BK == 0 && F % 8 == 0,
                 "dna_geglu_linear_dgrad: hidden %% 64 and F %% 8 required (N=%d F=%d)", N, F);
   if (M == 0) return DNA_OK;
@@ -2036,22 +2024,20 @@ extern "C" int dna_geglu_linear_dgrad(const void* dy, const void* w, const void*
   a.B = (const bf16*)w; a.ldb = F;
   a.C = nullptr; a.ldc = F; a.g = (const bf16*)g; a.aux = (bf16*)dg;
   a.M = M; a.N = F; a.K = N; a.ksplit = N; a.F = F;
-  a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
-  a.seed = seed; a.off = offset;
   return launch<true, false, EPI_GEGLU_BWD>(a, 1, as_stream(stream), "dna_geglu_linear_dgrad");
 }
 
-// dg[M, 2F] = geglu_bwd(dy[M, N] . Wt[F, N]^T, g) on the persistent kernel: the data gradient of
+// dg[M, 2F] = bf16(dy[M, N] . Wt[F, N]^T) * fac on the persistent kernel: the data gradient of
 // `wo` through its transposed bf16 copy (both operands K-major, as dna_linear_fwd's dgrad use),
-// with the GeGLU backward of bert_layers.py:292-296 in the epilogue; da never reaches memory.
-// Row blocks past 2^31-byte operands as dna_geglu_linear_fwd (dropout offset advanced per block).
-extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const void* g, int M, int F,
-                                        int N, float p_drop, uint64_t seed, uint64_t offset,
-                                        void* dg, void* stream) {
-  DNA_CHECK_ARG(dy && wt && g && dg, "dna_geglu_linear_dgrad_p: null pointer");
+// with the GeGLU backward of bert_layers.py:292-296 in the epilogue (fac = the forward's
+// factors, dropout folded in); da never reaches memory. Row blocks past 2^31-byte operands as
+// dna_geglu_linear_fwd.
+extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const void* fac, int M,
+                                        int F, int N, void* dg, void* stream) {
+  DNA_CHECK_ARG(dy && wt && fac && dg, "dna_geglu_linear_dgrad_p: null pointer");
   DNA_CHECK_ARG(M >= 0 && N % BK == 0 && (N / BK) % 2 == 0 && N >= 2 * BK && F % BN == 0,
                 "dna_geglu_linear_dgrad_p: hidden %% 128 and F %% 256 required (N=%d F=%d)", N, F);
-  DNA_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "dna_geglu_linear_dgrad_p: bad p");
+  const void* g = fac;
   DNA_CHECK_ARG((size_t)F * N * 2 < (1ull << 31), "dna_geglu_linear_dgrad_p: weight too large");
   if (M == 0) return DNA_OK;
   Args a = base_args();
@@ -2059,12 +2045,10 @@ extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const vo
   a.B = (const bf16*)wt; a.ldb = N;
   a.C = nullptr; a.ldc = 2 * F; a.g = (const bf16*)g; a.aux = (bf16*)dg;
   a.N = F; a.K = N; a.ksplit = N; a.F = F;
-  // DNA_GEMM_ABL (timing-only diagnostics, results invalid): 64 = epilogue without the GeGLU
-  // math (g loads + dg stores), 128 = without the g loads (math on zeros)
+  // DNA_GEMM_ABL=128 (timing-only diagnostic, results invalid): the epilogue without the
+  // factor loads
   const char* ab = getenv("DNA_GEMM_ABL");
   const int abl = ab ? atoi(ab) : 0;
-  a.p = p_drop; a.th = dropout_threshold16(p_drop); a.ks = 1.f / (1.f - p_drop);
-  a.seed = seed;
   a.tilesN = F / BN;
   a.GM = 8;
   if (const char* e = getenv("DNA_GEMM_GM")) a.GM = atoi(e);
@@ -2078,13 +2062,11 @@ extern "C" int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const vo
     c.g = a.g + (size_t)r0 * 2 * F;
     c.aux = a.aux + (size_t)r0 * 2 * F;
     c.M = M - r0 < mc ? M - r0 : mc;
-    c.off = offset + (uint64_t)r0 * F / 8;  // dropout groups of 8 elements, row-major
     c.tilesM = (c.M + BM - 1) / BM;
     const int U = c.tilesM * c.tilesN;
     int G = num_cus();
     G = U < G ? U : (G & ~7);
-    if (abl == 64) hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 64, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
-    else if (abl == 128) hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 128, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
+    if (abl == 128) hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 128, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
     else hipLaunchKernelGGL((gemmp_kernel<EPI_GEGLU_BWD, 0, 2>), dim3(G), dim3(NTHR), 0, as_stream(stream), c);
     DNA_LAUNCH_CHECK("dna_geglu_linear_dgrad_p");
   }

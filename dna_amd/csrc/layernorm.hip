@@ -183,6 +183,8 @@ struct BwdArgs {
   float* part;  // [gridDim.x][3][cols]: dgamma, dbeta, dbias
   int rms;      // RMSNorm backward: mean taken as 0, no mean-gradient term
   const float* dsum;  // dna_add_ln_bwd: gradient of the pre-norm sum output, added to the LN's
+  const float* yin;   // dna_ln_bwd_from_y: the forward's fp32 output y; x_hat = (y - beta) / gamma
+  const float* beta;  //   replaces the recomputation from x (+ bias, dropout) + residual
 };
 
 template <int NV, bool VEC>
@@ -219,6 +221,12 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
   load_row<float, NV, VEC>(a.gamma, lane, gam);
   if (a.bias) load_row<float, NV, VEC>(a.bias, lane, bias);
   const float inv_cols = 1.f / a.cols;
+  float ginv[NV], bet[NV];
+  if (a.yin) {
+    load_row<float, NV, VEC>(a.beta, lane, bet);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) ginv[k] = gam[k] != 0.f ? 1.f / gam[k] : 0.f;
+  }
   struct In {
     RawRow<TX, NV, VEC> x;
     RawRow<float, NV, VEC> r, dy, ds;
@@ -238,14 +246,22 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
   // rows of up to 512 columns; at 768 (DNABERT-2) the second row set takes the kernel past 256
   // VGPRs and the plain loop below is faster (0.58 vs 0.61 ms, profiles/r05/ab_ln_bwd_prefetch.txt)
   constexpr bool PF = NV <= 8;
-  if constexpr (!PF) {
+  if (!PF || a.yin) {  // (the from-y backward always takes the plain loop)
     for (int row = gw; row < a.rows; row += nw) {
       const size_t ro = (size_t)row * a.cols;
       float u[NV], v[NV];
+      bool keep[NV];
+      float mu;
+      if (a.yin) {  // x_hat from the output: (y - beta) / gamma (act none; mean not needed)
+        load_row<float, NV, VEC>(a.yin + ro, lane, v);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) { v[k] = (v[k] - bet[k]) * ginv[k]; u[k] = 0.f; }
+        if (a.p > 0.f) keep_bits<NV, VEC>(keep, row, a.cols, lane, a.seed, a.off, a.th);
+        mu = 0.f;
+      } else {
       load_row<TX, NV, VEC>(reinterpret_cast<const TX*>(a.x) + ro, lane, u);
 #pragma unroll
       for (int k = 0; k < NV; ++k) { u[k] += bias[k]; v[k] = a.act == DNA_ACT_GELU ? gelu_erf(u[k]) : u[k]; }
-      bool keep[NV];
       if (a.p > 0.f) {
         keep_bits<NV, VEC>(keep, row, a.cols, lane, a.seed, a.off, a.th);
 #pragma unroll
@@ -257,7 +273,9 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) v[k] += r[k];
       }
-      const float mu = a.rms ? 0.f : a.mean[row], rs = a.rstd[row];
+      mu = a.rms ? 0.f : a.mean[row];
+      }
+      const float rs = a.rstd[row];
       float g[NV];
 #pragma unroll
       for (int k = 0; k < NV; ++k) g[k] = 0.f;
@@ -271,7 +289,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(BwdArgs a) {
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        const float xh = (v[k] - mu) * rs;
+        const float xh = a.yin ? v[k] : (v[k] - mu) * rs;
         v[k] = xh;
         acc_g[k] += g[k] * xh;
         acc_b[k] += g[k];
@@ -616,6 +634,44 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
   hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
                      (const float*)workspace, nb, cols, dgamma, dbeta, dbias);
   DNA_LAUNCH_CHECK("dna_ln_bwd");
+  return DNA_OK;
+}
+
+// The same backward with x_hat recomputed from the forward's fp32 output, x_hat = (y - beta) /
+// gamma (act none only): it reads y instead of x and the residual -- one fp32 row instead of a
+// bf16 and an fp32 row (3.2 instead of 3.6 GB per DNABERT-2 call at T = 262,144) -- and neither
+// x nor the residual has to be kept for the backward. gamma must have no zero entries (those
+// columns' x_hat cannot be recovered; they are taken as 0).
+extern "C" int dna_ln_bwd_from_y(const float* dy, const void* dy_bf16, const float* y, int x_dtype,
+                                 float p_drop, uint64_t seed, uint64_t offset, const float* gamma,
+                                 const float* beta, const float* rstd, int rows, int cols,
+                                 float* dresidual, void* dx, float* dgamma, float* dbeta,
+                                 float* dbias, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+  DNA_CHECK_ARG(y && gamma && beta && rstd && dx, "dna_ln_bwd_from_y: null pointer");
+  DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_ln_bwd_from_y: bad dtype");
+  if (rows == 0) return DNA_OK;
+  DNA_CHECK_ARG(workspace && workspace_bytes >= dna_ln_bwd_workspace(rows, cols),
+                "dna_ln_bwd_from_y: workspace too small (%zu < %zu)", workspace_bytes,
+                dna_ln_bwd_workspace(rows, cols));
+  const int nb = bwd_blocks(rows, cols);
+  BwdArgs a{dy, (const bf16*)dy_bf16, nullptr, nullptr, DNA_ACT_NONE, p_drop,
+            dropout_threshold(p_drop), 1.f / (1.f - p_drop), seed, offset, nullptr, gamma, nullptr,
+            rstd, rows, cols, dresidual, dx, (float*)workspace, 0, nullptr, y, beta};
+  hipStream_t s = as_stream(stream);
+  const size_t lds = (size_t)WAVES * 3 * cols * sizeof(float);
+  int st = dispatch_cols(cols, [&](auto nv, auto vec) {
+    constexpr int NV = decltype(nv)::value;
+    constexpr bool VEC = decltype(vec)::value;
+    if (x_dtype == DNA_BF16)
+      hipLaunchKernelGGL((bwd_kernel<bf16, NV, VEC>), dim3(nb), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((bwd_kernel<float, NV, VEC>), dim3(nb), dim3(256), lds, s, a);
+  });
+  if (st) return st;
+  hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
+                     (const float*)workspace, nb, cols, dgamma, dbeta, dbias);
+  DNA_LAUNCH_CHECK("dna_ln_bwd_from_y");
   return DNA_OK;
 }
 

@@ -328,12 +328,21 @@ class FusedLayerNorm(torch.autograd.Function):
             N.call("dna_ln_fwd", x.data_ptr(), _dt(x), _p(bias), act, p, seed, off, _p(residual),
                    gamma.data_ptr(), beta.data_ptr(), n, d, eps, _p(y), _p(yb), mean.data_ptr(),
                    rstd.data_ptr(), N.stream_ptr())
-        ctx.save_for_backward(x, bias, residual, gamma, mean, rstd)
+        # backward from the fp32 output (x_hat = (y - beta) / gamma, dna_ln_bwd_from_y): one fp32
+        # row read instead of x + the residual, and neither is kept alive for the backward
+        ctx.from_y = y is not None and act == N.ACT_NONE and _LN_BWD_FROM_Y
+        if ctx.from_y:
+            ctx.save_for_backward(y, bias, gamma, beta, rstd)
+            ctx.shape = (n, d, x.dtype, residual is not None)
+        else:
+            ctx.save_for_backward(x, bias, residual, gamma, mean, rstd)
         ctx.cfg = (act, p, seed, off)
         return y, yb
 
     @staticmethod
     def backward(ctx, dy, dyb):
+        if ctx.from_y:
+            return FusedLayerNorm._backward_from_y(ctx, dy, dyb)
         x, bias, residual, gamma, mean, rstd = ctx.saved_tensors
         act, p, seed, off = ctx.cfg
         n, d = x.shape
@@ -356,6 +365,36 @@ class FusedLayerNorm(torch.autograd.Function):
                    _p(dres), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _p(dbias), ws.data_ptr(),
                    nws, N.stream_ptr())
         return dx, dbias, dres, dg, db, None, None, None, None, None, None, None
+
+    @staticmethod
+    def _backward_from_y(ctx, dy, dyb):
+        y, bias, gamma, beta, rstd = ctx.saved_tensors
+        act, p, seed, off = ctx.cfg
+        n, d, xdt, has_res = ctx.shape
+        dx = torch.empty(n, d, device=y.device, dtype=xdt)
+        dres = torch.empty(n, d, device=y.device, dtype=torch.float32) if has_res else None
+        dg = torch.empty_like(gamma)
+        db = torch.empty_like(gamma)
+        dbias = torch.empty_like(bias) if bias is not None else None
+        nws = N.lib().dna_ln_bwd_workspace(n, d)
+        ws = torch.empty(max(nws, 16), device=y.device, dtype=torch.uint8)
+        dy = None if dy is None else dy.contiguous()
+        dyb = None if dyb is None else dyb.contiguous()
+        es = dx.element_size()
+        # reads dy / dy_bf16 and y; writes dx and (with a residual) d(residual) fp32
+        nbytes = n * (d * ((4 if dy is not None else 0) + (2 if dyb is not None else 0) + 4 + es
+                           + (4 if has_res else 0)) + 4)
+        with _timed("ln_bwd", nbytes, "byte"):
+            N.call("dna_ln_bwd_from_y", _p(dy), _p(dyb), y.data_ptr(), _dt(dx), p, seed, off,
+                   gamma.data_ptr(), beta.data_ptr(), rstd.data_ptr(), n, d, _p(dres),
+                   dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _p(dbias), ws.data_ptr(), nws,
+                   N.stream_ptr())
+        return dx, dbias, dres, dg, db, None, None, None, None, None, None, None
+
+
+# DNA_LN_BWD_FROM_Y=0: the LayerNorm backward recomputes x_hat from x (+ bias, dropout) + the
+# residual instead of from the fp32 output (A/B switch)
+_LN_BWD_FROM_Y = os.environ.get("DNA_LN_BWD_FROM_Y", "1") != "0"
 
 
 class AddLayerNorm(torch.autograd.Function):
@@ -507,18 +546,23 @@ def alibi_attention(qkv, key_valid, slopes, b, S, H, scale=None, bias_grad=False
 
 # ----------------------------------------------------------------------------------- GeGLU
 def _geglu_forward(g, p, seed, off):
+    """(a, fac): the GeGLU output and the backward factors fac = [d a / d g1 | d a / d g2]
+    (dropout folded in; csrc/common.h geglu_fwd_fac), so the backward is dg = da * fac. From
+    the gated_layers epilogue, which wrote fac in g's place (Linear, geglu=...), or the separate
+    pass (dna_geglu_fwd; fac in a new buffer, g is left as it is)."""
     pre = getattr(g, "_dna_geglu", None)
     if pre is not None and pre[1] == (p, seed, off):
         a = pre[0]  # computed in the producing GEMM's epilogue (Linear, geglu=...)
         del g._dna_geglu
-        return a
+        return a, g
     g = g.contiguous()
     n, F2 = g.shape
     a = torch.empty(n, F2 // 2, device=g.device, dtype=g.dtype)
-    with _timed("geglu_fwd", n * F2 // 2 * 3 * g.element_size(), "byte"):
+    fac = torch.empty_like(g)
+    with _timed("geglu_fwd", n * F2 // 2 * 5 * g.element_size(), "byte"):
         N.call("dna_geglu_fwd", g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off, a.data_ptr(),
-               N.stream_ptr())
-    return a
+               fac.data_ptr(), N.stream_ptr())
+    return a, fac
 
 
 class GeGLU(torch.autograd.Function):
@@ -527,20 +571,18 @@ class GeGLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, g, p, seed, off):
         _gpu(g)
-        a = _geglu_forward(g, p, seed, off)
-        ctx.save_for_backward(g)
-        ctx.cfg = (p, seed, off)
+        a, fac = _geglu_forward(g, p, seed, off)
+        ctx.save_for_backward(fac)
         return a
 
     @staticmethod
     def backward(ctx, da):
-        (g,) = ctx.saved_tensors
-        p, seed, off = ctx.cfg
-        n, F2 = g.shape
-        dg = torch.empty_like(g)
+        (fac,) = ctx.saved_tensors
+        n, F2 = fac.shape
+        dg = torch.empty_like(fac)
         da = da.contiguous()
-        with _timed("geglu_bwd", n * F2 // 2 * 5 * g.element_size(), "byte"):
-            N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), _dt(g), n, F2 // 2, p, seed, off,
+        with _timed("geglu_bwd", n * F2 // 2 * 5 * fac.element_size(), "byte"):
+            N.call("dna_geglu_bwd", da.data_ptr(), fac.data_ptr(), _dt(fac), n, F2 // 2,
                    dg.data_ptr(), N.stream_ptr())
         return dg, None, None, None
 
@@ -634,15 +676,16 @@ def _geglu_fused_ok(x, w_lp):
 
 
 def _hip_geglu_linear(x, w_nk, p, seed, off):
-    """g[M, 2F] = x . w^T and a[M, F] = dropout(gelu(g1) g2) (dna_geglu_linear_fwd)."""
+    """fac[M, 2F] (the GeGLU backward factors of g = x . w^T, in g's place) and
+    a[M, F] = dropout(gelu(g1) g2) in one launch (dna_geglu_linear_fwd)."""
     x = x.contiguous()
     M, K = x.shape
     F2 = w_nk.shape[0]
-    g = torch.empty(M, F2, device=x.device, dtype=torch.bfloat16)
+    fac = torch.empty(M, F2, device=x.device, dtype=torch.bfloat16)
     a = torch.empty(M, F2 // 2, device=x.device, dtype=torch.bfloat16)
     N.call("dna_geglu_linear_fwd", x.data_ptr(), w_nk.data_ptr(), None, M, F2 // 2, K, float(p),
-           seed, off, g.data_ptr(), a.data_ptr(), N.stream_ptr())
-    return g, a
+           seed, off, fac.data_ptr(), a.data_ptr(), N.stream_ptr())
+    return fac, a
 
 
 def _hip_linear(x, w_nk, bias):
@@ -742,8 +785,10 @@ class Linear(torch.autograd.Function):
         flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
         if geglu is not None and b is None and _geglu_fused_ok(x, w_lp):
             # g = x . w^T and a = dropout(gelu(g1) g2) in one launch (the GeGLU epilogue of the
-            # persistent GEMM); `a` rides on g for the GeGLU node that follows (bit-identical to
-            # the separate dna_geglu_fwd pass, which then does not run)
+            # persistent GEMM). The tensor returned in g's place holds the GeGLU backward factors
+            # (g itself is never stored); `a` rides on it for the GeGLU node that follows, which
+            # must be its only consumer (bit-identical to the separate dna_geglu_fwd pass, which
+            # then does not run)
             with _timed("gemm_geglu", flops):
                 g, a = _hip_geglu_linear(x, w_lp, *geglu)
             g._dna_geglu = (a, tuple(geglu))
@@ -970,28 +1015,27 @@ class GeGLUOut(torch.autograd.Function):
     def forward(ctx, g, p, seed, off, w, w_lp, w_lpt):
         _gpu(g)
         g = g.contiguous()
-        a = _geglu_forward(g, p, seed, off)  # the same `a` (fused epilogue or dna_geglu_fwd)
+        # the same `a` (fused epilogue or dna_geglu_fwd) and the backward factors
+        a, fac = _geglu_forward(g, p, seed, off)
         n, F2 = g.shape
         flops = 2.0 * n * w_lp.shape[0] * w_lp.shape[1]
         with _timed("gemm_hip", flops):
             o = _hip_linear(a, w_lp, None)
-        ctx.save_for_backward(g, a, w_lpt)
+        ctx.save_for_backward(fac, a, w_lpt)
         ctx.weight = w
-        ctx.cfg = (p, seed, off)
         return o
 
     @staticmethod
     def backward(ctx, dy):
-        g, a, w_lpt = ctx.saved_tensors
-        p, seed, off = ctx.cfg
+        fac, a, w_lpt = ctx.saved_tensors
         dy = dy.contiguous()
-        n, F2 = g.shape
+        n, F2 = fac.shape
         Nh = dy.shape[1]
         flops = 2.0 * n * Nh * (F2 // 2)
-        dg = torch.empty_like(g)
+        dg = torch.empty_like(fac)
         with _timed("gemm_geglu_bwd", flops):
-            N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), w_lpt.data_ptr(), g.data_ptr(), n,
-                   F2 // 2, Nh, float(p), seed, off, dg.data_ptr(), N.stream_ptr())
+            N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), w_lpt.data_ptr(), fac.data_ptr(), n,
+                   F2 // 2, Nh, dg.data_ptr(), N.stream_ptr())
         dw = _weight_grad(ctx.weight, dy, a, flops)
         return dg, None, None, None, dw, None, None
 

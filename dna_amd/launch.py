@@ -85,6 +85,10 @@ def init_rank_process_group(local_rank):
         os.environ["MASTER_PORT"] = str(free_port())
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", "1")
+    hang = os.environ.get("DNA_HANG_DUMP")
+    if hang:  # diagnostics: every thread's Python stack on stderr if the rank is still alive then
+        import faulthandler
+        faulthandler.dump_traceback_later(int(hang), repeat=True)
     dev = rank_device_index(local_rank)
     torch.cuda.set_device(dev)
     if dist_backend() == "nccl":

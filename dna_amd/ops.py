@@ -9,8 +9,9 @@ asserts (flash_attn_triton.py:849-855) -- instead of letting a kernel read out o
     torch.ops.dna_amd.attn_fwd(qkv, key_valid, slopes, b, S, H, scale, out, lse)
     torch.ops.dna_amd.attn_bwd(qkv, out, dout, lse, key_valid, slopes, b, S, H, scale, dqkv)
     torch.ops.dna_amd.linear_fwd(x, w, bias, y)                   y = x w^T (+ bias), bf16 MFMA
-    torch.ops.dna_amd.geglu_fwd(g, p, seed, offset, a)            a = dropout(gelu(g1) g2)
-    torch.ops.dna_amd.geglu_bwd(da, g, p, seed, offset, dg)
+    torch.ops.dna_amd.geglu_fwd(g, p, seed, offset, a, fac)       a = dropout(gelu(g1) g2),
+                                                                  fac = backward factors
+    torch.ops.dna_amd.geglu_bwd(da, fac, dg)                      dg = da * fac
     torch.ops.dna_amd.xent_fwd(logits, target, loss, lse)         per-row CE
     torch.ops.dna_amd.transpose_bf16(src, dst)
 and the reference's FlashAttention kernel slot with its own signature (flash_attn_triton.py:
@@ -274,66 +275,72 @@ def transpose_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
     N.call("dna_transpose_bf16", src.data_ptr(), r, c, dst.data_ptr(), N.stream_ptr())
 
 
-@torch.library.custom_op("dna_amd::geglu_linear_fwd", mutates_args=("g", "a"))
+@torch.library.custom_op("dna_amd::geglu_linear_fwd", mutates_args=("fac", "a"))
 def geglu_linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, p: float,
-                     seed: int, offset: int, g: torch.Tensor, a: torch.Tensor) -> None:
-    """g = x . w^T (+ bias) and a = dropout(gelu(g[:, :F]) * g[:, F:]) in one launch
-    (gated_layers + GeGLU, bert_layers.py:292-296); same Philox mask as geglu_fwd."""
+                     seed: int, offset: int, fac: torch.Tensor, a: torch.Tensor) -> None:
+    """g = x . w^T (+ bias), a = dropout(gelu(g[:, :F]) * g[:, F:]) and fac = the backward
+    factors of geglu_fwd in one launch (gated_layers + GeGLU, bert_layers.py:292-296; g itself is
+    not stored); same bits as linear_fwd + geglu_fwd."""
     _cuda_contig("x", x, (torch.bfloat16,))
     _cuda_contig("w", w, (torch.bfloat16,))
-    _cuda_contig("g", g, (torch.bfloat16,))
+    _cuda_contig("fac", fac, (torch.bfloat16,))
     _cuda_contig("a", a, (torch.bfloat16,))
     M, K = x.shape
     F2 = w.shape[0]
-    _check(w.shape[1] == K and tuple(g.shape) == (M, F2) and tuple(a.shape) == (M, F2 // 2),
-           "shapes: x[M,K], w[2F,K], g[M,2F], a[M,F]")
+    _check(w.shape[1] == K and tuple(fac.shape) == (M, F2) and tuple(a.shape) == (M, F2 // 2),
+           "shapes: x[M,K], w[2F,K], fac[M,2F], a[M,F]")
     _check(K % 64 == 0 and F2 % 256 == 0, f"K % 64 and 2F % 256 required (K={K}, 2F={F2})")
     if bias is not None:
         _cuda_contig("bias", bias, (torch.float32,))
         _check(bias.numel() == F2, "bias must hold 2F floats")
     N.call("dna_geglu_linear_fwd", x.data_ptr(), w.data_ptr(), _p(bias), M, F2 // 2, K, float(p),
-           seed, offset, g.data_ptr(), a.data_ptr(), N.stream_ptr())
+           seed, offset, fac.data_ptr(), a.data_ptr(), N.stream_ptr())
 
 
 @torch.library.custom_op("dna_amd::geglu_linear_dgrad", mutates_args=("dg",))
-def geglu_linear_dgrad(dy: torch.Tensor, wt: torch.Tensor, g: torch.Tensor, p: float, seed: int,
-                       offset: int, dg: torch.Tensor) -> None:
-    """dg = geglu_bwd(dy . wt^T, g) in one launch: wo's data gradient (wt = wo^T, [F, hidden])
+def geglu_linear_dgrad(dy: torch.Tensor, wt: torch.Tensor, fac: torch.Tensor,
+                       dg: torch.Tensor) -> None:
+    """dg = geglu_bwd(dy . wt^T, fac) in one launch: wo's data gradient (wt = wo^T, [F, hidden])
     with the GeGLU backward in the epilogue (bert_layers.py:292-297); == linear_fwd + geglu_bwd."""
     _cuda_contig("dy", dy, (torch.bfloat16,))
     _cuda_contig("wt", wt, (torch.bfloat16,))
-    _cuda_contig("g", g, (torch.bfloat16,))
+    _cuda_contig("fac", fac, (torch.bfloat16,))
     _cuda_contig("dg", dg, (torch.bfloat16,))
     M, H = dy.shape
     F = wt.shape[0]
-    _check(wt.shape[1] == H and tuple(g.shape) == (M, 2 * F) and dg.shape == g.shape,
-           "shapes: dy[M,H], wt[F,H], g / dg[M,2F]")
+    _check(wt.shape[1] == H and tuple(fac.shape) == (M, 2 * F) and dg.shape == fac.shape,
+           "shapes: dy[M,H], wt[F,H], fac / dg[M,2F]")
     _check(H % 128 == 0 and H >= 256 and F % 256 == 0,
            f"hidden % 128, hidden >= 256 and F % 256 required (H={H}, F={F})")
-    N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), M, F, H,
-           float(p), seed, offset, dg.data_ptr(), N.stream_ptr())
+    N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), fac.data_ptr(), M, F, H,
+           dg.data_ptr(), N.stream_ptr())
 
 
 # ------------------------------------------------------------------------------- elementwise
-@torch.library.custom_op("dna_amd::geglu_fwd", mutates_args=("a",))
-def geglu_fwd(g: torch.Tensor, p: float, seed: int, offset: int, a: torch.Tensor) -> None:
+@torch.library.custom_op("dna_amd::geglu_fwd", mutates_args=("a", "fac"))
+def geglu_fwd(g: torch.Tensor, p: float, seed: int, offset: int, a: torch.Tensor,
+              fac: torch.Tensor) -> None:
+    """a = dropout(gelu(g[:, :F]) * g[:, F:]); fac [rows, 2F] = the backward factors
+    [d a / d g1 | d a / d g2] with the dropout folded in, for geglu_bwd (may be g itself)."""
     _cuda_contig("g", g, (torch.bfloat16, torch.float32))
     _cuda_contig("a", a, (g.dtype,))
     n, f2 = g.shape
     _check(tuple(a.shape) == (n, f2 // 2), "a must be [rows, F] for g [rows, 2F]")
+    _cuda_contig("fac", fac, (g.dtype,))
+    _check(fac.shape == g.shape, "fac must be shaped like g")
     N.call("dna_geglu_fwd", g.data_ptr(), _DT[g.dtype], n, f2 // 2, p, seed, offset, a.data_ptr(),
-           N.stream_ptr())
+           fac.data_ptr(), N.stream_ptr())
 
 
 @torch.library.custom_op("dna_amd::geglu_bwd", mutates_args=("dg",))
-def geglu_bwd(da: torch.Tensor, g: torch.Tensor, p: float, seed: int, offset: int,
-              dg: torch.Tensor) -> None:
-    _cuda_contig("g", g, (torch.bfloat16, torch.float32))
-    _cuda_contig("da", da, (g.dtype,))
-    _cuda_contig("dg", dg, (g.dtype,))
-    n, f2 = g.shape
-    _check(tuple(da.shape) == (n, f2 // 2) and dg.shape == g.shape, "da [rows, F], dg like g")
-    N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), _DT[g.dtype], n, f2 // 2, p, seed, offset,
+def geglu_bwd(da: torch.Tensor, fac: torch.Tensor, dg: torch.Tensor) -> None:
+    """dg = [da * fac1 | da * fac2] (fac from geglu_fwd / geglu_linear_fwd)."""
+    _cuda_contig("fac", fac, (torch.bfloat16, torch.float32))
+    _cuda_contig("da", da, (fac.dtype,))
+    _cuda_contig("dg", dg, (fac.dtype,))
+    n, f2 = fac.shape
+    _check(tuple(da.shape) == (n, f2 // 2) and dg.shape == fac.shape, "da [rows, F], dg like fac")
+    N.call("dna_geglu_bwd", da.data_ptr(), fac.data_ptr(), _DT[fac.dtype], n, f2 // 2,
            dg.data_ptr(), N.stream_ptr())
 
 

@@ -121,6 +121,14 @@ int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, int x_dtype,
                const float* residual, const float* gamma, const float* mean, const float* rstd,
                int rows, int cols, float* dresidual, void* dx, float* dgamma, float* dbeta,
                float* dbias, void* workspace, size_t workspace_bytes, void* stream);
+/* Backward of dna_ln_fwd (act none) with x_hat recomputed from the forward's fp32 output y:
+ * x_hat = (y - beta) / gamma (gamma without zero entries; mean not needed) -- reads y instead of
+ * x and the residual. Same outputs and workspace as dna_ln_bwd. */
+int dna_ln_bwd_from_y(const float* dy, const void* dy_bf16, const float* y, int x_dtype,
+                      float p_drop, uint64_t seed, uint64_t offset, const float* gamma,
+                      const float* beta, const float* rstd, int rows, int cols, float* dresidual,
+                      void* dx, float* dgamma, float* dbeta, float* dbias, void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 /* Pre-norm residual add + LayerNorm: sum = x + residual (fp32, written), y = LN(sum).
  * Replaces the flash_attn Block's `residual = dropout(x) + residual; norm(residual)` with
@@ -217,11 +225,14 @@ int dna_sum_slices(const float* parts, int s, size_t n, float* out, void* stream
 
 /* ------------------------------------------------------------------ GeGLU (+ dropout)
  * a = dropout( gelu_erf(g[:, :inter]) * g[:, inter:] )   (bert_layers.py:292-296)
- *   g [rows, 2*inter] dtype -> a [rows, inter] dtype. */
+ *   g [rows, 2*inter] dtype -> a [rows, inter] dtype, and (fac non-NULL) the backward factors
+ *   fac [rows, 2*inter] = [k*s*g2*gelu'(g1) | k*s*gelu(g1)] (k the element's keep bit, s =
+ *   1/(1-p)); fac may alias g. Backward: dg = [da * fac1 | da * fac2] (the keep bits need no
+ *   second draw). */
 int dna_geglu_fwd(const void* g, int dtype, int rows, int inter, float p_drop, uint64_t seed,
-                  uint64_t offset, void* a, void* stream);
-int dna_geglu_bwd(const void* da, const void* g, int dtype, int rows, int inter, float p_drop,
-                  uint64_t seed, uint64_t offset, void* dg, void* stream);
+                  uint64_t offset, void* a, void* fac, void* stream);
+int dna_geglu_bwd(const void* da, const void* fac, int dtype, int rows, int inter, void* dg,
+                  void* stream);
 
 /* ------------------------------------------------------------------ projections (MFMA GEMM)
  * The encoder's nn.Linear layers (bert_layers.py:158 Wqkv, :214 attention dense, :292
@@ -307,22 +318,23 @@ int dna_linear_wgrad_p_splits(int M, int N, int K);
 int dna_linear_wgrad_p(const void* dy, const void* x, int M, int N, int K, int splits,
                        float* partials, void* stream);
 /* gated_layers + GeGLU + dropout in one launch (bert_layers.py:292-296):
- *   g[M, 2F] = x[M,K] . wg^T + bias (bias fp32 [2F] or NULL),
- *   out[M, F] = dropout(gelu_erf(g[:, :F]) * g[:, F:])   -- same Philox mask as dna_geglu_fwd.
+ *   g = x[M,K] . wg^T + bias (bias fp32 [2F] or NULL; rounded to bf16, never stored),
+ *   out[M, F] = dropout(gelu_erf(g[:, :F]) * g[:, F:]) and fac[M, 2F] = the backward factors of
+ *   dna_geglu_fwd -- the same bits as dna_linear_fwd + dna_geglu_fwd (same Philox mask).
  * K % 64 == 0, F % 128 == 0. */
 int dna_geglu_linear_fwd(const void* x, const void* wg, const float* bias, int M, int F, int K,
-                         float p_drop, uint64_t seed, uint64_t offset, void* g, void* out,
+                         float p_drop, uint64_t seed, uint64_t offset, void* fac, void* out,
                          void* stream);
 /* wo dgrad + GeGLU backward in one launch: da = dy[M,N] . wo ([N, F]), then
- * dg[M, 2F] = dna_geglu_bwd(da, g). N % 64 == 0, F % 8 == 0. */
-int dna_geglu_linear_dgrad(const void* dy, const void* wo, const void* g, int M, int F, int N,
-                           float p_drop, uint64_t seed, uint64_t offset, void* dg, void* stream);
+ * dg[M, 2F] = dna_geglu_bwd(bf16(da), fac). N % 64 == 0, F % 8 == 0. */
+int dna_geglu_linear_dgrad(const void* dy, const void* wo, const void* fac, int M, int F, int N,
+                           void* dg, void* stream);
 /* The same on the persistent kernel (the training step's path), with wo's transposed bf16 copy
- * wt [F, N] (dna_transpose_bf16) as the K-major operand: dg[M, 2F] = dna_geglu_bwd(dy . wt^T, g);
- * da never reaches memory. N % 128 == 0, F % 256 == 0. Replaces the backward of wo's nn.Linear
- * and of the GeGLU (bert_layers.py:292-297). */
-int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const void* g, int M, int F, int N,
-                             float p_drop, uint64_t seed, uint64_t offset, void* dg, void* stream);
+ * wt [F, N] (dna_transpose_bf16) as the K-major operand: dg[M, 2F] =
+ * dna_geglu_bwd(bf16(dy . wt^T), fac); da never reaches memory. N % 128 == 0, F % 256 == 0.
+ * Replaces the backward of wo's nn.Linear and of the GeGLU (bert_layers.py:292-297). */
+int dna_geglu_linear_dgrad_p(const void* dy, const void* wt, const void* fac, int M, int F, int N,
+                             void* dg, void* stream);
 
 /* dh = gelu_tanh'(h) * bf16(dy . W) -- the data gradient of a Linear fed by a tanh-GELU (the
  * flash_attn Mlp's fc2 in the HyenaDNA Blocks, reference long_conv_lm.py create_mlp_cls with

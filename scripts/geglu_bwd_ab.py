@@ -24,15 +24,15 @@ def main():
     pdrop = float(os.environ.get("P", "0.1"))
 
     def fused():
-        N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), T, F, H, pdrop,
-               7, 0, dg.data_ptr(), s)
+        N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), T, F, H,
+               dg.data_ptr(), s)
 
     def gemm():  # the same GEMM with the plain bf16 epilogue (da stored, no GeGLU)
         N.call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, T, F, H, da.data_ptr(), s)
 
     def pair():
         N.call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, T, F, H, da.data_ptr(), s)
-        N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, T, F, pdrop, 7, 0, dg.data_ptr(), s)
+        N.call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, T, F, dg.data_ptr(), s)
 
     variants = [v for v in os.environ.get("VARS", "0").split(",") if v]
     iters = int(os.environ.get("ITERS", "20"))

@@ -1,8 +1,9 @@
 #!/usr/bin/env python
 """Where the GeGLU epilogue GEMMs' time goes, at the bench shape (T = 262,144 tokens, F = 3072,
-hidden 768): the fused forward (gated_layers + GeGLU, dna_geglu_linear_fwd) and the fused
-backward (wo data gradient + GeGLU backward, dna_geglu_linear_dgrad_p) at dropout p = 0.1 and
-p = 0 (p = 0 skips the keep-bit draws), against the same GEMMs with the plain bf16 epilogue.
+hidden 768): the fused forward (gated_layers + GeGLU, dna_geglu_linear_fwd) at dropout p = 0.1
+and p = 0 (p = 0 skips the keep-bit draws) and the fused backward (wo data gradient + GeGLU
+backward, dna_geglu_linear_dgrad_p: dg = bf16(da) * fac, no draws since round 6), against the
+same GEMMs with the plain bf16 epilogue.
 Interleaved rounds, one JSON line per (kernel, round); DNA_AMD_LIB picks the library build.
 
     python scripts/geglu_epi_ab.py [ROUNDS]"""
@@ -36,10 +37,8 @@ def main():
                                  T, F, H, 0.0, 7, 3, g.data_ptr(), a.data_ptr(), s),
         "fwd_plain": lambda: N.call("dna_linear_fwd", x.data_ptr(), wg.data_ptr(), bg.data_ptr(),
                                     T, 2 * F, H, g.data_ptr(), s),
-        "bwd_p0.1": lambda: N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(),
-                                   g.data_ptr(), T, F, H, 0.1, 7, 0, dg.data_ptr(), s),
-        "bwd_p0": lambda: N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(),
-                                 g.data_ptr(), T, F, H, 0.0, 7, 0, dg.data_ptr(), s),
+        "bwd_fac": lambda: N.call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(),
+                                  g.data_ptr(), T, F, H, dg.data_ptr(), s),
         "bwd_plain": lambda: N.call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, T, F, H,
                                     a.data_ptr(), s),
     }

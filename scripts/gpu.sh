@@ -89,6 +89,21 @@ ab-lib)
     done
   done | tee gpurun_out/ab.log
   ;;
+ab-tree)
+  # interleaved bench A/B of whole source trees (scripts/build_tree_variant.sh REV NAME ->
+  # _ab/NAME): TREES = "main base ..." ("main" = this tree)
+  TREES=${1:?trees}
+  REPS=${2:-2}
+  STEPS=${3:-20}
+  for rep in $(seq $REPS); do
+    for t in $TREES; do
+      if [ "$t" = main ]; then b=$ROOT/bench.py; else b=$ROOT/_ab/$t/bench.py; fi
+      timeout -k 10 300 python $b --steps $STEPS --warmup 5 --no-cpu-baseline \
+        --no-b64 --no-data-pipeline > gpurun_out/ab.json 2> gpurun_out/ab.err
+      echo "$t $(python -c "import json;d=json.load(open('gpurun_out/ab.json'));print(d['value'], d['ms_per_step'], {k: round(v['avg_ms'],3) for k,v in d['kernels'].items()})")"
+    done
+  done | tee gpurun_out/ab.log
+  ;;
 fftpmc)
   # config-D FFT long conv: rocprofv3 --stats + separate FETCH_SIZE / WRITE_SIZE passes of
   # scripts/fftconv_bench.py, per-kernel traffic table (scripts/fft_traffic.py) -> $OUT/traffic.md

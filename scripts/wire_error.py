@@ -21,6 +21,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import torch
 import torch.distributed as dist
@@ -42,13 +43,20 @@ def _metrics(flat, approx, exact):
             "worst_param_norm_rel": worst, "worst_param": worst_name}
 
 
+def _note(rank, t0, what):
+    if rank == 0:  # progress on stderr (a silent multi-minute run looks hung)
+        print(f"[wire_error {time.perf_counter() - t0:7.1f}s] {what}", file=sys.stderr, flush=True)
+
+
 def run(args):
+    t0 = time.perf_counter()
     import bench
     from dna_amd.bert_layers import BertForMaskedLM
     from dna_amd.launch import init_rank_process_group
     from dna_amd.trainer import MLMTrainer
     device = init_rank_process_group(int(os.environ.get("LOCAL_RANK", "0")))
     rank, world = dist.get_rank(), dist.get_world_size()
+    _note(rank, t0, f"process group up ({dist.get_backend()}, {world} ranks)")
     torch.manual_seed(2222)
     model = BertForMaskedLM(bench.MODEL_CFG, precision="bf16")
     tr = MLMTrainer(model, device, lr=5e-4, weight_decay=1e-5, max_grad_norm=1.0)
@@ -67,18 +75,25 @@ def run(args):
         torch.cuda.synchronize()
         return tr.flat.grad.detach().clone()
 
+    _note(rank, t0, "model and batch ready")
     grads(True, "fp32")                      # first backward: the reducer learns its counts
     local = grads(False, "fp32")             # this rank's own gradient
     g32 = grads(True, "fp32")
+    _note(rank, t0, "fp32 wire done")
     g16 = grads(True, "bf16")
-    exact = local.double()
+    _note(rank, t0, "bf16 wire done")
+    # the checks' own exchanges on host tensors (gloo moves CUDA tensors through the host anyway)
+    local_h = local.cpu()
+    exact = local_h.double()
     dist.all_reduce(exact, op=dist.ReduceOp.SUM)
-    parts = [torch.empty_like(local) for _ in range(world)]
-    dist.all_gather(parts, local.to(torch.bfloat16).float())  # bf16 values, fp32 carrier
+    parts = [torch.empty_like(local_h) for _ in range(world)]
+    dist.all_gather(parts, local_h.to(torch.bfloat16).float())  # bf16 values, fp32 carrier
     ring = parts[0].to(torch.bfloat16)
     for p in parts[1:]:
         ring = (ring.float() + p).to(torch.bfloat16)  # every hop rounds to bf16
     del parts
+    g32, g16 = g32.cpu(), g16.cpu()
+    _note(rank, t0, "exact sum and ring emulation done")
     if rank == 0:
         names = {id(p): n for n, p in model.named_parameters()}
         flat = [(names.get(id(p), "?"), (o, n)) for p, (o, n, _) in zip(tr.flat.params, tr.flat.slices)]

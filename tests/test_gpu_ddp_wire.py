@@ -26,10 +26,13 @@ def wire():
     env = dict(os.environ, DNA_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "wire_error.py"),
-                        "--ranks", "4", "--batch", "8"], cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=500)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    log = os.path.join(ROOT, "gpurun_out", "wire_error.log")  # progress, visible while it runs
+    with open(log, "w") as err:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "wire_error.py"),
+                            "--ranks", "4", "--batch", "8"], cwd=ROOT, env=env,
+                           stdout=subprocess.PIPE, stderr=err, text=True, timeout=500)
+    assert r.returncode == 0, (r.stdout[-2000:], open(log).read()[-4000:])
     (line,) = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     print(json.dumps(line))
     return line

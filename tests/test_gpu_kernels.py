@@ -196,6 +196,53 @@ def test_fused_layernorm(dtype, cols, act, use_bias, use_res):
         assert (a.grad.float() - r.grad).abs().max().item() < tol * sc
 
 
+@pytest.mark.parametrize("cols", [128, 768])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_ln_bwd_from_y_equals_recompute_from_x(cols, p):
+    """dna_ln_bwd_from_y (x_hat = (y - beta) / gamma from the forward's fp32 output) against
+    dna_ln_bwd (x_hat recomputed from x + bias, the dropout mask and the residual) on the same
+    forward, dropout on and off: every output within fp32 recompute noise."""
+    from dna_amd import _native as N
+    g = torch.Generator(device=DEV).manual_seed(cols + int(10 * p))
+    n = 1000
+    x = torch.randn(n, cols, device=DEV, generator=g).bfloat16()
+    bias = torch.randn(cols, device=DEV, generator=g) * 0.1
+    res = torch.randn(n, cols, device=DEV, generator=g)
+    gm = 1 + 0.1 * torch.randn(cols, device=DEV, generator=g)
+    bt = 0.1 * torch.randn(cols, device=DEV, generator=g)
+    y = torch.empty(n, cols, device=DEV)
+    mean, rstd = torch.empty(n, device=DEV), torch.empty(n, device=DEV)
+    st = N.stream_ptr()
+    N.call("dna_ln_fwd", x.data_ptr(), N.BF16, bias.data_ptr(), 0, p, 5, 7, res.data_ptr(),
+           gm.data_ptr(), bt.data_ptr(), n, cols, 1e-12, y.data_ptr(), None, mean.data_ptr(),
+           rstd.data_ptr(), st)
+    dy = torch.randn(n, cols, device=DEV, generator=g)
+    dyb = torch.randn(n, cols, device=DEV, generator=g).bfloat16()
+    nws = N.lib().dna_ln_bwd_workspace(n, cols)
+    ws = torch.empty(nws, device=DEV, dtype=torch.uint8)
+    outs = []
+    for from_y in (False, True):
+        dx = torch.empty_like(x)
+        dres = torch.empty(n, cols, device=DEV)
+        dg, db, dbias = (torch.empty(cols, device=DEV) for _ in range(3))
+        if from_y:
+            N.call("dna_ln_bwd_from_y", dy.data_ptr(), dyb.data_ptr(), y.data_ptr(), N.BF16, p, 5, 7,
+                   gm.data_ptr(), bt.data_ptr(), rstd.data_ptr(), n, cols, dres.data_ptr(),
+                   dx.data_ptr(), dg.data_ptr(), db.data_ptr(), dbias.data_ptr(), ws.data_ptr(),
+                   nws, st)
+        else:
+            N.call("dna_ln_bwd", dy.data_ptr(), dyb.data_ptr(), x.data_ptr(), N.BF16, bias.data_ptr(),
+                   0, p, 5, 7, res.data_ptr(), gm.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n,
+                   cols, dres.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                   dbias.data_ptr(), ws.data_ptr(), nws, st)
+        outs.append((dx.float(), dres, dg, db, dbias))
+    for i, (a, b) in enumerate(zip(*outs)):
+        # dx is bf16: a recompute difference at fp32 noise level may flip its rounding (1 ulp)
+        tol = 2 ** -7 * b.abs().max().item() if i == 0 else 2e-5 * max(b.abs().max().item(), 1.0)
+        assert (a - b).abs().max().item() <= tol, i
+    assert torch.equal(outs[0][0] == 0, outs[1][0] == 0)  # the same dropout mask
+
+
 def _rms_ref(x, g, eps):
     return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * g
 
@@ -342,14 +389,16 @@ def test_geglu_row_unrolled_bf16(n):
     outs = {}
     for dt, code in ((torch.bfloat16, 1), (torch.float32, 0)):
         a = torch.empty(n, F, device=DEV, dtype=dt)
+        fac = torch.empty(n, 2 * F, device=DEV, dtype=dt)
         dg = torch.empty(n, 2 * F, device=DEV, dtype=dt)
         # converted inputs held in variables: a temporary passed as `.to(dt).data_ptr()` is freed
         # before the kernel runs, and the next conversion may reuse its block (seen in the full
         # suite: the fp32 reference read a dO overwritten by g's conversion)
         gi, di = g.to(dt), da.to(dt)
-        N.call("dna_geglu_fwd", gi.data_ptr(), code, n, F, 0.1, 7, 3, a.data_ptr(), N.stream_ptr())
-        N.call("dna_geglu_bwd", di.data_ptr(), gi.data_ptr(), code, n, F, 0.1, 7, 3,
-               dg.data_ptr(), N.stream_ptr())
+        N.call("dna_geglu_fwd", gi.data_ptr(), code, n, F, 0.1, 7, 3, a.data_ptr(), fac.data_ptr(),
+               N.stream_ptr())
+        N.call("dna_geglu_bwd", di.data_ptr(), fac.data_ptr(), code, n, F, dg.data_ptr(),
+               N.stream_ptr())
         outs[code] = (a.float(), dg.float())
     (a1, dg1), (a0, dg0) = outs[1], outs[0]
     assert torch.equal(a1 == 0, a0 == 0)
@@ -545,24 +594,43 @@ def test_gemm_geglu_fused_equals_unfused(p):
     x = torch.randn(M, H, generator=g0).to(DEV).bfloat16()
     wg = (torch.randn(2 * F, H, generator=g0) * 0.05).to(DEV).bfloat16()
     bg = (torch.randn(2 * F, generator=g0) * 0.1).to(DEV)
-    g = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    fac = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
     a = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
     _gemm_call("dna_geglu_linear_fwd", x.data_ptr(), wg.data_ptr(), bg.data_ptr(), M, F, H, p, 11, 5,
-               g.data_ptr(), a.data_ptr())
+               fac.data_ptr(), a.data_ptr())
+    g = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    _gemm_call("dna_linear_fwd", x.data_ptr(), wg.data_ptr(), bg.data_ptr(), M, 2 * F, H, g.data_ptr())
     assert _rel(g, x.float() @ wg.float().t() + bg) < 1e-2
-    a2 = torch.empty_like(a)
-    _gemm_call("dna_geglu_fwd", g.data_ptr(), 1, M, F, p, 11, 5, a2.data_ptr())
-    assert torch.equal(a, a2)
+    a2, fac2 = torch.empty_like(a), torch.empty_like(fac)
+    _gemm_call("dna_geglu_fwd", g.data_ptr(), 1, M, F, p, 11, 5, a2.data_ptr(), fac2.data_ptr())
+    assert torch.equal(a, a2) and torch.equal(fac, fac2)
+    _geglu_factors_match(g, a, fac, p)
     dy = torch.randn(M, H, generator=g0).to(DEV).bfloat16()
     wo = (torch.randn(H, F, generator=g0) * 0.05).to(DEV).bfloat16()
     dg = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
-    _gemm_call("dna_geglu_linear_dgrad", dy.data_ptr(), wo.data_ptr(), g.data_ptr(), M, F, H, p, 11, 5,
+    _gemm_call("dna_geglu_linear_dgrad", dy.data_ptr(), wo.data_ptr(), fac.data_ptr(), M, F, H,
                dg.data_ptr())
     da = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
     _gemm_call("dna_linear_dgrad", dy.data_ptr(), wo.data_ptr(), M, H, F, da.data_ptr())
     dg2 = torch.empty_like(dg)
-    _gemm_call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, M, F, p, 11, 5, dg2.data_ptr())
+    _gemm_call("dna_geglu_bwd", da.data_ptr(), fac.data_ptr(), 1, M, F, dg2.data_ptr())
     assert torch.equal(dg, dg2)
+
+
+def _geglu_factors_match(g, a, fac, p):
+    """fac = [k s g2 gelu'(g1) | k s gelu(g1)] (k = a's keep bit, s = 1 / (1 - p)) vs fp32 torch's
+    GELU and its autograd derivative on the same bf16 g, to bf16 rounding."""
+    F = a.shape[1]
+    h1, h2 = g[:, :F].float(), g[:, F:].float()
+    kept = (a != 0).float() / (1.0 - p) if p > 0 else torch.ones_like(h1)
+    x1 = h1.clone().requires_grad_(True)
+    torch.nn.functional.gelu(x1).sum().backward()
+    want1, want2 = h2 * x1.grad * kept, torch.nn.functional.gelu(h1) * kept
+    got1, got2 = fac[:, :F].float(), fac[:, F:].float()
+    assert (got1 - want1).abs().max().item() <= 8e-3 * want1.abs().max().item()
+    assert (got2 - want2).abs().max().item() <= 8e-3 * want2.abs().max().item()
+    wa = torch.nn.functional.gelu(h1) * h2 * kept
+    assert (a.float() - wa).abs().max().item() <= 8e-3 * wa.abs().max().item()
 
 
 @pytest.mark.parametrize("M", [1, 255, 257, 300, 1000])
@@ -593,9 +661,10 @@ def test_gemm_persistent_ragged_rows_write_nothing_past_m(M, kind):
         _gemm_call("dna_geglu_linear_fwd", x.data_ptr(), wg.data_ptr(), bg.data_ptr(), M, F, K, 0.0,
                    1, 0, gbuf.data_ptr(), abuf.data_ptr())
         torch.cuda.synchronize()
-        assert _rel(gbuf[:M], x.float() @ wg.float().t() + bg) < 1e-2
         assert torch.isnan(gbuf[M:]).all() and torch.isnan(abuf[M:]).all()
-        assert not torch.isnan(abuf[:M]).any()
+        assert not torch.isnan(abuf[:M]).any() and not torch.isnan(gbuf[:M]).any()
+        g = (x.float() @ wg.float().t() + bg).bfloat16()  # the factors of fp32 torch's g
+        _geglu_factors_match(g, abuf[:M], gbuf[:M], 0.0)
 
 
 # ------------------------------------------------------------------ bench-shape GEMM parity
@@ -637,70 +706,80 @@ def test_gemm_geglu_fused_bench_shape_row_blocks():
     g0 = torch.Generator(device=DEV).manual_seed(7)
     x = torch.randn(T, H, device=DEV, generator=g0).bfloat16()
     w = (torch.randn(2 * F, H, device=DEV, generator=g0) * 0.05).bfloat16()
-    g = torch.empty(T, 2 * F, device=DEV, dtype=torch.bfloat16)
+    fac = torch.empty(T, 2 * F, device=DEV, dtype=torch.bfloat16)
     a = torch.empty(T, F, device=DEV, dtype=torch.bfloat16)
     _gemm_call("dna_geglu_linear_fwd", x.data_ptr(), w.data_ptr(), None, T, F, H, 0.1, 123, 77,
-               g.data_ptr(), a.data_ptr())
-    g2 = torch.empty_like(g)
-    _gemm_call("dna_linear_fwd", x.data_ptr(), w.data_ptr(), None, T, 2 * F, H, g2.data_ptr())
-    assert torch.equal(g, g2)
-    del g2
+               fac.data_ptr(), a.data_ptr())
+    g = torch.empty_like(fac)
+    _gemm_call("dna_linear_fwd", x.data_ptr(), w.data_ptr(), None, T, 2 * F, H, g.data_ptr())
     a2 = torch.empty_like(a)
-    _gemm_call("dna_geglu_fwd", g.data_ptr(), 1, T, F, 0.1, 123, 77, a2.data_ptr())
+    _gemm_call("dna_geglu_fwd", g.data_ptr(), 1, T, F, 0.1, 123, 77, a2.data_ptr(), g.data_ptr())
     assert torch.equal(a, a2)
+    assert torch.equal(fac, g)  # the factors, written over g in place
 
 
-def _geglu_dgrad_pair(dy, wt, g, M, F, H, p, seed, off):
+def _geglu_dgrad_pair(dy, wt, fac, M, F, H):
     """The unfused pair the fused kernel replaces: da = dy . wt^T (dna_linear_fwd, the dgrad
-    through the transposed copy), then dg = dna_geglu_bwd(da, g)."""
+    through the transposed copy), then dg = dna_geglu_bwd(da, fac)."""
     da = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
     _gemm_call("dna_linear_fwd", dy.data_ptr(), wt.data_ptr(), None, M, F, H, da.data_ptr())
     dg = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
-    _gemm_call("dna_geglu_bwd", da.data_ptr(), g.data_ptr(), 1, M, F, p, seed, off, dg.data_ptr())
+    _gemm_call("dna_geglu_bwd", da.data_ptr(), fac.data_ptr(), 1, M, F, dg.data_ptr())
     return dg
 
 
+def _random_factors(M, F, gen):
+    """GeGLU backward factors as a dropout-on forward leaves them: random, ~10 % exact zeros."""
+    fac = torch.randn(M, 2 * F, generator=gen)
+    drop = torch.rand(M, F, generator=gen) < 0.1
+    fac[:, :F][drop] = 0.0
+    fac[:, F:][drop] = 0.0
+    return fac.to(DEV).bfloat16()
+
+
 @pytest.mark.parametrize("M", [1, 257, 1000, 4096])
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_gemm_geglu_dgrad_p_equals_pair_and_writes_nothing_past_m(M, p):
+def test_gemm_geglu_dgrad_p_equals_pair_and_writes_nothing_past_m(M):
     """wo's data gradient with the GeGLU backward in the persistent kernel's epilogue
-    (dna_geglu_linear_dgrad_p) equals the separate pair bit for bit, dropout on or off; the
-    output is the head of a NaN-filled buffer and g's rows past M are NaN: rows past M read as
+    (dna_geglu_linear_dgrad_p: dg = bf16(da) * fac) equals the separate pair bit for bit; the
+    output is the head of a NaN-filled buffer and fac's rows past M are NaN: rows past M read as
     zero and are never written."""
     F, H = 3072, 768
-    gen = torch.Generator(device="cpu").manual_seed(M + int(p * 10))
+    gen = torch.Generator(device="cpu").manual_seed(M)
     dy = torch.randn(M, H, generator=gen).to(DEV).bfloat16()
     wt = (torch.randn(F, H, generator=gen) * 0.05).to(DEV).bfloat16()
     gb = torch.full((M + 256, 2 * F), float("nan"), device=DEV, dtype=torch.bfloat16)
-    gb[:M] = torch.randn(M, 2 * F, generator=gen).to(DEV).bfloat16()
+    gb[:M] = _random_factors(M, F, gen)
     g = gb[:M]
     dgb = torch.full((M + 256, 2 * F), float("nan"), device=DEV, dtype=torch.bfloat16)
-    _gemm_call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), M, F, H, p,
-               91, 13, dgb.data_ptr())
+    _gemm_call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), M, F, H,
+               dgb.data_ptr())
     torch.cuda.synchronize()
-    ref = _geglu_dgrad_pair(dy, wt, g, M, F, H, p, 91, 13)
+    ref = _geglu_dgrad_pair(dy, wt, g, M, F, H)
     assert torch.equal(dgb[:M], ref)
     assert torch.isnan(dgb[M:]).all()
 
 
 def test_gemm_geglu_dgrad_p_bench_shape_row_blocks():
-    """The fused wo dgrad + GeGLU backward at T = 262,144 (g / dg are 3.2 GB: two row-block
-    launches, the dropout counter advanced per block) equals the separate pair bit for bit,
-    incl. the rows on both sides of the block seam, and matches fp32 torch on sampled rows."""
+    """The fused wo dgrad + GeGLU backward at T = 262,144 (fac / dg are 3.2 GB: two row-block
+    launches) equals the separate pair bit for bit, incl. the rows on both sides of the block
+    seam, and, with the factors of a dropout-off forward on random g, matches the fp32 GeGLU
+    backward (erf GELU and its derivative) on sampled rows."""
     T, F, H = BENCH_T, 3072, 768
     gen = torch.Generator(device=DEV).manual_seed(5)
     dy = torch.randn(T, H, device=DEV, generator=gen).bfloat16()
     wt = (torch.randn(F, H, device=DEV, generator=gen) * 0.05).bfloat16()
     g = torch.randn(T, 2 * F, device=DEV, generator=gen).bfloat16()
+    a = torch.empty(T, F, device=DEV, dtype=torch.bfloat16)
+    fac = torch.empty_like(g)
+    _gemm_call("dna_geglu_fwd", g.data_ptr(), 1, T, F, 0.0, 0, 0, a.data_ptr(), fac.data_ptr())
+    del a
     dg = torch.empty_like(g)
-    _gemm_call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), T, F, H,
-               0.1, 321, 9, dg.data_ptr())
-    ref = _geglu_dgrad_pair(dy, wt, g, T, F, H, 0.1, 321, 9)
+    _gemm_call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), fac.data_ptr(), T, F, H,
+               dg.data_ptr())
+    ref = _geglu_dgrad_pair(dy, wt, fac, T, F, H)
     assert torch.equal(dg, ref)
     del ref
-    # fp32 restatement on sampled rows, dropout off (bf16 da rounding as the reference's bf16 step)
-    _gemm_call("dna_geglu_linear_dgrad_p", dy.data_ptr(), wt.data_ptr(), g.data_ptr(), T, F, H,
-               0.0, 0, 0, dg.data_ptr())
+    # fp32 restatement on sampled rows (bf16 da rounding as the reference's bf16 step)
     mc = ((1 << 31) - 1) // (2 * F * 2) // 256 * 256
     rows = torch.cat([_sample_rows(T), torch.tensor([mc - 1, mc, mc + 1], device=DEV)])
     da = dy[rows].float() @ wt.float().t()

@@ -61,7 +61,7 @@ def test_linear_geglu_xent_ops_vs_torch():
     assert torch.equal(wt, w.t().contiguous())
     gg = torch.randn(256, 2 * 512, generator=g).cuda().bfloat16()
     a = torch.empty(256, 512, device="cuda", dtype=torch.bfloat16)
-    torch.ops.dna_amd.geglu_fwd(gg, 0.0, 1, 0, a)
+    torch.ops.dna_amd.geglu_fwd(gg, 0.0, 1, 0, a, torch.empty_like(gg))
     g1, g2 = gg.float().chunk(2, dim=1)
     aref = torch.nn.functional.gelu(g1) * g2
     assert float((a.float() - aref).abs().max()) < 2e-2 * float(aref.abs().max())
@@ -84,20 +84,30 @@ def test_fused_geglu_linear_ops_equal_separate_ops():
     M, H, F = 1000, 768, 3072
     x = torch.randn(M, H, generator=g0).cuda().bfloat16()
     wg = (torch.randn(2 * F, H, generator=g0) * 0.05).cuda().bfloat16()
-    g = torch.empty(M, 2 * F, device="cuda", dtype=torch.bfloat16)
+    fac = torch.empty(M, 2 * F, device="cuda", dtype=torch.bfloat16)
     a = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
-    torch.ops.dna_amd.geglu_linear_fwd(x, wg, None, 0.1, 5, 3, g, a)
-    g2 = torch.empty_like(g)
+    torch.ops.dna_amd.geglu_linear_fwd(x, wg, None, 0.1, 5, 3, fac, a)
+    g2 = torch.empty_like(fac)
     torch.ops.dna_amd.linear_fwd(x, wg, None, g2)
-    a2 = torch.empty_like(a)
-    torch.ops.dna_amd.geglu_fwd(g2, 0.1, 5, 3, a2)
-    assert torch.equal(g, g2) and torch.equal(a, a2)
+    a2, fac2 = torch.empty_like(a), torch.empty_like(fac)
+    torch.ops.dna_amd.geglu_fwd(g2, 0.1, 5, 3, a2, fac2)
+    assert torch.equal(fac, fac2) and torch.equal(a, a2)
+    # the factors: [keep * s * g2 * gelu'(g1) | keep * s * gelu(g1)], s = 1 / 0.9
+    h1, h2 = g2.float().chunk(2, dim=1)
+    kept = (a != 0).float() / 0.9
+    x1 = h1.clone().requires_grad_(True)
+    torch.nn.functional.gelu(x1).sum().backward()
+    ref1 = h2 * x1.grad * kept
+    ref2 = torch.nn.functional.gelu(h1) * kept
+    f1, f2 = fac.float().chunk(2, dim=1)
+    assert float((f1 - ref1).abs().max()) <= 1e-2 * float(ref1.abs().max())
+    assert float((f2 - ref2).abs().max()) <= 1e-2 * float(ref2.abs().max())
     dy = torch.randn(M, H, generator=g0).cuda().bfloat16()
     wo_t = (torch.randn(F, H, generator=g0) * 0.05).cuda().bfloat16()
-    dg = torch.empty_like(g)
-    torch.ops.dna_amd.geglu_linear_dgrad(dy, wo_t, g, 0.1, 5, 3, dg)
+    dg = torch.empty_like(fac)
+    torch.ops.dna_amd.geglu_linear_dgrad(dy, wo_t, fac, dg)
     da = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
     torch.ops.dna_amd.linear_fwd(dy, wo_t, None, da)
-    dg2 = torch.empty_like(g)
-    torch.ops.dna_amd.geglu_bwd(da, g, 0.1, 5, 3, dg2)
+    dg2 = torch.empty_like(fac)
+    torch.ops.dna_amd.geglu_bwd(da, fac, dg2)
     assert torch.equal(dg, dg2)

@@ -229,8 +229,12 @@ def test_bench_multi_rank_real_model(tmp_path, ranks):
            "--dump-params", dump]
     env = _two_rank_env("", dump)
     env.pop("DNA_DUMP_PARAMS")
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
-    assert r.returncode == 0, r.stderr[-3000:]
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    log = os.path.join(ROOT, "gpurun_out", f"bench_{ranks}rank.log")  # visible while it runs
+    with open(log, "w") as err:
+        r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=err, text=True,
+                           timeout=400)
+    assert r.returncode == 0, open(log).read()[-3000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     line = lines[0]
