@@ -231,6 +231,7 @@ def main():
     torch.cuda.set_device(device)
 
     from dna_amd.bert_layers import BertForMaskedLM
+    from dna_amd.ddp import all_reduce_
     from dna_amd.functional import OpTimer
     from dna_amd.trainer import MLMTrainer
 
@@ -265,7 +266,7 @@ def main():
         timer.__exit__()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
     if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        all_reduce_(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     final_loss = float(loss.item())
 
@@ -291,7 +292,7 @@ def main():
             dist.barrier()
         e64 = torch.tensor([time.perf_counter() - t2], dtype=torch.float64, device=device)
         if world > 1:
-            dist.all_reduce(e64, op=dist.ReduceOp.MAX)
+            all_reduce_(e64, op=dist.ReduceOp.MAX)
         e64 = float(e64.item())
         b64 = {"value": round(64 * n64 * world / e64, 2), "ms_per_step": round(e64 / n64 * 1e3, 3),
                "steps": n64, "warmup": 3, "per_gpu_batch": 64}

@@ -54,12 +54,13 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 #define DNA_PHILOX_ROUNDS 10
 #endif
 struct Philox {
+  template <int R = DNA_PHILOX_ROUNDS>
   __device__ __forceinline__ static uint4 gen(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1) {
     // each round's two 32x32 -> 64-bit products as one 64-bit multiply apiece (the pair
     // v_mul_hi_u32 + v_mul_lo_u32 per product otherwise; same bits either way)
 #pragma unroll
-    for (int r = 0; r < DNA_PHILOX_ROUNDS; ++r) {
+    for (int r = 0; r < R; ++r) {
       const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
       const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
       const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
@@ -85,12 +86,14 @@ __device__ __forceinline__ uint32_t dropout_keep4(uint64_t seed, uint64_t offset
 // Keep-mask for 8 consecutive elements starting at element index `idx8 * 8`: one Philox call,
 // element j uses the 16-bit half j of the 128-bit draw and is kept when it is >= p * 2^16
 // (keep probability quantised to 1/65536: p = 0.1 -> 0.099991). Half the Philox work of
-// two dropout_keep4 calls, which is what bounds the GeGLU kernels.
+// two dropout_keep4 calls. Philox4x32 with 7 rounds: Salmon et al. (SC'11) find 7 rounds of
+// Philox4x32 pass TestU01's BigCrush (10 is Random123's default safety margin); the draws sit in
+// the GeGLU GEMM epilogue's VALU budget (geglu_epi_ab.py: 10 -> 7 rounds -0.03 ms per launch).
 __device__ __forceinline__ uint32_t dropout_keep8(uint64_t seed, uint64_t offset, uint64_t idx8,
                                                   uint32_t thresh16) {
   uint64_t c = idx8 + offset;
-  uint4 r = Philox::gen((uint32_t)c, (uint32_t)(c >> 32), 0x5EED8u, 0u, (uint32_t)seed,
-                        (uint32_t)(seed >> 32));
+  uint4 r = Philox::gen<7>((uint32_t)c, (uint32_t)(c >> 32), 0x5EED8u, 0u, (uint32_t)seed,
+                           (uint32_t)(seed >> 32));
   const uint32_t w[4] = {r.x, r.y, r.z, r.w};
   uint32_t m = 0;
 #pragma unroll

@@ -20,6 +20,45 @@ import torch
 import torch.distributed as dist
 
 
+def _host_staged(t, group=None):
+    """gloo (the one-GPU multi-rank rehearsal) reduces CUDA tensors through its CUDA algorithms,
+    which deadlocked with more than two ranks sharing one GPU (round 6: every rank parked in the
+    first bucket's wait at 4 ranks, fine at 2): its collectives go through a host copy instead.
+    RCCL (the real multi-GPU path) reduces device buffers in place."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_reduce_(t, op=dist.ReduceOp.SUM, group=None):
+    """In-place all-reduce of `t` (blocking), host-staged under gloo."""
+    if _host_staged(t, group):
+        torch.cuda.current_stream(t.device).synchronize()
+        c = t.cpu()
+        dist.all_reduce(c, op=op, group=group)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+    return t
+
+
+def broadcast_(t, src=0, group=None):
+    """In-place broadcast of `t` from rank `src` (blocking), host-staged under gloo."""
+    if _host_staged(t, group):
+        torch.cuda.current_stream(t.device).synchronize()
+        c = t.cpu()
+        dist.broadcast(c, src=src, group=group)
+        t.copy_(c)
+    else:
+        dist.broadcast(t, src=src, group=group)
+    return t
+
+
+class _Done:
+    """A finished collective (the host-staged gloo path is synchronous)."""
+
+    def wait(self):
+        return True
+
+
 class GradBucketReducer:
     """wire_dtype "fp32" (default) all-reduces the fp32 gradient buckets in place; "bf16" halves
     the bytes on the wire (234 MB instead of 468 MB for DNABERT-2): each bucket is
@@ -91,13 +130,16 @@ class GradBucketReducer:
             if self._wire is None:
                 self._wire = torch.empty(self.flat.grad.numel(), dtype=torch.bfloat16,
                                          device=self.flat.grad.device)
-            w = self._wire[s:e]
-            w.copy_(self.flat.grad[s:e])
-            self._works.append((dist.all_reduce(w, op=dist.ReduceOp.SUM, group=self.group,
-                                                async_op=True), s, e))
+            buf = self._wire[s:e]
+            buf.copy_(self.flat.grad[s:e])
         else:
-            self._works.append((dist.all_reduce(self.flat.grad[s:e], op=dist.ReduceOp.SUM,
-                                                group=self.group, async_op=True), s, e))
+            buf = self.flat.grad[s:e]
+        if _host_staged(buf, self.group):  # rehearsal backend: synchronous, through the host
+            all_reduce_(buf, group=self.group)
+            self._works.append((_Done(), s, e))
+        else:
+            self._works.append((dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group,
+                                                async_op=True), s, e))
 
     def prepare(self, sync=True):
         """Call before each backward; sync=False for accumulation micro-batches (no collective,
@@ -153,7 +195,7 @@ def reduce_metrics(loss, num_tokens, group=None, extra=None):
     t = torch.stack([lv] + [torch.as_tensor(v).detach().to(device=lv.device, dtype=torch.float64)
                             .reshape(()) for v in vals])
     if grouped:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        all_reduce_(t, group=group)
         world = dist.get_world_size(group)
     else:
         world = 1

@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 
 from .bert_layers import BertForMaskedLM, MLMIndex
-from .ddp import GradBucketReducer
+from .ddp import GradBucketReducer, broadcast_
 from .flat import FlatParams
 from .optim import FusedAdamW, LinearLRSchedulerWarmup
 
@@ -63,7 +63,7 @@ class ModuleTrainer:
         self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
         self.world = self.reducer.world
         if self.reducer.enabled:  # DDP construction broadcast
-            dist.broadcast(self.flat.flat, src=0)
+            broadcast_(self.flat.flat, src=0)
         self.global_step = 0
 
     def step(self, batch) -> torch.Tensor:
@@ -97,7 +97,7 @@ class MLMTrainer:
         self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
         self.world = self.reducer.world
         if self.reducer.enabled:  # DDP construction broadcast (C2 in SURVEY §2.2)
-            dist.broadcast(self.flat.flat, src=0)
+            broadcast_(self.flat.flat, src=0)
             self.flat.refresh_shadow()
         # dropout stream: derived from train.seed when given, and distinct per rank
         rank = dist.get_rank() if dist.is_initialized() else 0

@@ -344,11 +344,16 @@ def test_dropout_mask_consistent_fwd_bwd():
     kept = a != 0
     rate = kept.float().mean().item()
     assert abs(rate - 0.9) < 0.005, rate
-    # neighbours share one 32-bit Philox word (16-bit halves): their bits must be independent
+    # neighbours share one 32-bit Philox word (16-bit halves): their bits must be independent,
+    # also across the 8-element groups of one draw (lag 8) and down a column (next row)
     k = kept.float()
-    for s in (1, 2, 4):
+    for s in (1, 2, 3, 4, 7, 8):
         both = (k[:, :-s] * k[:, s:]).mean().item()
         assert abs(both - rate * rate) < 0.005, (s, both, rate * rate)
+    both = (k[:-1] * k[1:]).mean().item()
+    assert abs(both - rate * rate) < 0.005, ("row", both, rate * rate)
+    for j in range(8):  # every slot of the 128-bit draw keeps at the same rate
+        assert abs(k[:, j::8].mean().item() - 0.9) < 0.01, j
     da = torch.randn(n, F, device=DEV)
     a.backward(da)
     g2 = g.detach().clone().requires_grad_(True)
