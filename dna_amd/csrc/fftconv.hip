@@ -502,8 +502,8 @@ constexpr int RB_NT = 256, RB_LOG_PTS = LOG_PTS - 1;
 __host__ __device__ __forceinline__ int log_rowbwd_group(const Geo& g) {
   return (RB_LOG_PTS - g.logM2) < g.logM1 ? (RB_LOG_PTS - g.logM2) : g.logM1;
 }
-template <int LN, bool DK, bool DU>
-__global__ __launch_bounds__(RB_NT, 3) void row_bwd_kernel(cf* __restrict__ zy, const cf* __restrict__ zu,
+template <int LN, bool DK, bool DU, int MINB = 3>
+__global__ __launch_bounds__(RB_NT, MINB) void row_bwd_kernel(cf* __restrict__ zy, const cf* __restrict__ zu,
                                                            const cf* __restrict__ kspec, int BP, Geo g_,
                                                            cf* __restrict__ pk) {
   const Geo g = fixed<LN>(g_);
@@ -986,9 +986,11 @@ void launch_row(cf* ws, const cf* kspec, Pairing pr, const Geo& g, int P, hipStr
 template <bool DK, bool DU>
 void launch_row_bwd(cf* zy, const cf* zu, const cf* kspec, int BP, int D, const Geo& g, cf* pk,
                     hipStream_t s) {
+  // DNA_FFT_RB_BLOCKS=4 (A/B): four blocks per CU (128 VGPRs, spills) instead of three
+  static const bool rb4 = getenv("DNA_FFT_RB_BLOCKS") && atoi(getenv("DNA_FFT_RB_BLOCKS")) == 4;
 #define L_(LN)                                                                                   \
   {                                                                                              \
-    auto k = row_bwd_kernel<LN, DK, DU>;                                                         \
+    auto k = (DK && DU && rb4) ? row_bwd_kernel<LN, DK, DU, 4> : row_bwd_kernel<LN, DK, DU>;     \
     const size_t lds = ((size_t)(1 << log_rowbwd_group(g)) * seq_stride(g.logM2, false) +        \
                         (1u << g.logM2)) * sizeof(cf);                                           \
     allow_lds(k, lds);                                                                           \

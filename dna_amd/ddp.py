@@ -29,10 +29,12 @@ def _host_staged(t, group=None):
 
 
 def all_reduce_(t, op=dist.ReduceOp.SUM, group=None):
-    """In-place all-reduce of `t` (blocking), host-staged under gloo."""
+    """In-place all-reduce of `t` (blocking), host-staged under gloo (a bf16 tensor is summed in
+    fp32 there and rounded once; RCCL's ring rounds every hop -- scripts/wire_error.py emulates
+    that order)."""
     if _host_staged(t, group):
         torch.cuda.current_stream(t.device).synchronize()
-        c = t.cpu()
+        c = t.float().cpu() if t.dtype == torch.bfloat16 else t.cpu()
         dist.all_reduce(c, op=op, group=group)
         t.copy_(c)
     else:

@@ -969,7 +969,8 @@ def wgrad_accumulate(dy, x, grad):
 def _weight_grad(w, dy, x, flops):
     """dW = dy^T x of the projection with fp32 master weight w: straight into the flat gradient
     buffer when a FlatParams owns w (None returned, bucket reducer notified), else returned."""
-    direct = getattr(w, "_dna_direct", False) and w.grad is not None and x.dtype != torch.float32
+    direct = (getattr(w, "_dna_direct", False) and w.grad is not None and x.dtype != torch.float32
+              and _hip_wgrad_ok(dy, x))
     side = _side_stream() if direct else None
     if side is not None:
         # wgrad beside the rest of the backward; dy / x must outlive it on the side stream

@@ -193,6 +193,7 @@ class ChannelLinear(torch.autograd.Function):
         ctx.save_for_backward(xin, w)
         ctx.cfg = (x.dtype, weight.dtype)
         ctx.sink = sink
+        ctx.weight = weight
         return y
 
     @staticmethod
@@ -225,7 +226,7 @@ class ChannelLinear(torch.autograd.Function):
                 _strided_gemm(dy, (dy.stride(1), 1, dy.stride(0)), xin,
                               (1, xin.stride(1), xin.stride(0)), part, (K, M * K), M, K, L, b, s,
                               out_f32=True)
-            dw = _sum_parts(part, (M, K), wdt)
+            dw = _finish_wgrad(part, ctx.weight, (M, K), wdt)
         return (None if dx is None else dx.to(xdt)), dw, None
 
 
@@ -240,6 +241,23 @@ def _wgrad_tokens(dy, sa, x, sb, M, Nn, T, batch, part=None, row0=0, rows_total=
     assert part.shape[0] == batch * s
     DF.strided_gemm(dy, sa, x, sb, part[:, row0:], (Nn, rt * Nn), M, Nn, T, batch, s, out_f32=True)
     return part, s
+
+
+def _finish_wgrad(part, weight, shape, dtype):
+    """A weight gradient from its fp32 split-K slices: summed straight into the flat fp32 .grad
+    when a FlatParams trainer owns the parameter (ModuleTrainer enables it; the bucket reducer is
+    notified and autograd gets None, so its AccumulateGrad add -- two per tied BiMamba
+    projection -- never runs), else returned."""
+    g = weight.grad if getattr(weight, "_dna_direct", False) else None
+    if g is not None and g.dtype == torch.float32 and g.is_contiguous() and \
+            tuple(g.shape) == tuple(shape):
+        N.call("dna_sum_slices_accum", part.data_ptr(), part.shape[0], g.numel(), g.data_ptr(),
+               N.stream_ptr())
+        notify = getattr(weight, "_dna_notify", None)
+        if notify is not None:
+            notify(weight)
+        return None
+    return _sum_parts(part, shape, dtype)
 
 
 def _sum_parts(part, shape, dtype):
@@ -308,6 +326,7 @@ class InProj(torch.autograd.Function):
         ctx.save_for_backward(h2, w)
         ctx.cfg = (b, L, h.dtype, weight.dtype, bool(reverse))
         ctx.sink = sink
+        ctx.weight = weight
         E = E2 // 2
         return xz[:, :E], xz[:, E:]
 
@@ -371,7 +390,7 @@ class InProj(torch.autograd.Function):
                 hb, sbk = (_rows_from_end(h2, b, L, d), -d) if rev else (h2, d)
                 for i, g in halves:  # dW[c][j] = sum_{b,l} g[b][c][l] h[b][l'][j]
                     _wgrad_tokens(g, (L, 1, E * L), hb, (sbk, 1, L * d), E, d, L, b, part, i * E, E2)
-                dw = _sum_parts(part, (E2, d), wdt)
+                dw = _finish_wgrad(part, ctx.weight, (E2, d), wdt)
         return dh, dw, None, None
 
 
@@ -417,6 +436,7 @@ class OutProj(torch.autograd.Function):
                           bias_n=bn, accumulate=into is not None)
         ctx.save_for_backward(yc, w)
         ctx.cfg = (y.dtype, weight.dtype, None if bias is None else bias.dtype, into is not None)
+        ctx.weight = weight
         if into is not None:
             ctx.mark_dirty(into)
         return out
@@ -440,7 +460,7 @@ class OutProj(torch.autograd.Function):
             if ctx.needs_input_grad[1]:  # dW[o][e] = sum_{b,l} dout[b][l'][o] y[b][e][l]
                 part, _ = _wgrad_tokens(db_, (1, sd, L * d), yc, (1, yc.stride(1), yc.stride(0)),
                                         d, E, L, b)
-                dw = _sum_parts(part, (d, E), wdt)
+                dw = _finish_wgrad(part, ctx.weight, (d, E), wdt)
             if bdt is not None and ctx.needs_input_grad[2]:
                 db = dout.float().sum((0, 1)).to(bdt)
         return dy, dw, db, (dout if rev else None)

@@ -58,6 +58,9 @@ class ModuleTrainer:
         self.loss_fn = loss_fn
         self.autocast = autocast
         self.flat = FlatParams(self.model, device, shadow_dtype=None)
+        # weight gradients the hand-written kernels can write into the flat buffer go there
+        # directly (no returned dW, no AccumulateGrad add); others return theirs as before
+        self.flat.enable_direct_grad(True)
         self.opt = FusedAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                               max_grad_norm=max_grad_norm)
         self.reducer = GradBucketReducer(self.flat, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
