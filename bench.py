@@ -158,7 +158,7 @@ CONFIG_A = dict(vocab_size=4096, hidden_size=128, num_hidden_layers=2, num_atten
                 intermediate_size=512)
 
 
-def dist_skeleton(args, world, rank):
+def dist_skeleton(args, world, rank, out=None):
     """--dist-dry-run: the multi-rank measurement protocol without the model (CPU, gloo): the
     same barrier / timed region / max-over-ranks / one-JSON-line path, with a gradient-sized
     all-reduce as the step. Used by the CPU test of the launcher; never a bench number."""
@@ -178,7 +178,7 @@ def dist_skeleton(args, world, rank):
                           "steps": args.steps, "warmup": args.warmup, "dry_run": True,
                           "ms_per_step": round(float(el) / max(1, args.steps) * 1e3, 3),
                           "config": {"parallelism": f"dp{world}", "global_batch": args.batch * world}}),
-              flush=True)
+              file=out or sys.stdout, flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -212,8 +212,14 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} ranks",
               file=sys.stderr)
+    # the result is ONE JSON line on stdout: everything else the process writes to fd 1 -- RCCL's
+    # init banner ("RCCL version ...", NCCL WARN lines), gloo's "[Gloo] Rank ..." lines -- goes
+    # to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     if args.dist_dry_run:
-        return dist_skeleton(args, world, rank)
+        return dist_skeleton(args, world, rank, result_out)
 
     data_pipeline = None
     if rank == 0 and world == 1 and not args.no_data_pipeline:
@@ -366,7 +372,7 @@ def main():
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
             "data_pipeline": data_pipeline, "b64": b64,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     if use_pg:
         dist.barrier()
         dist.destroy_process_group()

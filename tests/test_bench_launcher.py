@@ -18,6 +18,8 @@ def _run(n):
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
+    # and nothing else on stdout (the process-group libraries' own lines go to stderr)
+    assert r.stdout.strip().splitlines() == lines, r.stdout
     return json.loads(lines[0])
 
 

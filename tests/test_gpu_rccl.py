@@ -74,6 +74,16 @@ def test_bench_world1_rccl_bf16_wire():
     assert len(lines) == 1
     line = lines[0]
     assert line["config"]["grad_allreduce"] is True and line["config"]["grad_wire"] == "bf16"
+    # RCCL writes its init banner to stdout; bench.py routes it to stderr so the driver reads
+    # exactly one line (round 6: the banner broke a JSON parse of the RCCL arm)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup",
+                        "1", "--batch", "16", "--no-cpu-baseline", "--no-b64",
+                        "--no-data-pipeline", "--no-kernel-timing"],
+                       cwd=ROOT, env=_env(NCCL_DEBUG="WARN"), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(r.stdout.strip().splitlines()) == 1, r.stdout[:2000]
+    json.loads(r.stdout)
     assert line["native_only"] is True and line["value"] > 0
     assert math.isfinite(line["final_loss"])
 

@@ -235,6 +235,7 @@ def test_bench_multi_rank_real_model(tmp_path, ranks):
         r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=err, text=True,
                            timeout=400)
     assert r.returncode == 0, open(log).read()[-3000:]
+    assert len(r.stdout.strip().splitlines()) == 1, r.stdout  # ONE line: RCCL / gloo talk -> stderr
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     line = lines[0]
