@@ -185,7 +185,7 @@ class ChannelLinear(torch.autograd.Function):
         xin = x.to(dt)
         if xin.stride(2) != 1:
             xin = xin.contiguous()
-        w = weight.detach().to(dt).contiguous()
+        w = _lowp(weight, dt)
         y = torch.empty(b, M, L, device=x.device, dtype=dt)
         with _timed("mamba_proj", (b * K * L + b * M * L) * xin.element_size(), "byte"):
             _strided_gemm(w, (K, 1, 0), xin, (xin.stride(1), 1, xin.stride(0)), y, (L, M * L),
@@ -241,6 +241,16 @@ def _wgrad_tokens(dy, sa, x, sb, M, Nn, T, batch, part=None, row0=0, rows_total=
     assert part.shape[0] == batch * s
     DF.strided_gemm(dy, sa, x, sb, part[:, row0:], (Nn, rt * Nn), M, Nn, T, batch, s, out_f32=True)
     return part, s
+
+
+def _lowp(weight, dt):
+    """The weight in the compute dtype: the trainer's persistent bf16 copy when one exists
+    (ModuleTrainer: FlatParams' shadow, rewritten by the fused AdamW step -- the same bits as
+    autocast's cast), else a cast."""
+    lp = getattr(weight, "_dna_lp", None)
+    if dt == torch.bfloat16 and lp is not None:
+        return lp
+    return weight.detach().to(dt).contiguous()
 
 
 def _finish_wgrad(part, weight, shape, dtype):
@@ -310,7 +320,7 @@ class InProj(torch.autograd.Function):
         if (reverse or sink is not None) and dt != torch.bfloat16:
             raise NotImplementedError("InProj: reverse / sink need bf16 (autocast)")
         h2 = h.reshape(b * L, d).to(dt).contiguous()
-        w = weight.detach().to(dt).contiguous()
+        w = _lowp(weight, dt)
         xz = torch.empty(b, E2, L, device=h.device, dtype=dt)
         with _timed("mamba_proj", (b * L * d + b * E2 * L) * h2.element_size(), "byte"):
             # xz[b][c][l] = sum_j W[c][j] h[b][l'][j],  l' = l or L-1-l
@@ -418,7 +428,7 @@ class OutProj(torch.autograd.Function):
         yc = y.to(dt)
         if yc.stride(2) != 1 or yc.stride(1) != L:
             yc = yc.contiguous()
-        w = weight.detach().to(dt).contiguous()
+        w = _lowp(weight, dt)
         d = w.shape[0]
         bn = None if bias is None else bias.detach().to(dt).float().contiguous()
         if into is not None:

@@ -57,7 +57,14 @@ class ModuleTrainer:
         self.device = torch.device(device)
         self.loss_fn = loss_fn
         self.autocast = autocast
-        self.flat = FlatParams(self.model, device, shadow_dtype=None)
+        # bf16 autocast: a persistent bf16 copy of every parameter, rewritten by the fused AdamW
+        # step, stands in for autocast's per-forward weight casts where the kernels read it
+        # (mamba._lowp: `_dna_lp` on the parameter)
+        lowp = autocast == torch.bfloat16 and torch.device(device).type == "cuda"
+        self.flat = FlatParams(self.model, device, shadow_dtype=torch.bfloat16 if lowp else None)
+        if lowp:
+            for p in self.flat.params:
+                p._dna_lp = self.flat.lp(p)
         # weight gradients the hand-written kernels can write into the flat buffer go there
         # directly (no returned dW, no AccumulateGrad add); others return theirs as before
         self.flat.enable_direct_grad(True)
@@ -67,6 +74,7 @@ class ModuleTrainer:
         self.world = self.reducer.world
         if self.reducer.enabled:  # DDP construction broadcast
             broadcast_(self.flat.flat, src=0)
+            self.flat.refresh_shadow()
         self.global_step = 0
 
     def step(self, batch) -> torch.Tensor:

@@ -1,10 +1,8 @@
+set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r06
-for rep in 1 2; do
-PYTHONFAULTHANDLER=1 NCCL_DEBUG=WARN DNA_DDP_FORCE=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-b64 --no-data-pipeline > gpurun_out/r06/force$rep.json 2> gpurun_out/r06/force$rep.err
-echo "force rc=$?"
-head -c 300 gpurun_out/r06/force$rep.json; echo
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-b64 --no-data-pipeline > gpurun_out/r06/noforce$rep.json 2> gpurun_out/r06/noforce$rep.err
-echo "noforce rc=$?"
-head -c 300 gpurun_out/r06/noforce$rep.json; echo
-done
+bash scripts/gpu.sh ab-env DNA_DDP_FORCE "0 1" 3
+cp gpurun_out/ab.log gpurun_out/r06/ab_reducer_force.txt
+timeout -k 10 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread -m gpu -p no:cacheprovider \
+  tests/test_gpu_rccl.py > gpurun_out/r06/tests_rccl.log 2>&1
+tail -3 gpurun_out/r06/tests_rccl.log
