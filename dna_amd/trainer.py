@@ -42,6 +42,18 @@ class DeviceBatch:
                                                        idx.flat_masked))), n_mask, n_unk)
 
 
+def _sync_shadow(flat, versions):
+    """Re-derive the bf16 parameter copy when a parameter was changed in place outside the fused
+    AdamW step (load_state_dict, a manual edit): torch bumps the tensor's version counter then, the
+    AdamW kernel (raw pointers) does not. Returns the versions to compare against next step."""
+    if flat.shadow is None:
+        return None
+    v = [p._version for p in flat.params]
+    if v != versions:
+        flat.refresh_shadow()
+    return v
+
+
 class ModuleTrainer:
     """The same data-parallel step for any model (BASELINE configs D / E: HyenaDNA, Caduceus):
     parameters and gradients in one flat buffer (FlatParams), gradient buckets all-reduced over
@@ -74,10 +86,11 @@ class ModuleTrainer:
         self.world = self.reducer.world
         if self.reducer.enabled:  # DDP construction broadcast
             broadcast_(self.flat.flat, src=0)
-            self.flat.refresh_shadow()
+        self._versions = _sync_shadow(self.flat, None)  # bf16 copy of the (broadcast) weights
         self.global_step = 0
 
     def step(self, batch) -> torch.Tensor:
+        self._versions = _sync_shadow(self.flat, self._versions)
         self.opt.zero_grad()
         self.reducer.prepare(sync=True)
         if self.autocast is not None:
@@ -109,12 +122,12 @@ class MLMTrainer:
         self.world = self.reducer.world
         if self.reducer.enabled:  # DDP construction broadcast (C2 in SURVEY §2.2)
             broadcast_(self.flat.flat, src=0)
-            self.flat.refresh_shadow()
         # dropout stream: derived from train.seed when given, and distinct per rank
         rank = dist.get_rank() if dist.is_initialized() else 0
         base = self.model.dropout_rng.seed if seed is None else int(seed) + 0x5EED
         self.model.dropout_rng.seed = (base * 1000003 + rank) & (2 ** 63 - 1)
         self.global_step = 0
+        self._versions = _sync_shadow(self.flat, None)
         self.micro_losses = []  # undivided loss of each micro-batch of the last step (metrics)
 
     def rng_state(self):
@@ -134,6 +147,7 @@ class MLMTrainer:
         no_sync)."""
         micro = batch if isinstance(batch, (list, tuple)) else [batch]
         div = len(micro) if accum is None else int(accum)
+        self._versions = _sync_shadow(self.flat, self._versions)
         self.opt.zero_grad()
         total = None
         self.micro_losses = []

@@ -106,3 +106,20 @@ def test_caduceus_two_ranks_equals_single_process(autocast, wire):
         frac = ((r0 - ref).abs() > 0.25 * lr).float().mean().item()
         assert frac < 0.01, frac
         assert float((d_dp - d_ref).norm() / d_ref.norm()) < 0.1
+
+
+def test_bf16_shadow_follows_load_state_dict():
+    """The Mamba projections read the trainer's bf16 parameter copy; weights loaded after the
+    trainer exists (load_state_dict) must reach it before the next step."""
+    src = _trainer(seed=1, autocast=torch.bfloat16)
+    tr = _trainer(seed=0, autocast=torch.bfloat16)
+    tr.model.load_state_dict(src.model.state_dict())
+    batch = tuple(t.cuda() for t in _batch(3, 2))
+    la, lb = tr.step(batch), src.step(batch)
+    torch.cuda.synchronize()
+    assert float(la) == float(lb)  # the forward saw the loaded weights
+    # the scan backward sums dA / dB / dC with atomics (order-dependent last bits), so the two
+    # updates agree up to AdamW's lr * sign(g) on near-zero gradient entries
+    frac = ((tr.flat.flat - src.flat.flat).abs() > 0.25 * 2e-3).float().mean().item()
+    assert frac < 0.01, frac
+    assert torch.equal(tr.flat.shadow, tr.flat.flat.bfloat16())
