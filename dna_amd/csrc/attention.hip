@@ -337,17 +337,28 @@ __device__ __forceinline__ constexpr int aoff(int r) { return (r & 3) + 8 * (r >
 
 // NW waves per workgroup: 4 (two workgroups per CU) or 8 (one workgroup covers 512 queries, so
 // at S = 512 each (b, h)'s K/V tiles stream from HBM once instead of once per 256 queries)
-template <int NQB, int NW = 4>
+// DMA (NW = 4 only): the K / V tiles go global -> LDS by LDS-DMA (buffer_load ... lds) into a
+// ring of NST tile buffers, two tiles ahead of the one computed -- no staging registers, no LDS
+// writes by the waves, and a tile's HBM latency has two iterations to land; the pad bias of the
+// whole key row is staged in LDS once. LDS image as before (the swizzle is applied by choosing
+// which 16-B chunk of its row each lane fetches).
+constexpr int NST = 3;
+constexpr size_t fwd_dma_lds(int S) { return (size_t)NST * 2 * BK * D * 2 + (size_t)S * 4; }
+
+template <int NQB, int NW = 4, bool DMA = false>
 __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fwd2_bf16_kernel(const bf16* __restrict__ qkv,
                                                            const uint8_t* __restrict__ key_valid,
                                                            const float* __restrict__ slopes,
                                                            int S, int H, float c,
                                                            bf16* __restrict__ out,
                                                            float* __restrict__ lse) {
+  static_assert(!DMA || NW == 4, "DMA staging: 4 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* Ks = reinterpret_cast<bf16*>(smem);               // [2][64*64] swizzled
   bf16* Vs = Ks + 2 * BK * D;                             // [2][64*64] swizzled
   float* kb = reinterpret_cast<float*>(Vs + 2 * BK * D);  // [2][64] pad bias (log2 units)
+  // DMA: tile buffer t = K [64*64] then V [64*64] at smem + t * 16 KB; pad bias [S] after them
+  float* kball = reinterpret_cast<float*>(smem + (size_t)NST * 2 * BK * D * 2);
 
   int qblk, h, b;
   constexpr int QPB = NW * 32 * NQB;  // queries per workgroup
@@ -371,6 +382,29 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
     for (int s = 0; s < 4; ++s)
       qf[j][s] = *reinterpret_cast<const bf16x8*>(base + (size_t)qrow * ld + h * D + 16 * s + 8 * hh);
   }
+  // DMA: per-lane byte offsets of piece p (rows (p*4 + wave)*8 + lane/8 of a tile, the 16-B chunk
+  // that lands in slot lane%8 of the swizzled row); the tile's row offset is added per issue
+  const auto rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(base), (short)0,
+                                                    (int)((size_t)S * ld * 2), 0x00020000);
+  uint32_t vk[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int rr = (p * 4 + wave) * 8 + (lane >> 3);
+    const int cc = (lane & 7) ^ swz_key(rr);
+    vk[p] = (uint32_t)((rr * ld + H * D + h * D + cc * 8) * 2);
+  }
+  auto issue = [&](int kt, int buf) __attribute__((always_inline)) {
+    typedef __attribute__((address_space(3))) void lds_v;
+    const uint32_t toff = (uint32_t)(kt * BK * ld * 2);
+    char* dk = smem + (size_t)buf * 2 * BK * D * 2;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      char* dst = dk + (p * 4 + wave) * 8 * 128;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (lds_v*)dst, 16, vk[p] + toff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (lds_v*)(dst + BK * D * 2), 16,
+                                               vk[p] + (uint32_t)(H * D * 2) + toff, 0, 0, 0);
+    }
+  };
   f32x16 initL, initR;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -429,23 +463,39 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
 
   const int nt = S / BK;
   const int kt0 = (qblk * (QPB / BK) + (NQB == 1 ? 0 : 1)) % nt;  // near-diagonal tiles first
-  {
+  auto tile_at = [&](int i) { const int t = kt0 + i % nt; return t >= nt ? t - nt : t; };
+  if constexpr (DMA) {
+    // the Q and key_valid loads are older than the tile pieces, so the first wait retires them
+    for (int j = tid; j < S; j += 64 * NW)
+      kball[j] = key_valid && !key_valid[(size_t)b * S + j] ? PAD_BIAS * LOG2E : 0.f;
+    issue(tile_at(0), 0);
+    issue(tile_at(1), 1);
+  } else {
     TileRegs t; float bias;
     load_tile(kt0, t, bias);
     store_tile(0, t, bias);
+    __syncthreads();
   }
-  __syncthreads();
 
   for (int it = 0; it < nt; ++it) {
     int kt = kt0 + it;
     if (kt >= nt) kt -= nt;
-    const int buf = it & 1;
+    const int buf = DMA ? it % NST : it & 1;
     TileRegs nx; float nbias = 0.f;
-    if (it + 1 < nt) load_tile(kt + 1 < nt ? kt + 1 : kt + 1 - nt, nx, nbias);
+    if constexpr (DMA) {
+      // this tile's pieces landed (the 4 of the next tile may still be in flight), everyone's
+      // pieces too and every wave is past the tile it - 1, whose buffer the issue below refills
+      // (past the end: a tile nobody reads, so every wait keeps the same count)
+      __builtin_amdgcn_s_waitcnt((4 & 0xF) | (0x7 << 4) | (0xF << 8));
+      __syncthreads();
+      issue(tile_at(it + 2), (it + 2) % NST);
+    } else {
+      if (it + 1 < nt) load_tile(kt + 1 < nt ? kt + 1 : kt + 1 - nt, nx, nbias);
+    }
 
-    const bf16* K = Ks + buf * BK * D;
-    const bf16* V = Vs + buf * BK * D;
-    const float* kbias = kb + buf * BK;
+    const bf16* K = DMA ? reinterpret_cast<const bf16*>(smem) + (size_t)buf * 2 * BK * D : Ks + buf * BK * D;
+    const bf16* V = DMA ? K + BK * D : Vs + buf * BK * D;
+    const float* kbias = DMA ? kball + kt * BK : kb + buf * BK;
     const bool haspad = key_valid && wave_any(kbias[lane] != 0.f);
 
 #pragma unroll
@@ -528,9 +578,12 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
           for (int j = 0; j < NQB; ++j) o[j][dt] = mfma(a, pbf[j][s], o[j][dt]);
         }
     }
-    if (it + 1 < nt) store_tile(buf ^ 1, nx, nbias);
-    __syncthreads();
+    if constexpr (!DMA) {
+      if (it + 1 < nt) store_tile(buf ^ 1, nx, nbias);
+      __syncthreads();
+    }
   }
+  if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the block
 
 #pragma unroll
   for (int j = 0; j < NQB; ++j) {
@@ -2008,6 +2061,19 @@ extern "C" int dna_attn_fwd(const void* qkv, const uint8_t* key_valid, const flo
         dim3 grid(((seqlen + 127) / 128) * heads * batch);
         hipLaunchKernelGGL((fwd2_bf16_kernel<1>), grid, dim3(256), FWD_LDS, s, (const bf16*)qkv,
                            key_valid, slopes, seqlen, heads, softmax_scale * LOG2E, (bf16*)out, lse);
+      } else if (forced != 2 && forced != 8 && fwd_dma_lds(seqlen) <= 96 * 1024) {
+        // default: the LDS-DMA K/V ring (0.731 -> 0.712 ms at b = 512, interleaved A/B in
+        // profiles/r06/ab_attn_fwd_dma.txt); DNA_ATTN_FWD=2 runs the register-staged form
+        static const bool attr = [] {
+          (void)hipFuncSetAttribute((const void*)fwd2_bf16_kernel<2, 4, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+          return true;
+        }();
+        (void)attr;
+        dim3 grid(((seqlen + BQ2 - 1) / BQ2) * heads * batch);
+        hipLaunchKernelGGL((fwd2_bf16_kernel<2, 4, true>), grid, dim3(256), fwd_dma_lds(seqlen), s,
+                           (const bf16*)qkv, key_valid, slopes, seqlen, heads,
+                           softmax_scale * LOG2E, (bf16*)out, lse);
       } else if (forced == 8) {  // eight waves, 512 queries per workgroup (A/B)
         dim3 grid(((seqlen + 511) / 512) * heads * batch);
         hipLaunchKernelGGL((fwd2_bf16_kernel<2, 8>), grid, dim3(512), FWD_LDS, s, (const bf16*)qkv,
