@@ -89,11 +89,20 @@ __device__ __forceinline__ uint32_t dropout_keep4(uint64_t seed, uint64_t offset
 // two dropout_keep4 calls. Philox4x32 with 7 rounds: Salmon et al. (SC'11) find 7 rounds of
 // Philox4x32 pass TestU01's BigCrush (10 is Random123's default safety margin); the draws sit in
 // the GeGLU GEMM epilogue's VALU budget (geglu_epi_ab.py: 10 -> 7 rounds -0.03 ms per launch).
+// The draw itself: element j of the group keeps iff its 16-bit half (r[j / 2] >> 16 * (j & 1)) &
+// 0xFFFF is >= thresh16 (dropout_kept8).
+__device__ __forceinline__ uint4 dropout_draw8(uint64_t seed, uint64_t offset, uint64_t idx8) {
+  const uint64_t c = idx8 + offset;
+  return Philox::gen<7>((uint32_t)c, (uint32_t)(c >> 32), 0x5EED8u, 0u, (uint32_t)seed,
+                        (uint32_t)(seed >> 32));
+}
+__device__ __forceinline__ bool dropout_kept8(const uint4& r, int j, uint32_t thresh16) {
+  const uint32_t w = j < 2 ? r.x : j < 4 ? r.y : j < 6 ? r.z : r.w;
+  return ((j & 1) ? (w >> 16) : (w & 0xFFFFu)) >= thresh16;
+}
 __device__ __forceinline__ uint32_t dropout_keep8(uint64_t seed, uint64_t offset, uint64_t idx8,
                                                   uint32_t thresh16) {
-  uint64_t c = idx8 + offset;
-  uint4 r = Philox::gen<7>((uint32_t)c, (uint32_t)(c >> 32), 0x5EED8u, 0u, (uint32_t)seed,
-                           (uint32_t)(seed >> 32));
+  const uint4 r = dropout_draw8(seed, offset, idx8);
   const uint32_t w[4] = {r.x, r.y, r.z, r.w};
   uint32_t m = 0;
 #pragma unroll

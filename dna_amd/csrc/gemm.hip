@@ -783,12 +783,14 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       const uint32_t oa = voAx + (uint32_t)((row * a.F + c.n0) * 2);
       const bf16x8 h1 = __builtin_bit_cast(bf16x8, g1), h2 = __builtin_bit_cast(bf16x8, g2);
       const size_t e = (size_t)(row + wr * 64 + (lane & 15)) * a.F + c.n0 + colq;  // e % 8 == 0
-      const uint32_t keep = a.p > 0.f ? dropout_keep8(a.seed, a.off, e >> 3, a.th) : 0xFFu;
+      // the keep decision per element straight from its 16-bit half of the draw (a compare +
+      // select each; packing the 8 bits into a mask and unpacking them cost ~4 VALU more apiece)
+      const uint4 r = a.p > 0.f ? dropout_draw8(a.seed, a.off, e >> 3) : make_uint4(~0u, ~0u, ~0u, ~0u);
       bf16x8 o, f1, f2;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         float x, y1, y2;
-        geglu_fwd_fac((float)h1[q], (float)h2[q], (keep >> q) & 1, a.ks, x, y1, y2);
+        geglu_fwd_fac((float)h1[q], (float)h2[q], dropout_kept8(r, q, a.th), a.ks, x, y1, y2);
         o[q] = (bf16)x;
         f1[q] = (bf16)y1;
         f2[q] = (bf16)y2;
