@@ -140,7 +140,8 @@ __device__ __forceinline__ float erf_fast(float z, float& e) {
   p = fmaf(p, t, -0.284496736f);
   p = fmaf(p, t, 0.254829592f);
   p *= t;
-  e = __builtin_amdgcn_exp2f(-az * az * 1.4426950408889634f);
+  // z * z, not |z| * |z| (same bits): no abs modifier, so the compiler pairs it into v_pk_mul
+  e = __builtin_amdgcn_exp2f(z * z * -1.4426950408889634f);
   return copysignf(fmaf(-p, e, 1.f), z);
 }
 __device__ __forceinline__ float gelu_erf(float x) {
@@ -150,7 +151,7 @@ __device__ __forceinline__ float gelu_erf(float x) {
 // GELU(x) and its derivative Phi(x) + x phi(x), sharing one erf / exp
 __device__ __forceinline__ void gelu_erf_and_grad(float x, float& g, float& dg) {
   float e;
-  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f, e));
+  const float cdf = fmaf(0.5f, erf_fast(x * 0.70710678118654752f, e), 0.5f);  // one v_pk_fma
   g = x * cdf;
   dg = fmaf(x * 0.3989422804014327f, e, cdf);  // e = exp(-x^2 / 2)
 }
