@@ -36,7 +36,8 @@ def _qkv(b, S, H, dtype, pad_rows=(), seed=0):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 3e-2)])
 @pytest.mark.parametrize("b,S,H,pads", [(2, 128, 2, [(1, 77)]), (1, 512, 12, []),
-                                        (3, 64, 1, [(0, 5), (2, 63)]), (2, 256, 4, [(0, 200)])])
+                                        (3, 64, 1, [(0, 5), (2, 63)]), (2, 256, 4, [(0, 200)]),
+                                        (1, 2048, 2, [(0, 1500)])])  # 32 tiles through the ring
 def test_attention_forward(dtype, tol, b, S, H, pads):
     from dna_amd import functional as DF
     from dna_amd.config import alibi_slopes
