@@ -60,6 +60,8 @@ _SIGS = {
                         _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dna_ln_bwd_from_y": (_i, [_vp, _vp, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _i, _i, _vp,
                                _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dna_ln_bwd_from_y_acc": (_i, [_vp, _vp, _vp, _i, _f, _u64, _u64, _vp, _vp, _vp, _i, _i, _vp,
+                                   _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dna_add_ln_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _i, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dna_add_ln_bwd": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp,
                             _vp, _vp, _sz, _vp]),

@@ -507,7 +507,8 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(EmbBwdArgs a) {
 constexpr int RP_GROUPS = 16;
 __global__ __launch_bounds__(64 * RP_GROUPS) void reduce_partials(const float* __restrict__ part,
                                                                   int nblocks, int cols,
-                                                                  float* o0, float* o1, float* o2) {
+                                                                  float* o0, float* o1, float* o2,
+                                                                  int acc = 0) {
   __shared__ float red[RP_GROUPS][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + tx;
@@ -531,7 +532,8 @@ __global__ __launch_bounds__(64 * RP_GROUPS) void reduce_partials(const float* _
     for (int g = 1; g < RP_GROUPS; ++g) s += red[g][tx];
     const int q = i / cols, c = i % cols;
     float* o = q == 0 ? o0 : (q == 1 ? o1 : o2);
-    if (o) o[c] = s;
+    // acc: o += s (the parameter's fp32 gradient, as AccumulateGrad's add would do it)
+    if (o) o[c] = acc ? o[c] + s : s;
   }
 }
 
@@ -632,7 +634,7 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
   });
   if (st) return st;
   hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
-                     (const float*)workspace, nb, cols, dgamma, dbeta, dbias);
+                     (const float*)workspace, nb, cols, dgamma, dbeta, dbias, 0);
   DNA_LAUNCH_CHECK("dna_ln_bwd");
   return DNA_OK;
 }
@@ -642,12 +644,11 @@ extern "C" int dna_ln_bwd(const float* dy, const void* dy_bf16, const void* x, i
 // bf16 and an fp32 row (3.2 instead of 3.6 GB per DNABERT-2 call at T = 262,144) -- and neither
 // x nor the residual has to be kept for the backward. gamma must have no zero entries (those
 // columns' x_hat cannot be recovered; they are taken as 0).
-extern "C" int dna_ln_bwd_from_y(const float* dy, const void* dy_bf16, const float* y, int x_dtype,
-                                 float p_drop, uint64_t seed, uint64_t offset, const float* gamma,
-                                 const float* beta, const float* rstd, int rows, int cols,
-                                 float* dresidual, void* dx, float* dgamma, float* dbeta,
-                                 float* dbias, void* workspace, size_t workspace_bytes,
-                                 void* stream) {
+static int ln_bwd_from_y(const float* dy, const void* dy_bf16, const float* y, int x_dtype,
+                         float p_drop, uint64_t seed, uint64_t offset, const float* gamma,
+                         const float* beta, const float* rstd, int rows, int cols,
+                         float* dresidual, void* dx, float* dgamma, float* dbeta, float* dbias,
+                         void* workspace, size_t workspace_bytes, void* stream, int acc) {
   DNA_CHECK_ARG(y && gamma && beta && rstd && dx, "dna_ln_bwd_from_y: null pointer");
   DNA_CHECK_ARG(x_dtype == DNA_F32 || x_dtype == DNA_BF16, "dna_ln_bwd_from_y: bad dtype");
   if (rows == 0) return DNA_OK;
@@ -670,9 +671,34 @@ extern "C" int dna_ln_bwd_from_y(const float* dy, const void* dy_bf16, const flo
   });
   if (st) return st;
   hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
-                     (const float*)workspace, nb, cols, dgamma, dbeta, dbias);
+                     (const float*)workspace, nb, cols, dgamma, dbeta, dbias, acc);
   DNA_LAUNCH_CHECK("dna_ln_bwd_from_y");
   return DNA_OK;
+}
+
+extern "C" int dna_ln_bwd_from_y(const float* dy, const void* dy_bf16, const float* y, int x_dtype,
+                                 float p_drop, uint64_t seed, uint64_t offset, const float* gamma,
+                                 const float* beta, const float* rstd, int rows, int cols,
+                                 float* dresidual, void* dx, float* dgamma, float* dbeta,
+                                 float* dbias, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+  return ln_bwd_from_y(dy, dy_bf16, y, x_dtype, p_drop, seed, offset, gamma, beta, rstd, rows,
+                       cols, dresidual, dx, dgamma, dbeta, dbias, workspace, workspace_bytes,
+                       stream, 0);
+}
+
+// The same, adding dgamma / dbeta / dbias into the given (parameter-gradient) buffers instead
+// of overwriting them: the fp32 flat gradient of a FlatParams-owned LayerNorm (dna_amd.flat),
+// with no separate accumulate launch per parameter.
+extern "C" int dna_ln_bwd_from_y_acc(const float* dy, const void* dy_bf16, const float* y,
+                                     int x_dtype, float p_drop, uint64_t seed, uint64_t offset,
+                                     const float* gamma, const float* beta, const float* rstd,
+                                     int rows, int cols, float* dresidual, void* dx, float* dgamma,
+                                     float* dbeta, float* dbias, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  return ln_bwd_from_y(dy, dy_bf16, y, x_dtype, p_drop, seed, offset, gamma, beta, rstd, rows,
+                       cols, dresidual, dx, dgamma, dbeta, dbias, workspace, workspace_bytes,
+                       stream, 1);
 }
 
 // Pre-norm residual add + LayerNorm / RMSNorm (rms = 1: mamba_ssm's Block with fused_add_norm,
@@ -736,7 +762,7 @@ extern "C" int dna_add_ln_bwd(const float* dy, const void* dy_bf16, const float*
   });
   if (st) return st;
   hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
-                     (const float*)workspace, nb, cols, dgamma, rms ? (float*)nullptr : dbeta, (float*)nullptr);
+                     (const float*)workspace, nb, cols, dgamma, rms ? (float*)nullptr : dbeta, (float*)nullptr, 0);
   DNA_LAUNCH_CHECK("dna_add_ln_bwd");
   return DNA_OK;
 }
@@ -791,7 +817,7 @@ static int embed_ln_bwd_impl(const float* dy, const void* dy_bf16, const int64_t
   if (st) return st;
   // partial slots: 0 dgamma, 1 dbeta, 2 d(type_row)
   hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
-                     (const float*)workspace, nb, cols, dgamma, dbeta, dtype_row);
+                     (const float*)workspace, nb, cols, dgamma, dbeta, dtype_row, 0);
   DNA_LAUNCH_CHECK("dna_embed_ln_bwd");
   return DNA_OK;
 }
@@ -871,7 +897,7 @@ extern "C" int dna_rms_bwd(const float* dy, const void* dy_bf16, const void* x, 
   });
   if (st) return st;
   hipLaunchKernelGGL(reduce_partials, dim3((3 * cols + 63) / 64), dim3(64 * RP_GROUPS), 0, s,
-                     (const float*)workspace, nb, cols, dgamma, (float*)nullptr, (float*)nullptr);
+                     (const float*)workspace, nb, cols, dgamma, (float*)nullptr, (float*)nullptr, 0);
   DNA_LAUNCH_CHECK("dna_rms_bwd");
   return DNA_OK;
 }

@@ -304,6 +304,19 @@ def strided_linear(x, weight, bias=None):
 
 
 # ----------------------------------------------------------------------------------- fused LN
+_PARAM_DIRECT = os.environ.get("DNA_PARAM_GRAD_DIRECT", "1") != "0"  # 0: AccumulateGrad (A/B)
+
+
+def _param_grads_direct(params):
+    """Every parameter of the tuple (None entries skipped) is FlatParams-owned with direct
+    gradients on (dna_amd.flat.enable_direct_grad) and holds its fp32 .grad view: the kernel may
+    then add its gradient there itself. Only for loss.backward() into those buffers."""
+    ps = [q for q in params if q is not None]
+    return _PARAM_DIRECT and bool(ps) and all(getattr(q, "_dna_direct", False) and q.grad is not None
+                            and q.grad.dtype == torch.float32 and q.grad.is_contiguous()
+                            for q in ps)
+
+
 class FusedLayerNorm(torch.autograd.Function):
     """LN(dropout(act(x + bias)) + residual) -> (y fp32|None, y_bf16|None).
 
@@ -334,6 +347,8 @@ class FusedLayerNorm(torch.autograd.Function):
         if ctx.from_y:
             ctx.save_for_backward(y, bias, gamma, beta, rstd)
             ctx.shape = (n, d, x.dtype, residual is not None)
+            # the parameters themselves (their .grad / FlatParams flags), for _param_grads_direct
+            ctx.params = (bias, gamma, beta)
         else:
             ctx.save_for_backward(x, bias, residual, gamma, mean, rstd)
         ctx.cfg = (act, p, seed, off)
@@ -373,9 +388,16 @@ class FusedLayerNorm(torch.autograd.Function):
         n, d, xdt, has_res = ctx.shape
         dx = torch.empty(n, d, device=y.device, dtype=xdt)
         dres = torch.empty(n, d, device=y.device, dtype=torch.float32) if has_res else None
-        dg = torch.empty_like(gamma)
-        db = torch.empty_like(gamma)
-        dbias = torch.empty_like(bias) if bias is not None else None
+        direct = _param_grads_direct(ctx.params)
+        if direct:
+            # dgamma / dbeta / dbias added straight into the flat fp32 gradient (dna_amd.flat)
+            # by the partial-sum pass, instead of three AccumulateGrad adds
+            pb, pg, pbe = ctx.params
+            dg, db, dbias = pg.grad, pbe.grad, (pb.grad if pb is not None else None)
+        else:
+            dg = torch.empty_like(gamma)
+            db = torch.empty_like(gamma)
+            dbias = torch.empty_like(bias) if bias is not None else None
         nws = N.lib().dna_ln_bwd_workspace(n, d)
         ws = torch.empty(max(nws, 16), device=y.device, dtype=torch.uint8)
         dy = None if dy is None else dy.contiguous()
@@ -385,10 +407,16 @@ class FusedLayerNorm(torch.autograd.Function):
         nbytes = n * (d * ((4 if dy is not None else 0) + (2 if dyb is not None else 0) + 4 + es
                            + (4 if has_res else 0)) + 4)
         with _timed("ln_bwd", nbytes, "byte"):
-            N.call("dna_ln_bwd_from_y", _p(dy), _p(dyb), y.data_ptr(), _dt(dx), p, seed, off,
-                   gamma.data_ptr(), beta.data_ptr(), rstd.data_ptr(), n, d, _p(dres),
-                   dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _p(dbias), ws.data_ptr(), nws,
-                   N.stream_ptr())
+            N.call("dna_ln_bwd_from_y_acc" if direct else "dna_ln_bwd_from_y", _p(dy), _p(dyb),
+                   y.data_ptr(), _dt(dx), p, seed, off, gamma.data_ptr(), beta.data_ptr(),
+                   rstd.data_ptr(), n, d, _p(dres), dx.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                   _p(dbias), ws.data_ptr(), nws, N.stream_ptr())
+        if direct:
+            for q in ctx.params:
+                notify = getattr(q, "_dna_notify", None) if q is not None else None
+                if notify is not None:
+                    notify(q)
+            return dx, None, dres, None, None, None, None, None, None, None, None, None
         return dx, dbias, dres, dg, db, None, None, None, None, None, None, None
 
 

@@ -129,6 +129,14 @@ int dna_ln_bwd_from_y(const float* dy, const void* dy_bf16, const float* y, int 
                       const float* beta, const float* rstd, int rows, int cols, float* dresidual,
                       void* dx, float* dgamma, float* dbeta, float* dbias, void* workspace,
                       size_t workspace_bytes, void* stream);
+/* dna_ln_bwd_from_y adding dgamma / dbeta / dbias into the given buffers (+=) instead of writing
+ * them: the parameters' fp32 gradient slices of a flat gradient buffer (dna_amd.flat), in place
+ * of torch AccumulateGrad's per-parameter add (same fp32 add). */
+int dna_ln_bwd_from_y_acc(const float* dy, const void* dy_bf16, const float* y, int x_dtype,
+                          float p_drop, uint64_t seed, uint64_t offset, const float* gamma,
+                          const float* beta, const float* rstd, int rows, int cols,
+                          float* dresidual, void* dx, float* dgamma, float* dbeta, float* dbias,
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* Pre-norm residual add + LayerNorm: sum = x + residual (fp32, written), y = LN(sum).
  * Replaces the flash_attn Block's `residual = dropout(x) + residual; norm(residual)` with
