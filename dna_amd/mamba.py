@@ -69,6 +69,7 @@ class SelectiveScan(torch.autograd.Function):
         ctx.cfg = (bool(delta_softplus), A.dtype, B.dtype, C.dtype, D is not None,
                    delta_bias is not None)
         ctx.sink = sink
+        ctx.refs = (D, delta_bias)  # the parameters themselves when passed as such (fp32)
         if return_last_state:
             ctx.mark_non_differentiable(last)
             return out, last
@@ -83,11 +84,33 @@ class SelectiveScan(torch.autograd.Function):
         dout = dout.contiguous().to(u.dtype)
         du, ddelta = torch.empty_like(u), torch.empty_like(u)
         dz = torch.empty_like(u) if z is not None else None
-        dA = torch.zeros_like(A32)
-        dB = torch.zeros(b, n, l, device=u.device, dtype=torch.float32)
-        dC = torch.zeros_like(dB)
-        dD = torch.zeros(d, device=u.device, dtype=torch.float32) if has_D else None
-        dbias = torch.zeros(d, device=u.device, dtype=torch.float32) if has_bias else None
+        # the kernel sums dA / dB / dC / dD / d(delta_bias) with atomics: zeroed buffers, one fill
+        # for the small ones and one for dB + dC; dD and d(delta_bias) of FlatParams-owned
+        # parameters are added straight into their fp32 gradient slices instead (no buffer, no
+        # AccumulateGrad add)
+        D_ref, bias_ref = ctx.refs
+        dD_direct = has_D and DF._param_grads_direct((D_ref,))
+        db_direct = has_bias and DF._param_grads_direct((bias_ref,))
+        nA = A32.numel()
+        small = torch.zeros(nA + (d if has_D and not dD_direct else 0)
+                            + (d if has_bias and not db_direct else 0),
+                            device=u.device, dtype=torch.float32)
+        dA = small[:nA].view_as(A32)
+        o = nA
+        if not has_D:
+            dD = None
+        elif dD_direct:
+            dD = D_ref.grad
+        else:
+            dD, o = small[o:o + d], o + d
+        if not has_bias:
+            dbias = None
+        elif db_direct:
+            dbias = bias_ref.grad
+        else:
+            dbias = small[o:o + d]
+        dBC = torch.zeros(2, b, n, l, device=u.device, dtype=torch.float32)
+        dB, dC = dBC[0], dBC[1]
         # u, delta, dout (+ z), B, C in; du, ddelta (+ dz) out; dB, dC fp32 out
         nz = 2 if z is not None else 0
         nbytes = (b * d * l * (5 + nz) + 2 * b * n * l) * u.element_size() + 2 * b * n * l * 4
@@ -100,7 +123,13 @@ class SelectiveScan(torch.autograd.Function):
         if ctx.sink is not None:
             ctx.sink.du = du
             du = None
-        return (du, ddelta, dA.to(adt), dB.to(bdt), dC.to(cdt), dD, dz, dbias, None, None, None)
+        for direct, q in ((dD_direct, D_ref), (db_direct, bias_ref)):
+            if direct:
+                notify = getattr(q, "_dna_notify", None)
+                if notify is not None:
+                    notify(q)
+        return (du, ddelta, dA.to(adt), dB.to(bdt), dC.to(cdt), None if dD_direct else dD, dz,
+                None if db_direct else dbias, None, None, None)
 
 
 def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
@@ -135,6 +164,7 @@ class CausalConv1d(torch.autograd.Function):
                    B, C, L, K, int(bool(silu)), out.data_ptr(), N.stream_ptr())
         ctx.save_for_backward(x, w, b)
         ctx.cfg = (bool(silu), weight.shape, weight.dtype, bias is not None)
+        ctx.refs = (weight, bias)
         return out
 
     @staticmethod
@@ -158,6 +188,18 @@ class CausalConv1d(torch.autograd.Function):
             s = torch.empty(C * (K + 1), device=x.device, dtype=torch.float32)
             N.call("dna_colsum_f32", part.data_ptr(), rows, C * (K + 1), s.data_ptr(), 0, N.stream_ptr())
         s = s.view(C, K + 1)
+        wref, bref = ctx.refs
+        if DF._param_grads_direct((wref, bref)):
+            # FlatParams-owned: the [C][K+1] sums go straight into the fp32 gradient slices (two
+            # strided adds instead of two copies and two AccumulateGrad adds)
+            wref.grad.view(C, K).add_(s[:, :K])
+            if bref is not None:
+                bref.grad.add_(s[:, K])
+            for q in (wref, bref):
+                notify = getattr(q, "_dna_notify", None) if q is not None else None
+                if notify is not None:
+                    notify(q)
+            return dx, None, None, None
         db = s[:, K].contiguous() if has_b else None
         return dx, s[:, :K].reshape(wshape).to(wdtype), db, None
 
