@@ -477,10 +477,12 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
     __syncthreads();
   }
 
-  for (int it = 0; it < nt; ++it) {
+  // one key tile; bufc is the tile's buffer -- a compile-time constant in the DMA ring (the loop
+  // below is unrolled by NST), so every LDS address is a per-lane base plus an immediate
+  auto iter = [&](const int it, const auto bufc) __attribute__((always_inline)) {
     int kt = kt0 + it;
     if (kt >= nt) kt -= nt;
-    const int buf = DMA ? it % NST : it & 1;
+    const int buf = bufc;
     TileRegs nx; float nbias = 0.f;
     if constexpr (DMA) {
       // this tile's pieces landed (the 4 of the next tile may still be in flight), everyone's
@@ -488,7 +490,7 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
       // (past the end: a tile nobody reads, so every wait keeps the same count)
       __builtin_amdgcn_s_waitcnt((4 & 0xF) | (0x7 << 4) | (0xF << 8));
       __syncthreads();
-      issue(tile_at(it + 2), (it + 2) % NST);
+      issue(tile_at(it + 2), (buf + 2) % NST);
     } else {
       if (it + 1 < nt) load_tile(kt + 1 < nt ? kt + 1 : kt + 1 - nt, nx, nbias);
     }
@@ -582,8 +584,24 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
       if (it + 1 < nt) store_tile(buf ^ 1, nx, nbias);
       __syncthreads();
     }
+  };
+  if constexpr (DMA) {
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    using B2 = std::integral_constant<int, 2>;
+    static_assert(NST == 3, "ring unrolled by 3");
+    int it = 0;
+    for (; it + NST <= nt; it += NST) {
+      iter(it, B0{});
+      iter(it + 1, B1{});
+      iter(it + 2, B2{});
+    }
+    if (it < nt) iter(it, B0{});
+    if (it + 1 < nt) iter(it + 1, B1{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the block
+  } else {
+    for (int it = 0; it < nt; ++it) iter(it, it & 1);
   }
-  if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the block
 
 #pragma unroll
   for (int j = 0; j < NQB; ++j) {
