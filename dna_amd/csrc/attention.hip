@@ -405,6 +405,10 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
                                                vk[p] + (uint32_t)(H * D * 2) + toff, 0, 0, 0);
     }
   };
+  // per-lane integer part of the key - query distance, as float (exact): dqk = kb2 + lq[j]
+  float lq[NQB];
+#pragma unroll
+  for (int j = 0; j < NQB; ++j) lq[j] = (float)(4 * hh - (q0 + 32 * j + ql));
   f32x16 initL, initR;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -503,6 +507,7 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
       const int kb2 = kt * BK + 32 * kh;  // first key of this half
+      const float kb2f = (float)kb2;
       bf16x8 kf[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -511,7 +516,6 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
 #pragma unroll
       for (int j = 0; j < NQB; ++j) {
         const int qf0 = q0 + 32 * j;  // wave-uniform
-        const int qi = qf0 + ql;
         const bool generic = haspad || kb2 == qf0;
         const bool left = kb2 < qf0;
         // every path leaves true score (log2 units) = sacc * c + U, U a per-lane constant, so
@@ -523,7 +527,7 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
           else sacc = mfma(kf[0], qf[j][0], initR);
 #pragma unroll
           for (int s = 1; s < 4; ++s) sacc = mfma(kf[s], qf[j][s], sacc);
-          const float dqk = (float)(kb2 + 4 * hh - qi);
+          const float dqk = kb2f + lq[j];
           U = left ? slope2 * dqk : -slope2 * dqk;
         } else {
           f32x16 zero;
@@ -532,7 +536,7 @@ __global__ __launch_bounds__(64 * NW, NQB == 1 ? 3 : (NQB == 2 ? 2 : 1)) void fw
           sacc = mfma(kf[0], qf[j][0], zero);
 #pragma unroll
           for (int s = 1; s < 4; ++s) sacc = mfma(kf[s], qf[j][s], sacc);
-          const float dqk = (float)(kb2 + 4 * hh - qi);
+          const float dqk = kb2f + lq[j];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const f32x4 pb = *reinterpret_cast<const f32x4*>(kbias + 32 * kh + 8 * g + 4 * hh);
