@@ -26,6 +26,9 @@ from . import functional as DF
 from .functional import _dt, _gpu, _p, _timed, strided_gemm as _strided_gemm
 
 
+_XDBL_SPLIT = os.environ.get("DNA_XDBL_SPLIT", "1") != "0"  # 0: autograd's slice nodes (A/B)
+
+
 class GradSink:
     """Hand-off of the scan's du to the x_proj backward (Mamba.forward): x feeds both the scan
     (u) and x_proj, so autograd would add the two gradients of x in a separate pass over
@@ -202,6 +205,28 @@ class CausalConv1d(torch.autograd.Function):
             return dx, None, None, None
         db = s[:, K].contiguous() if has_b else None
         return dx, s[:, :K].reshape(wshape).to(wdtype), db, None
+
+
+class XdblSplit(torch.autograd.Function):
+    """(x_dbl[:, :R], x_dbl[:, R:R+N], x_dbl[:, R+N:]) as views; the backward writes the three
+    slice gradients into one [b, R + 2N, L] buffer (one copy each, converting dtype on the way)
+    -- autograd's three SliceBackward nodes zero-fill a full-size tensor apiece and add them."""
+
+    @staticmethod
+    def forward(ctx, x_dbl, R, Ns):
+        ctx.cfg = (x_dbl.shape, x_dbl.dtype, x_dbl.device, R, Ns)
+        return x_dbl[:, :R], x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
+
+    @staticmethod
+    def backward(ctx, g_dt, g_b, g_c):
+        shape, dtype, dev, R, Ns = ctx.cfg
+        g = torch.empty(shape, device=dev, dtype=dtype)
+        for gi, lo, hi in ((g_dt, 0, R), (g_b, R, R + Ns), (g_c, R + Ns, shape[1])):
+            if gi is None:
+                g[:, lo:hi].zero_()
+            else:
+                g[:, lo:hi].copy_(gi)
+        return g, None, None
 
 
 class ChannelLinear(torch.autograd.Function):
@@ -588,8 +613,11 @@ class Mamba(nn.Module):
         sink = GradSink()  # the scan's du summed into x_proj's dx in its GEMM epilogue
         x_dbl = ChannelLinear.apply(x, self.x_proj.weight, sink)
         R, Ns = self.dt_rank, self.d_state
-        dt = ChannelLinear.apply(x_dbl[:, :R], self.dt_proj.weight)
-        Bm, Cm = x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
+        if _XDBL_SPLIT:
+            xdt, Bm, Cm = XdblSplit.apply(x_dbl, R, Ns)
+        else:
+            xdt, Bm, Cm = x_dbl[:, :R], x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
+        dt = ChannelLinear.apply(xdt, self.dt_proj.weight)
         y = SelectiveScan.apply(x, dt, A, Bm, Cm, self.D.float(), z.contiguous(),
                                 self.dt_proj.bias.float(), True, False, sink)
         return OutProj.apply(y, self.out_proj.weight, self.out_proj.bias, out_into)
