@@ -27,6 +27,7 @@ from .functional import _dt, _gpu, _p, _timed, strided_gemm as _strided_gemm
 
 
 _XDBL_SPLIT = os.environ.get("DNA_XDBL_SPLIT", "1") != "0"  # 0: autograd's slice nodes (A/B)
+_NEGEXP = os.environ.get("DNA_NEGEXP", "1") != "0"  # 0: -torch.exp(A_log) through autograd (A/B)
 
 
 class GradSink:
@@ -205,6 +206,31 @@ class CausalConv1d(torch.autograd.Function):
             return dx, None, None, None
         db = s[:, K].contiguous() if has_b else None
         return dx, s[:, :K].reshape(wshape).to(wdtype), db, None
+
+
+class NegExp(torch.autograd.Function):
+    """A = -exp(A_log) (mamba_ssm Mamba.forward) with a one-kernel backward, dA_log = dA * A,
+    added straight into a FlatParams-owned A_log's fp32 gradient (no separate neg / mul /
+    AccumulateGrad launches)."""
+
+    @staticmethod
+    def forward(ctx, a_log):
+        A = torch.exp(a_log.float()).neg_()
+        ctx.save_for_backward(A)
+        ctx.ref = a_log
+        return A
+
+    @staticmethod
+    def backward(ctx, dA):
+        (A,) = ctx.saved_tensors
+        ref = ctx.ref
+        if ref.dtype == torch.float32 and DF._param_grads_direct((ref,)):
+            ref.grad.addcmul_(dA, A)
+            notify = getattr(ref, "_dna_notify", None)
+            if notify is not None:
+                notify(ref)
+            return None
+        return (dA * A).to(ref.dtype)
 
 
 class XdblSplit(torch.autograd.Function):
@@ -604,7 +630,7 @@ class Mamba(nn.Module):
         if self.in_proj.bias is not None:
             bx, bz = self.in_proj.bias.chunk(2)
             x, z = x + bx.to(x.dtype)[:, None], z + bz.to(z.dtype)[:, None]
-        A = -torch.exp(self.A_log.float())
+        A = NegExp.apply(self.A_log) if _NEGEXP else -torch.exp(self.A_log.float())
         x = CausalConv1d.apply(x.contiguous(), self.conv1d.weight, self.conv1d.bias, True)
         # x_proj and dt_proj channel-major on the strided MFMA GEMM (ChannelLinear): x_dbl
         # [b, R + 2N, L] = x_proj.weight . x, delta [b, E, L] = dt_proj.weight . x_dbl[:, :R]
