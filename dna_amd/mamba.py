@@ -37,10 +37,14 @@ class GradSink:
     backward then accumulates its data gradient into du in the GEMM epilogue and returns the sum
     as the gradient of x -- the same total, one pass less. x_proj's backward necessarily runs
     after the scan's (it needs dB / dC)."""
-    __slots__ = ("du",)
+    __slots__ = ("du", "dB", "dC", "want_bc")
 
     def __init__(self):
         self.du = None
+        # with XdblSplit: the scan also leaves its fp32 dB / dC here, and the split's backward
+        # converts them straight into the x_dbl gradient (no separate .to(bf16) passes)
+        self.dB = self.dC = None
+        self.want_bc = False
 
 
 class SelectiveScan(torch.autograd.Function):
@@ -124,6 +128,11 @@ class SelectiveScan(torch.autograd.Function):
                    b, d, l, n, states.data_ptr(), dout.data_ptr(), du.data_ptr(), ddelta.data_ptr(),
                    dA.data_ptr(), dB.data_ptr(), dC.data_ptr(), _p(dD), _p(dz), _p(dbias),
                    N.stream_ptr())
+        if ctx.sink is not None and ctx.sink.want_bc:
+            ctx.sink.dB, ctx.sink.dC = dB, dC
+            gB = gC = None
+        else:
+            gB, gC = dB.to(bdt), dC.to(cdt)
         if ctx.sink is not None:
             ctx.sink.du = du
             du = None
@@ -132,7 +141,7 @@ class SelectiveScan(torch.autograd.Function):
                 notify = getattr(q, "_dna_notify", None)
                 if notify is not None:
                     notify(q)
-        return (du, ddelta, dA.to(adt), dB.to(bdt), dC.to(cdt), None if dD_direct else dD, dz,
+        return (du, ddelta, dA.to(adt), gB, gC, None if dD_direct else dD, dz,
                 None if db_direct else dbias, None, None, None)
 
 
@@ -239,20 +248,29 @@ class XdblSplit(torch.autograd.Function):
     -- autograd's three SliceBackward nodes zero-fill a full-size tensor apiece and add them."""
 
     @staticmethod
-    def forward(ctx, x_dbl, R, Ns):
+    def forward(ctx, x_dbl, R, Ns, sink=None):
+        ctx.set_materialize_grads(False)  # a slice without gradient arrives as None, not zeros
         ctx.cfg = (x_dbl.shape, x_dbl.dtype, x_dbl.device, R, Ns)
+        ctx.sink = sink
+        if sink is not None:
+            sink.want_bc = True
         return x_dbl[:, :R], x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
 
     @staticmethod
     def backward(ctx, g_dt, g_b, g_c):
         shape, dtype, dev, R, Ns = ctx.cfg
+        sink = ctx.sink
+        if sink is not None:  # the scan's fp32 dB / dC, converted by the copies below
+            g_b = sink.dB if g_b is None else g_b
+            g_c = sink.dC if g_c is None else g_c
+            sink.dB = sink.dC = None
         g = torch.empty(shape, device=dev, dtype=dtype)
         for gi, lo, hi in ((g_dt, 0, R), (g_b, R, R + Ns), (g_c, R + Ns, shape[1])):
             if gi is None:
                 g[:, lo:hi].zero_()
             else:
                 g[:, lo:hi].copy_(gi)
-        return g, None, None
+        return g, None, None, None
 
 
 class ChannelLinear(torch.autograd.Function):
@@ -640,7 +658,7 @@ class Mamba(nn.Module):
         x_dbl = ChannelLinear.apply(x, self.x_proj.weight, sink)
         R, Ns = self.dt_rank, self.d_state
         if _XDBL_SPLIT:
-            xdt, Bm, Cm = XdblSplit.apply(x_dbl, R, Ns)
+            xdt, Bm, Cm = XdblSplit.apply(x_dbl, R, Ns, sink)
         else:
             xdt, Bm, Cm = x_dbl[:, :R], x_dbl[:, R:R + Ns], x_dbl[:, R + Ns:]
         dt = ChannelLinear.apply(xdt, self.dt_proj.weight)
