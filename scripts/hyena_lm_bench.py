@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--L", type=int, default=65536)
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--trainer", default="module", choices=["module", "torch"],
+                    help="module: dna_amd.trainer.ModuleTrainer (flat buffers, clip 1.0 + fused "
+                         "AdamW, direct gradients); torch: torch AdamW(fused), no clip (rounds 3-5)")
     a = ap.parse_args()
     torch.manual_seed(0)
     layer = {"_name_": "hyena", "emb_dim": 5, "filter_order": 64, "short_filter_order": 3,
@@ -30,21 +33,39 @@ def main():
     m = BertLMHeadModel(d_model=256, n_layer=a.layers, d_inner=1024, vocab_size=12,
                         pad_vocab_size_multiple=8, embed_dropout=0.1, residual_in_fp32=True,
                         layer=layer).cuda()
-    opt = torch.optim.AdamW(m.parameters(), lr=6e-4, weight_decay=0.1, fused=True)
     g = torch.Generator(device="cuda").manual_seed(1)
     ids = torch.randint(7, 11, (a.B, a.L), device="cuda", generator=g)   # A C G T char ids
     masked = torch.rand(a.B, a.L, device="cuda", generator=g) < 0.15
     inp = torch.where(masked, torch.full_like(ids, 3), ids)              # [MASK] = 3
+    if a.trainer == "module":
+        from dna_amd.trainer import ModuleTrainer
+        labels = torch.where(masked, ids, torch.full_like(ids, -100)).view(-1)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            (out, _) = m((inp, masked))
+        def loss_fn(model, batch):
+            # CE mean over the masked positions without a host sync (no boolean indexing):
+            # per-token losses with ignore_index, summed, over their count
+            (out, _) = model(batch)
             logits = out.logits[0]
-        loss = F.cross_entropy(logits[masked].float(), ids[masked])
-        loss.backward()
-        opt.step()
-        return loss
+            ce = F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), labels,
+                                 ignore_index=-100, reduction="none")
+            return ce.sum() / (labels != -100).sum()
+
+        tr = ModuleTrainer(m, "cuda", loss_fn, lr=6e-4, weight_decay=0.1, max_grad_norm=1.0)
+
+        def step():
+            return tr.step((inp, masked))
+    else:
+        opt = torch.optim.AdamW(m.parameters(), lr=6e-4, weight_decay=0.1, fused=True)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                (out, _) = m((inp, masked))
+                logits = out.logits[0]
+            loss = F.cross_entropy(logits[masked].float(), ids[masked])
+            loss.backward()
+            opt.step()
+            return loss
 
     for _ in range(2):
         step()
@@ -106,7 +127,7 @@ def main():
                       "unit": "sequences/s", "tokens_per_s": round(a.B * a.L / dt), "ms_per_step": round(dt * 1e3, 2),
                       "steps": a.steps, "dtype": "bf16", "data": "synthetic uniform ACGT, random init",
                       "config": {"workload": f"HyenaDNA-small d256 x{a.layers} L={a.L}", "batch": a.B,
-                                 "seq_len": a.L}, "roofline": roof, "kernels": kernels}), flush=True)
+                                 "seq_len": a.L, "trainer": a.trainer}, "roofline": roof, "kernels": kernels}), flush=True)
 
 
 if __name__ == "__main__":
