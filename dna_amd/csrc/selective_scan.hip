@@ -240,6 +240,36 @@ __device__ __forceinline__ void scan_both(float& P, float& S, float& Pr, float& 
                : "+v"(P), "+v"(S), "+v"(Pr), "+v"(Sr));
   rev_rows(Pr, Sr, lane);
 }
+// scan_both with the suffix scan of (Pr, Sr) done as a prefix scan of the lane-reversed chain:
+// ds_bpermute reverses the 64 lanes (LDS crossbar, no VALU issue), both chains then take the same
+// six row_shr / row_bcast steps interleaved, and a second bpermute restores the lane order --
+// in place of the suffix's row_shl steps and rev_rows' cross-row composition (6 readlanes, 6
+// selects, 6 combine operations per state). rev = (63 - lane) * 4.
+#ifndef DNA_SCAN_BPERM
+#define DNA_SCAN_BPERM 1
+#endif
+#define DNA_SCAN_PAIR_M(CTRL, RM)                                                      \
+  "v_fmac_f32_dpp %1, %1, %0 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"             \
+  "v_mul_f32_dpp %0, %0, %0 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"              \
+  "v_fmac_f32_dpp %3, %3, %2 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"             \
+  "v_mul_f32_dpp %2, %2, %2 " CTRL " row_mask:" RM " bank_mask:0xf\n\t"
+__device__ __forceinline__ float bperm(int addr, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+}
+__device__ __forceinline__ void scan_both_bp(float& P, float& S, float& Pr, float& Sr, int rev) {
+  Pr = bperm(rev, Pr);
+  Sr = bperm(rev, Sr);
+  // each chain's DPP reads are two instructions (the other chain's step) after their producer;
+  // the trailing s_nop 1 covers DPP reads right after the block (the compiler does not see them)
+  asm volatile("s_nop 1\n\t"
+               DNA_SCAN_PAIR_M("row_shr:1", "0xf") DNA_SCAN_PAIR_M("row_shr:2", "0xf")
+               DNA_SCAN_PAIR_M("row_shr:4", "0xf") DNA_SCAN_PAIR_M("row_shr:8", "0xf")
+               DNA_SCAN_PAIR_M("row_bcast:15", "0xa") DNA_SCAN_PAIR_M("row_bcast:31", "0xc")
+               "s_nop 1\n\t"
+               : "+v"(P), "+v"(S), "+v"(Pr), "+v"(Sr));
+  Pr = bperm(rev, Pr);
+  Sr = bperm(rev, Sr);
+}
 // inclusive prefix sum over the wave
 __device__ __forceinline__ float prefix_sum(float v) {
   v += dpp<0x111>(0.f, v);
@@ -1029,6 +1059,7 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
   // w through readfirstlane: the channel row pointers are then SGPRs (a buffer resource built
   // from a VGPR becomes a readfirstlane waterfall loop around every load)
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rev = (63 - lane) * 4;  // ds_bpermute address of the lane-reversed order
   const int c = blockIdx.y, b = blockIdx.z;
   const size_t nchN = (size_t)q.nch * N;
   const float* hbuf = a.states + (size_t)a.batch * a.dim * nchN;
@@ -1157,7 +1188,11 @@ __global__ __launch_bounds__(CT) void chunk_bwd_kernel(Args a, Chunked q) {
 #pragma unroll
       for (int i = ITEMS - 1; i >= 0; --i)
         Sr = aa2[i >> 1][i & 1] * fmaf(Cv2[i >> 1][i & 1], dy2[i >> 1][i & 1], Sr);
+#if DNA_SCAN_BPERM
+      scan_both_bp(P, S, Pr, Sr, rev);
+#else
       scan_both(P, S, Pr, Sr, lane);
+#endif
       const float Pe = shr1(P, 1.f), Se = shr1(S, 0.f);
       const float xprev = fmaf(Pe, bcast(xcl, n), Se);
       float x = xprev;
