@@ -180,7 +180,10 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float kBeta = 0.7978845608028654f, kKappa = 0.044715f;
   const float x_sq = x * x, x_cube = x_sq * x;
   const float inner = kBeta * (x + kKappa * x_cube);
-  const float t = tanhf(inner);
+  // tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp, branch-free (OCML tanhf branches
+  // on |u| -- divergent, both paths run -- and was most of EPI_GELU_BWD's epilogue); |error| <
+  // 2e-7 absolute, saturating to +-1 for large |u| (exp -> inf / 0)
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(inner * 2.8853900817779268f));
   const float left = 0.5f * x, right = 1.f + t;
   const float left_derivative = 0.5f * right;
   const float right_derivative = left * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x_sq);

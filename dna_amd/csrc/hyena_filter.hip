@@ -326,7 +326,7 @@ __global__ __launch_bounds__(NT) void bwd_kernel(Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           y[i] = rb(acc[i] + bb);
-          s[i] = sinf(fr * y[i]);
+          s[i] = hsin(fr * y[i]);  // as the forward kernel computed it
           dst[(ms * 16 + 4 * lg + i) * RS + 16 * w + l16] = (bf16)s[i];
         }
         st4(yrow + ms * 16 + 4 * lg, y[0], y[1], y[2], y[3]);
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(NT) void bwd_kernel(Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float y = (float)yy[i];
-          const float darg = rb(dx[ms][i]) * cosf(fr * y);
+          const float darg = rb(dx[ms][i]) * hcos(fr * y);
           gfr = fmaf(darg, y, gfr);
           dy[i] = rb(darg * fr);
           gb += dy[i];
