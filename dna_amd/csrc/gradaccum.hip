@@ -171,13 +171,53 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ d
   flush(cur, true);
 }
 
+constexpr int SEG_GROUP = 32;  // chunks per group of the join's second level
+
+// A group of SEG_GROUP chunks lying wholly inside one run (the rows before and after it carry
+// its id) holds only slot-0 partials of that run: one wave per such group sums them in chunk
+// order into work2[group], so the join below steps over a frequent token's ~1000-chunk run
+// 32 chunks at a time.
+template <int NV>
+__global__ __launch_bounds__(256) void segsum_group_kernel(const int64_t* __restrict__ sorted_ids,
+                                                           int rows, int cols,
+                                                           const float* __restrict__ work,
+                                                           float* __restrict__ work2) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int p0 = g * SEG_GROUP * SEG_CHUNK;
+  const int p1 = p0 + SEG_GROUP * SEG_CHUNK;
+  if (p0 == 0 || p1 >= rows || sorted_ids[p0 - 1] != sorted_ids[p1]) return;
+  constexpr int GU = NV <= 4 ? SEG_GROUP : 8;  // partials in flight (registers)
+  float acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.f;
+  for (int u0 = 0; u0 < SEG_GROUP; u0 += GU) {
+    float part[GU][NV];
+#pragma unroll
+    for (int u = 0; u < GU; ++u)
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        part[u][k] = work[((size_t)(g * SEG_GROUP + u0 + u) * 2) * cols + k * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < GU; ++u)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) acc[k] += part[u][k];
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) work2[(size_t)g * cols + k * 64 + lane] = acc[k];
+}
+
 // One wave per chunk whose last run starts inside it and crosses its end: sum the run's partials
-// (this chunk's slot 1, then slot 0 of every following chunk the run reaches) in chunk order.
+// -- this chunk's slot 1, then the slot-0 partials of the chunks up to the next group boundary,
+// the group sums of the whole groups the run covers, and the slot-0 partials of the chunks after
+// them up to the run's end. The order is fixed by the ids alone, so the table gradient stays
+// bit-identical run to run; every phase loads a batch of partials and run-end tests at once.
 template <int NV>
 __global__ __launch_bounds__(256) void segsum_join_kernel(const int64_t* __restrict__ sorted_ids,
                                                           int rows, int cols, int vocab,
                                                           int pad_idx, float* __restrict__ dE,
-                                                          const float* __restrict__ work) {
+                                                          const float* __restrict__ work,
+                                                          const float* __restrict__ work2) {
   const int lane = threadIdx.x & 63;
   const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int p0 = chunk * SEG_CHUNK;
@@ -191,35 +231,74 @@ __global__ __launch_bounds__(256) void segsum_join_kernel(const int64_t* __restr
   float acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = work[((size_t)chunk * 2 + 1) * cols + k * 64 + lane];
-  // the run's partials are added in chunk order as before (same bits), but JU chunks' partials
-  // and run-end tests are loaded at once: a frequent token's run spans thousands of chunks, and
-  // one dependent load per chunk made this the embedding gradient's longest kernel
-  constexpr int JU = 8;
+  constexpr int JU = NV <= 4 ? 32 : (NV <= 8 ? 16 : 8);
   const int nch = (rows + SEG_CHUNK - 1) / SEG_CHUNK;
-  for (int c = chunk + 1;; c += JU) {
-    float part[JU][NV];
-    bool more[JU];
+  // slot-0 partials of chunks c, c+1, ... (at most n) while the run goes on; true once it ended
+  auto singles = [&](int& c, int n) -> bool {
+    while (n > 0) {
+      float part[JU][NV];
+      bool more[JU];
 #pragma unroll
-    for (int u = 0; u < JU; ++u) {
-      const int cu = min(c + u, nch - 1);  // past the last chunk: a harmless re-read, never added
-      const int q1 = min(rows, (cu + 1) * SEG_CHUNK);
+      for (int u = 0; u < JU; ++u) {
+        const int cu = min(c + u, nch - 1);  // past the last chunk: a harmless re-read, never added
+        const int q1 = min(rows, (cu + 1) * SEG_CHUNK);
 #pragma unroll
-      for (int k = 0; k < NV; ++k) part[u][k] = work[((size_t)cu * 2) * cols + k * 64 + lane];
-      // branch-free run-end test (a short-circuit && put a branch and a vmcnt(0) around each)
-      const long a = (long)sorted_ids[q1 - 1], b = (long)sorted_ids[min(q1, rows - 1)];
-      more[u] = (a == id) & (b == id) & (q1 < rows);
-    }
-    bool done = false;
-#pragma unroll
-    for (int u = 0; u < JU; ++u) {
-      if (!done) {
-#pragma unroll
-        for (int k = 0; k < NV; ++k) acc[k] += part[u][k];
-        done = !more[u];
+        for (int k = 0; k < NV; ++k) part[u][k] = work[((size_t)cu * 2) * cols + k * 64 + lane];
+        // branch-free run-end test (a short-circuit && put a branch and a vmcnt(0) around each)
+        const long a = (long)sorted_ids[q1 - 1], b = (long)sorted_ids[min(q1, rows - 1)];
+        more[u] = (a == id) & (b == id) & (q1 < rows);
       }
+      bool done = false;
+      int used = 0;
+#pragma unroll
+      for (int u = 0; u < JU; ++u) {
+        if (!done && u < n) {
+#pragma unroll
+          for (int k = 0; k < NV; ++k) acc[k] += part[u][k];
+          done = !more[u];
+          used = u + 1;
+        }
+      }
+      c += used;
+      n -= used;
+      if (done) return true;
     }
-    if (done) break;
+    return false;
+  };
+  int c = chunk + 1;
+  if (c % SEG_GROUP && singles(c, SEG_GROUP - c % SEG_GROUP)) goto store;
+  {
+    // whole groups: the run covers group c / SEG_GROUP iff the row after it still carries id
+    // (the run reaches the group's first row, and the ids are sorted)
+    constexpr int JG = 8;
+    const int ng = nch / SEG_GROUP;
+    for (;;) {
+      float part[JG][NV];
+      bool in[JG];
+#pragma unroll
+      for (int u = 0; u < JG; ++u) {
+        const int g = min(c / SEG_GROUP + u, max(ng - 1, 0));
+        const int q1 = (c / SEG_GROUP + u + 1) * SEG_GROUP * SEG_CHUNK;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) part[u][k] = work2[(size_t)g * cols + k * 64 + lane];
+        in[u] = (q1 < rows) & ((long)sorted_ids[min(q1, rows - 1)] == id);
+      }
+      bool done = false;
+#pragma unroll
+      for (int u = 0; u < JG; ++u) {
+        if (!done && in[u]) {
+#pragma unroll
+          for (int k = 0; k < NV; ++k) acc[k] += part[u][k];
+          c += SEG_GROUP;
+        } else {
+          done = true;
+        }
+      }
+      if (done) break;
+    }
   }
+  singles(c, nch);  // the run ends inside this group
+store:
   float* dst = dE + (size_t)id * cols;
 #pragma unroll
   for (int k = 0; k < NV; ++k) dst[k * 64 + lane] += acc[k];
@@ -297,7 +376,8 @@ extern "C" int dna_colsum_bf16(const void* x, int rows, int cols, float* out, in
 
 extern "C" size_t dna_embed_grad_segsum_workspace(int rows, int cols) {
   const size_t chunks = (size_t)(rows + gacc::SEG_CHUNK - 1) / gacc::SEG_CHUNK;
-  return chunks * 2 * (size_t)cols * sizeof(float);
+  // slot 0 / 1 partials per chunk, then one group sum per SEG_GROUP chunks
+  return (chunks * 2 + chunks / gacc::SEG_GROUP + 1) * (size_t)cols * sizeof(float);
 }
 
 extern "C" int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_ids,
@@ -312,13 +392,17 @@ extern "C" int dna_embed_grad_segsum(const float* drows, const int64_t* sorted_i
   const int chunks = (rows + gacc::SEG_CHUNK - 1) / gacc::SEG_CHUNK;
   dim3 grid((chunks + 3) / 4);
   hipStream_t s = as_stream(stream);
+  float* work2 = work + (size_t)chunks * 2 * cols;
   switch (cols / 64) {
 #define DNA_SEG_CASE(K)                                                                         \
   case K:                                                                                       \
     hipLaunchKernelGGL(gacc::segsum_kernel<K>, grid, dim3(256), 0, s, drows, sorted_ids, perm,   \
                        rows, cols, vocab, padding_idx, dword_emb, work);                         \
+    if (chunks >= gacc::SEG_GROUP)                                                              \
+      hipLaunchKernelGGL(gacc::segsum_group_kernel<K>, dim3((chunks / gacc::SEG_GROUP + 3) / 4), \
+                         dim3(256), 0, s, sorted_ids, rows, cols, work, work2);                  \
     hipLaunchKernelGGL(gacc::segsum_join_kernel<K>, grid, dim3(256), 0, s, sorted_ids, rows,     \
-                       cols, vocab, padding_idx, dword_emb, work);                               \
+                       cols, vocab, padding_idx, dword_emb, work, work2);                        \
     break;
     DNA_SEG_CASE(1) DNA_SEG_CASE(2) DNA_SEG_CASE(3) DNA_SEG_CASE(4) DNA_SEG_CASE(6)
     DNA_SEG_CASE(8) DNA_SEG_CASE(12) DNA_SEG_CASE(16)

@@ -74,10 +74,6 @@ __device__ __forceinline__ float hsin(float x) {
   const float r = x * 0.15915494309189535f;
   return __builtin_amdgcn_sinf(r - rintf(r));
 }
-__device__ __forceinline__ float hcos(float x) {
-  const float r = x * 0.15915494309189535f;
-  return __builtin_amdgcn_cosf(r - rintf(r));
-}
 __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -392,7 +388,8 @@ __global__ __launch_bounds__(NT) void bwd_kernel(Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float y = (float)yy[i];
-          const float darg = rb(dx[ms][i]) * hcos(fr * y);
+          // (library cosf: v_sin / v_cos in this loop crash the ROCm 7.2 code generator)
+          const float darg = rb(dx[ms][i]) * cosf(fr * y);
           gfr = fmaf(darg, y, gfr);
           dy[i] = rb(darg * fr);
           gb += dy[i];

@@ -309,11 +309,14 @@ def test_colsum_bf16_bias_grad(rows, cols):
 
 
 @pytest.mark.parametrize("V,d,shape,pad", [(16, 256, (2, 65536), None), (12, 128, (3, 777), 4),
-                                           (4096, 64, (5000,), 0)])
+                                           (4096, 64, (5000,), 0), (5, 768, (70001,), 2),
+                                           (3, 64, (40960,), None), (2, 1024, (33 * 1024,), None),
+                                           (1, 256, (50000,), None)])
 def test_embedding_fn_grad_vs_torch(V, d, shape, pad):
     """functional.embedding (HipEmbedding): forward = F.embedding; the table gradient of the
     sorted segmented sum matches torch's embedding backward (fp32 sums in another order) and is
-    bit-identical run to run; the padding row gets no gradient."""
+    bit-identical run to run; the padding row gets no gradient. Runs of thousands of chunks (the
+    join's group level), runs ending with the data, one run over everything, d = 64 .. 1024."""
     from dna_amd import functional as DF
     g = torch.Generator(device="cpu").manual_seed(V + d)
     ids = torch.randint(0, V, shape, generator=g).to(DEV)
