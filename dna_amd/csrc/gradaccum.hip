@@ -155,18 +155,39 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ d
       else dst[k * 64 + lane] = acc[k];
     }
   };
-  for (int p = p0; p < p1; ++p) {
-    const long id = (long)sorted_ids[p];
-    if (id != cur) {
-      flush(cur, false);
-      first = false;
+  // the chunk's ids and row indices are read once, one per lane, and handed out by readlane;
+  // RU rows' loads are issued before their adds (same order of adds as one row at a time)
+  const int n = p1 - p0;
+  const int pl = p0 + min(lane & (SEG_CHUNK - 1), n - 1);
+  const long my_id = (long)sorted_ids[pl];
+  const int my_row = (int)perm[pl];
+  constexpr int RU = NV <= 4 ? 8 : 4;
+  for (int q = 0; q < n; q += RU) {
+    float row[RU][NV];
 #pragma unroll
-      for (int k = 0; k < NV; ++k) acc[k] = 0.f;
-      cur = id;
+    for (int u = 0; u < RU; ++u) {
+      const int r = __builtin_amdgcn_readlane(my_row, min(q + u, n - 1));
+      const float* src = drows + (size_t)r * cols;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) row[u][k] = src[k * 64 + lane];
     }
-    const float* src = drows + (size_t)perm[p] * cols;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] += src[k * 64 + lane];
+    for (int u = 0; u < RU; ++u) {
+      if (q + u < n) {
+        const int lo = __builtin_amdgcn_readlane((int)my_id, q + u);
+        const int hi = __builtin_amdgcn_readlane((int)(my_id >> 32), q + u);
+        const long id = (long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+        if (id != cur) {
+          flush(cur, false);
+          first = false;
+#pragma unroll
+          for (int k = 0; k < NV; ++k) acc[k] = 0.f;
+          cur = id;
+        }
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] += row[u][k];
+      }
+    }
   }
   flush(cur, true);
 }

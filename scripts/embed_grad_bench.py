@@ -20,12 +20,13 @@ def main():
     ap.add_argument("--L", type=int, default=65536)
     ap.add_argument("--V", type=int, default=16)
     ap.add_argument("--d", type=int, default=256)
+    ap.add_argument("--ids", type=int, default=4, help="distinct ids in the text")
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
-    # a 4-letter DNA text over a 16-symbol vocabulary: 4 frequent ids with ~T/4 rows each
-    ids = (torch.randint(0, 4, (a.B * a.L,), generator=g) + 7).to(dev)
+    # default: a 4-letter DNA text over a 16-symbol vocabulary, 4 frequent ids with ~T/4 rows each
+    ids = ((torch.randint(0, a.ids, (a.B * a.L,), generator=g) + 7) % a.V).to(dev)
     drows = torch.randn(a.B * a.L, a.d, generator=g).to(dev)
     T = ids.numel()
     sorted_ids, perm = torch.sort(ids, stable=True)
