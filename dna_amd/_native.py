@@ -80,6 +80,7 @@ _SIGS = {
     "dna_geglu_fwd": (_i, [_vp, _i, _i, _i, _f, _u64, _u64, _vp, _vp, _vp]),
     "dna_geglu_bwd": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_linear_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
+    "dna_linear_gelu_fwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     "dna_linear_dgrad": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "dna_linear_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "dna_transpose_bf16": (_i, [_vp, _i, _i, _vp, _vp]),

@@ -174,16 +174,27 @@ __device__ __forceinline__ void geglu_fwd_fac(float h1, float h2, bool kept, flo
   f1 = dge * s * h2;
 }
 
-// d/dx of the tanh-approximation GELU 0.5 x (1 + tanh(k (x + 0.044715 x^3))), k = sqrt(2/pi),
-// in the operation order of torch's GeluBackward (approximate="tanh")
+// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp, branch-free (OCML tanhf branches on
+// |u| -- divergent, both paths run -- and was most of EPI_GELU_BWD's epilogue); |error| < 2e-7
+// absolute, saturating to +-1 for large |u| (exp -> inf / 0)
+__device__ __forceinline__ float tanh_fast(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * 2.8853900817779268f));
+}
+// the tanh-approximation GELU 0.5 x (1 + tanh(u)), u = k (x + 0.044715 x^3), k = sqrt(2/pi),
+// as x / (1 + exp(-2u)) (the same function; no cancellation in 1 + tanh(u) for u << 0, where
+// torch's fp32 form rounds to 0 and this one keeps the tiny tail): one v_exp + one v_rcp
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float kBeta = 0.7978845608028654f, kKappa = 0.044715f;
+  const float x_cube = x * x * x;
+  const float inner = kBeta * (x + kKappa * x_cube);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(inner * -2.8853900817779268f));
+}
+// d/dx of gelu_tanh, in the operation order of torch's GeluBackward (approximate="tanh")
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float kBeta = 0.7978845608028654f, kKappa = 0.044715f;
   const float x_sq = x * x, x_cube = x_sq * x;
   const float inner = kBeta * (x + kKappa * x_cube);
-  // tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp, branch-free (OCML tanhf branches
-  // on |u| -- divergent, both paths run -- and was most of EPI_GELU_BWD's epilogue); |error| <
-  // 2e-7 absolute, saturating to +-1 for large |u| (exp -> inf / 0)
-  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(inner * 2.8853900817779268f));
+  const float t = tanh_fast(inner);
   const float left = 0.5f * x, right = 1.f + t;
   const float left_derivative = 0.5f * right;
   const float right_derivative = left * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x_sq);

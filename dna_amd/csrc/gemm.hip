@@ -38,7 +38,9 @@ constexpr int BM = 256, BN = 256, BK = 64, NTHR = 512;
 constexpr int HALF = 128 * BK * 2;      // bytes of one half-tile image (16 KB)
 constexpr int LDS_BYTES = 8 * HALF;     // 2 buffers x {A0, A1, B0, B1} = 128 KB
 
-enum Epi { EPI_BF16 = 0, EPI_F32 = 1, EPI_GEGLU = 2, EPI_GEGLU_BWD = 3, EPI_GELU_BWD = 4 };
+// EPI_BF16_GELU: the bf16 output h plus a = gelu_tanh(h) into aux (the HyenaDNA Mlp's fc1 + act)
+enum Epi { EPI_BF16 = 0, EPI_F32 = 1, EPI_GEGLU = 2, EPI_GEGLU_BWD = 3, EPI_GELU_BWD = 4,
+           EPI_BF16_GELU = 5 };
 
 typedef __attribute__((address_space(3))) void lds_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -584,7 +586,7 @@ template <int EPI, int ABL = 0, int SCH = 0>
 __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GEGLU ||
                     (EPI == EPI_GEGLU_BWD && SCH == 2 && (ABL == 0 || ABL == 128)) ||
-                    (EPI == EPI_GELU_BWD && SCH == 2 && ABL == 0),
+                    ((EPI == EPI_GELU_BWD || EPI == EPI_BF16_GELU) && SCH == 2 && ABL == 0),
                 "persistent kernel: bf16 / GeGLU epilogues (GeGLU backward: lean body only)");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES + BIAS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -716,6 +718,8 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
   const int ldo = EPI == EPI_GEGLU ? 2 * a.F : a.ldc;
   const auto rC = out_rsrc((EPI == EPI_GEGLU_BWD || EPI == EPI_GELU_BWD) ? (void*)a.aux : a.C,
                            (uint32_t)((size_t)a.M * ldo * 2));
+  // EPI_BF16_GELU: gelu(h) beside h, same layout
+  const auto rAct = out_rsrc(EPI == EPI_BF16_GELU ? (void*)a.aux : a.C, (uint32_t)((size_t)a.M * ldo * 2));
   const uint32_t voC = (uint32_t)(((wr * 64 + (lane & 15)) * ldo + wc * 32 + cq) * 2);
   // BF16: a quadrant (mq, nq) is final right after its MFMAs in a unit's last K-step, so it is
   // stored there (bias from LDS), overlapping the remaining phases. For each (row block i) the
@@ -1110,6 +1114,20 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
         uint32_t off = voQ + (uint32_t)__builtin_amdgcn_readfirstlane(
                                  ((c.m0 + mq * 128 + i * 16) * a.ldc + c.n0 + nq * 128) * 2);
         off = a.dbg == 1 ? kOOB : off;  // diagnostics: stores dropped by the range check
+        if constexpr (EPI == EPI_BF16_GELU) {
+          // a = bf16(gelu_tanh(h)) of the bf16-rounded h, as torch's GELU reads h
+          const bf16x4 e0 = __builtin_bit_cast(bf16x4, h0), e1 = __builtin_bit_cast(bf16x4, h1);
+          bf16x4 g0, g1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            g0[q] = (bf16)gelu_tanh((float)e0[q]);
+            g1[q] = (bf16)gelu_tanh((float)e1[q]);
+          }
+          const u32x2 k0 = __builtin_bit_cast(u32x2, g0), k1 = __builtin_bit_cast(u32x2, g1);
+          const auto gx = __builtin_amdgcn_permlane16_swap(k0[0], k1[0], false, false);
+          const auto gy = __builtin_amdgcn_permlane16_swap(k0[1], k1[1], false, false);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{gx[0], gy[0], gx[1], gy[1]}, rAct, off, 0, 0);
+        }
         // DNA_GEMM_NT=1 (A/B): non-temporal stores. Measured (profiles/r03b): nt, sc1 and sc0 sc1
         // stores and whole-line store patterns are all slower or equal; dropping the stores
         // (DNA_GEMM_DBG=1) saves ~3.5 us per unit at every K: the in-order vmcnt makes the
@@ -1196,8 +1214,9 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       // group after an epilogue wait that retired everything older than its g loads
       // (GELU backward: 4 h loads and 4 dh stores per quadrant)
       constexpr int QB = EPI == EPI_GELU_BWD ? 4 : 8;
-      constexpr int n = EPI == EPI_BF16
-                            ? (role == 0 ? 8 : role == 1 ? 8 + p * QS : 8 + (4 - p) * QS)
+      constexpr int QE = EPI == EPI_BF16_GELU ? 2 * QS : QS;  // + the a stores
+      constexpr int n = (EPI == EPI_BF16 || EPI == EPI_BF16_GELU)
+                            ? (role == 0 ? 8 : role == 1 ? 8 + p * QE : 8 + (4 - p) * QE)
                             : (EPI == EPI_GEGLU_BWD || EPI == EPI_GELU_BWD)
                             ? (role == 0 ? 8 : role == 1 ? 8 + QB + p * QB : 8 + (4 - p) * QB)
                             : (role == 0 ? 8 : role == 1 ? 8 + (p >= 2 ? GS : 0) : 8 + (p < 2 ? 2 * GS : GS));
@@ -1207,7 +1226,7 @@ __global__ __launch_bounds__(NTHR) void gemmp_kernel(Args a) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     };
-    constexpr bool SB = EPI == EPI_BF16;  // per-quadrant stores (else GeGLU halves)
+    constexpr bool SB = EPI == EPI_BF16 || EPI == EPI_BF16_GELU;  // per-quadrant stores (else GeGLU halves)
     constexpr bool GB = EPI == EPI_GEGLU_BWD || EPI == EPI_GELU_BWD;  // per-quadrant backward epilogue
     // one K-step k of the current unit in buffer parity par; ZI: the unit's first K-step (MFMA
     // chains start from zero)
@@ -1858,19 +1877,23 @@ int launchp(Args& a, hipStream_t s, const char* name) {
   if (const char* e = getenv("DNA_GEMM_NT")) a.nt = atoi(e);
   a.order = 0;
   if (const char* e = getenv("DNA_GEMM_ORDER")) a.order = atoi(e);
-  const char* ab = getenv("DNA_GEMM_ABL");
-  const int abl = ab ? atoi(ab) : 0;
-  if (abl == 0 && gemm_sched() == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 1>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (abl == 0 && gemm_sched() == 2 && (a.K / BK) % 2 == 0)
+  if constexpr (EPI == EPI_BF16_GELU) {  // lean body only (K / BK even: the launcher checks)
     hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 2>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (abl == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 1>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (abl == 2) hipLaunchKernelGGL((gemmp_kernel<EPI, 2>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (abl == 3) hipLaunchKernelGGL((gemmp_kernel<EPI, 3>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (abl == 7) hipLaunchKernelGGL((gemmp_kernel<EPI, 7>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (abl == 8) hipLaunchKernelGGL((gemmp_kernel<EPI, 8>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (abl == 16) hipLaunchKernelGGL((gemmp_kernel<EPI, 16>), dim3(G), dim3(NTHR), 0, s, a);
-  else if (abl == 32) hipLaunchKernelGGL((gemmp_kernel<EPI, 32>), dim3(G), dim3(NTHR), 0, s, a);
-  else hipLaunchKernelGGL((gemmp_kernel<EPI>), dim3(G), dim3(NTHR), 0, s, a);
+  } else {
+    const char* ab = getenv("DNA_GEMM_ABL");
+    const int abl = ab ? atoi(ab) : 0;
+    if (abl == 0 && gemm_sched() == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 1>), dim3(G), dim3(NTHR), 0, s, a);
+    else if (abl == 0 && gemm_sched() == 2 && (a.K / BK) % 2 == 0)
+      hipLaunchKernelGGL((gemmp_kernel<EPI, 0, 2>), dim3(G), dim3(NTHR), 0, s, a);
+    else if (abl == 1) hipLaunchKernelGGL((gemmp_kernel<EPI, 1>), dim3(G), dim3(NTHR), 0, s, a);
+    else if (abl == 2) hipLaunchKernelGGL((gemmp_kernel<EPI, 2>), dim3(G), dim3(NTHR), 0, s, a);
+    else if (abl == 3) hipLaunchKernelGGL((gemmp_kernel<EPI, 3>), dim3(G), dim3(NTHR), 0, s, a);
+    else if (abl == 7) hipLaunchKernelGGL((gemmp_kernel<EPI, 7>), dim3(G), dim3(NTHR), 0, s, a);
+    else if (abl == 8) hipLaunchKernelGGL((gemmp_kernel<EPI, 8>), dim3(G), dim3(NTHR), 0, s, a);
+    else if (abl == 16) hipLaunchKernelGGL((gemmp_kernel<EPI, 16>), dim3(G), dim3(NTHR), 0, s, a);
+    else if (abl == 32) hipLaunchKernelGGL((gemmp_kernel<EPI, 32>), dim3(G), dim3(NTHR), 0, s, a);
+    else hipLaunchKernelGGL((gemmp_kernel<EPI>), dim3(G), dim3(NTHR), 0, s, a);
+  }
   DNA_LAUNCH_CHECK(name);
   return DNA_OK;
 }
@@ -1945,6 +1968,37 @@ extern "C" int dna_linear_fwd(const void* x, const void* w, const float* bias, i
     }
   }
   return launch<true, true, EPI_BF16>(a, 1, as_stream(stream), "dna_linear_fwd");
+}
+
+extern "C" int dna_linear_gelu_fwd(const void* x, const void* w, const float* bias, int M, int N,
+                                   int K, void* h, void* act, void* stream) {
+  DNA_CHECK_ARG(x && w && h && act, "dna_linear_gelu_fwd: null pointer");
+  DNA_CHECK_ARG(M >= 0 && N > 0 && K > 0, "dna_linear_gelu_fwd: bad shape");
+  // the persistent kernel's lean body only: N a multiple of the 256-column tile with its bias in
+  // LDS, an even number of 64-deep K-steps, the weight under 2 GB (32-bit offsets)
+  DNA_CHECK_ARG(N % BN == 0 && N <= BIAS_LDS / 4 && K % (2 * BK) == 0 &&
+                    (size_t)N * K * 2 < (1ull << 31),
+                "dna_linear_gelu_fwd: N %% 256 (<= %d) and K %% 128 required (N=%d K=%d)",
+                BIAS_LDS / 4, N, K);
+  if (M == 0) return DNA_OK;
+  Args a = base_args();
+  a.A = (const bf16*)x; a.lda = K;
+  a.B = (const bf16*)w; a.ldb = K;
+  a.C = h; a.ldc = N; a.bias = bias; a.aux = (bf16*)act;
+  a.M = M; a.N = N; a.K = K; a.ksplit = K;
+  const size_t wide = (size_t)(K > N ? K : N) * 2;
+  const int cap = (int)(((1ull << 31) - 1) / wide / BM * BM);
+  const int mc = row_block(M, cap);
+  for (int r0 = 0; r0 < M; r0 += mc) {
+    Args c = a;
+    c.A = a.A + (size_t)r0 * K;
+    c.C = (bf16*)a.C + (size_t)r0 * N;
+    c.aux = a.aux + (size_t)r0 * N;
+    c.M = M - r0 < mc ? M - r0 : mc;
+    const int st = launchp<EPI_BF16_GELU>(c, as_stream(stream), "dna_linear_gelu_fwd");
+    if (st != DNA_OK) return st;
+  }
+  return DNA_OK;
 }
 
 extern "C" int dna_linear_dgrad(const void* dy, const void* w, int M, int N, int K, void* dx,

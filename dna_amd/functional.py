@@ -716,6 +716,27 @@ def _hip_geglu_linear(x, w_nk, p, seed, off):
     return fac, a
 
 
+def _gelu_fc1_ok(x, w_lp):
+    """dna_linear_gelu_fwd applies (the persistent kernel's lean body: N % 256, N <= 8192,
+    K % 128); DNA_GELU_FC1_FUSED=0: torch's separate GELU pass (A/B)."""
+    Nn, K = w_lp.shape
+    return (os.environ.get("DNA_GELU_FC1_FUSED", "1") != "0" and _hip_gemm_ok(x, w_lp, Nn, K)
+            and Nn % 256 == 0 and Nn <= 8192 and K % 128 == 0 and Nn * K * 2 < 2 ** 31)
+
+
+def _hip_linear_gelu(x, w_nk, bias):
+    """h = x . w_nk^T (+ fp32 bias) and act = bf16(gelu_tanh(h)) from one launch
+    (dna_linear_gelu_fwd)."""
+    x = x.contiguous()
+    M, K = x.shape
+    Nn = w_nk.shape[0]
+    h = torch.empty(M, Nn, device=x.device, dtype=torch.bfloat16)
+    act = torch.empty_like(h)
+    N.call("dna_linear_gelu_fwd", x.data_ptr(), w_nk.data_ptr(), _p(bias), M, Nn, K, h.data_ptr(),
+           act.data_ptr(), N.stream_ptr())
+    return h, act
+
+
 def _hip_linear(x, w_nk, bias):
     """y[M, N] = x[M, K] . w_nk[N, K]^T (+ fp32 bias): the persistent MFMA GEMM (dna_linear_fwd)."""
     x = x.contiguous()
@@ -752,10 +773,11 @@ class GeluLinear(torch.autograd.Function):
     weight gradient from a = gelu(h), bias gradient by the native column sum."""
 
     @staticmethod
-    def forward(ctx, h, w, b, w_lp, w_lpt):
+    def forward(ctx, h, w, b, w_lp, w_lpt, act=None):
         _gpu(h)
         h = h.contiguous()
-        a = F.gelu(h, approximate="tanh")
+        # act: gelu(h) from fc1's GEMM epilogue (dna_linear_gelu_fwd), else torch's GELU pass
+        a = act if act is not None else F.gelu(h, approximate="tanh")
         flops = 2.0 * h.shape[0] * w_lp.shape[0] * w_lp.shape[1]
         with _timed("gemm_hip", flops):
             o = _hip_linear(a, w_lp, None if b is None else b.float())
@@ -777,7 +799,7 @@ class GeluLinear(torch.autograd.Function):
                    Nn, dh.data_ptr(), N.stream_ptr())
         dw = _weight_grad(ctx.weight, do, a, flops)
         db = bias_grad(do) if ctx.has_b else None
-        return dh, dw, db, None, None
+        return dh, dw, db, None, None, None
 
 
 def gelu_linear_ok(h, w):
@@ -790,11 +812,13 @@ def gelu_linear_ok(h, w):
             and os.environ.get("DNA_GELU_BWD_FUSED", "1") != "0")
 
 
-def gelu_linear(h, w, b):
-    """F.linear(F.gelu(h, approximate="tanh"), w, b) under bf16 autocast (GeluLinear)."""
+def gelu_linear(h, w, b, act=None):
+    """F.linear(F.gelu(h, approximate="tanh"), w, b) under bf16 autocast (GeluLinear); act:
+    gelu(h) already computed by fc1's epilogue (hyena.hip_linear(..., gelu=True))."""
     lead, F_ = h.shape[:-1], h.shape[-1]
     w_lp = w.to(torch.bfloat16)
-    y = GeluLinear.apply(h.reshape(-1, F_), w, b, w_lp, w_lp.t().contiguous())
+    y = GeluLinear.apply(h.reshape(-1, F_), w, b, w_lp, w_lp.t().contiguous(),
+                         None if act is None else act.reshape(-1, F_))
     return y.view(*lead, w.shape[0])
 
 
@@ -806,7 +830,7 @@ class Linear(torch.autograd.Function):
     folded into the flat gradient by dna_sum_slices_accum)."""
 
     @staticmethod
-    def forward(ctx, x, w, w_lp, b, w_lpt, geglu=None):
+    def forward(ctx, x, w, w_lp, b, w_lpt, geglu=None, gelu=False):
         ctx.save_for_backward(x, w_lp, w_lpt)
         ctx.weight = w
         ctx.has_b = b is not None
@@ -821,6 +845,13 @@ class Linear(torch.autograd.Function):
                 g, a = _hip_geglu_linear(x, w_lp, *geglu)
             g._dna_geglu = (a, tuple(geglu))
             return g
+        if gelu and _gelu_fc1_ok(x, w_lp):
+            # h and gelu_tanh(h) from one launch; gelu(h) rides on h for the GeluLinear node
+            # that follows (it carries the GELU backward: this node's gradient stays dh)
+            with _timed("gemm_gelu", flops):
+                h, act = _hip_linear_gelu(x, w_lp, b if (b is None or b.dtype == torch.float32) else b.float())
+            h._dna_gelu = act
+            return h
         if _hip_gemm_ok(x, w_lp, w_lp.shape[0], w_lp.shape[1]):
             with _timed("gemm_hip", flops):
                 return _hip_linear(x, w_lp, b if (b is None or b.dtype == torch.float32) else b.float())
@@ -859,7 +890,7 @@ class Linear(torch.autograd.Function):
             db = getattr(dy, "_dna_colsum", None)  # fused upstream (AlibiAttention.backward)
             if db is None:
                 db = bias_grad(dy)
-        return dx, dw, None, db, None, None
+        return dx, dw, None, db, None, None, None
 
 
 # ------------------------------------------------------------------ weight-gradient side stream

@@ -24,13 +24,15 @@ from .functional import _dt, _gpu, _p, _timed
 _TORCH_LINEAR = os.environ.get("DNA_HYENA_TORCH_LINEAR", "0") == "1"  # A/B switch: torch Linear
 
 
-def hip_linear(x, weight, bias=None):
+def hip_linear(x, weight, bias=None, gelu=False):
     """F.linear(x, weight, bias) with autocast nn.Linear's dtype flow on hand-written kernels:
     under CUDA bf16 autocast with K % 64 == 0 and N % 256 == 0 the persistent MFMA GEMM
     (`dna_linear_fwd`, dgrad on a transposed bf16 weight copy, fp32 split-K weight gradient);
     every other CUDA case -- fp32, skinny or ragged N such as a 16-token character vocabulary --
     the strided MFMA GEMM (`functional.strided_linear`). CPU tensors (module-level CPU tests)
-    and DNA_HYENA_TORCH_LINEAR=1 (A/B) keep torch's linear."""
+    and DNA_HYENA_TORCH_LINEAR=1 (A/B) keep torch's linear. gelu=True (the Mlp's fc1 ahead of
+    GeluLinear): on the persistent path the output also carries `_dna_gelu` = gelu_tanh of it
+    from the same launch (dna_linear_gelu_fwd)."""
     K, Nout = weight.shape[1], weight.shape[0]
     if _TORCH_LINEAR or not x.is_cuda:
         return F.linear(x, weight, bias)
@@ -39,8 +41,12 @@ def hip_linear(x, weight, bias=None):
         return DF.strided_linear(x, weight, bias)
     w_lp = weight.to(torch.bfloat16)
     y = _LinearFn.apply(x.reshape(-1, K).to(torch.bfloat16), weight, w_lp, bias,
-                        w_lp.t().contiguous())
-    return y.view(*x.shape[:-1], Nout)
+                        w_lp.t().contiguous(), None, gelu)
+    out = y.view(*x.shape[:-1], Nout)
+    act = getattr(y, "_dna_gelu", None)
+    if act is not None:
+        out._dna_gelu = act.view(out.shape)
+    return out
 
 
 class HipLinear(nn.Linear):

@@ -22,7 +22,7 @@ import torch.nn.functional as F
 
 from . import functional as DF
 from .functional import HipEmbedding
-from .hyena import HipLinear, HyenaOperator
+from .hyena import HipLinear, HyenaOperator, hip_linear
 
 
 CausalLMOutput = namedtuple("CausalLMOutput", ["logits"])
@@ -112,19 +112,22 @@ class Mlp(nn.Module):
         self.fc2 = HipLinear(hidden_features, out_features or in_features, **fk)
 
     def forward(self, x):
-        h = self.fc1(x)
-        if self._gelu_fused(h):
+        if self._tanh_gelu_bf16() and isinstance(self.fc1, HipLinear):
+            # fc1's GEMM also writes gelu(h) (dna_linear_gelu_fwd): no separate GELU pass
+            h = hip_linear(x, self.fc1.weight, self.fc1.bias, gelu=True)
+        else:
+            h = self.fc1(x)
+        if self._tanh_gelu_bf16() and DF.gelu_linear_ok(h, self.fc2.weight):
             # act + fc2 as one node: fc2's data gradient carries the GELU backward (GeluLinear)
-            return DF.gelu_linear(h, self.fc2.weight, self.fc2.bias)
+            return DF.gelu_linear(h, self.fc2.weight, self.fc2.bias, getattr(h, "_dna_gelu", None))
         return self.fc2(self.activation(h))
 
-    def _gelu_fused(self, h):
+    def _tanh_gelu_bf16(self):
         act = self.activation
         return (isinstance(act, partial) and act.func is F.gelu and not act.args
                 and act.keywords == {"approximate": "tanh"} and isinstance(self.fc2, HipLinear)
                 and not _TORCH_LINEAR_MLP and torch.is_autocast_enabled("cuda")
-                and torch.get_autocast_dtype("cuda") == torch.bfloat16
-                and DF.gelu_linear_ok(h, self.fc2.weight))
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16)
 
 
 class Block(nn.Module):

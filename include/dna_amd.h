@@ -253,6 +253,13 @@ int dna_geglu_bwd(const void* da, const void* fac, int dtype, int rows, int inte
 int dna_linear_fwd(const void* x, const void* w, const float* bias, int M, int N, int K, void* y,
                    void* stream);
 int dna_linear_dgrad(const void* dy, const void* w, int M, int N, int K, void* dx, void* stream);
+/* HyenaDNA Mlp fc1 + activation (flash_attn Mlp: fc2(act(fc1(x))), act = F.gelu(approximate=
+ * "tanh"); standalone_hyenadna.py:431 Mlp): h[M,N] = x . w^T + bias (bf16) and
+ * act[M,N] = bf16(gelu_tanh(h)) from one persistent-GEMM launch (N % 256 == 0, N <= 8192,
+ * K % 128 == 0), replacing fc1's GEMM and torch's separate GELU pass; fc2's data gradient reads h
+ * (dna_gelu_linear_dgrad_p), its forward and weight gradient read act. */
+int dna_linear_gelu_fwd(const void* x, const void* w, const float* bias, int M, int N, int K,
+                        void* h, void* act, void* stream);
 int dna_linear_wgrad(const void* dy, const void* x, int M, int N, int K, int splits,
                      float* partials, void* stream);
 

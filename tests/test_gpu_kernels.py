@@ -925,3 +925,52 @@ def test_gelu_linear_fused_bwd_vs_separate(M, F, Nn):
     err = (dh1.float() - dh2.float()).abs().max().item()
     assert err <= 1e-2 * dh2.float().abs().max().item(), err
     assert torch.allclose(dw1, dw2, rtol=1e-5, atol=1e-5) and torch.allclose(db1, db2, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,K,Nn", [(5000, 256, 1024), (131072, 256, 1024), (700, 128, 256)])
+def test_linear_gelu_fwd_vs_separate(M, K, Nn):
+    """dna_linear_gelu_fwd (fc1 + tanh-GELU of the HyenaDNA Mlp in one persistent-GEMM launch):
+    h bit-equal to dna_linear_fwd on the same operands; act = gelu_tanh(h) of the bf16 h within
+    one bf16 rounding step of torch's GELU (the kernel evaluates x / (1 + exp(-2u)) with the
+    hardware exp / rcp, so a handful of elements round the other way), plus 1e-6 |h| where
+    torch's 0.5 x (1 + tanh(u)) cancels for u << 0 (it returns 0 where the kernel keeps the
+    ~1e-7 tail)."""
+    from dna_amd import functional as DF
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    x = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    w = (torch.randn(Nn, K, generator=g) / K ** 0.5).to(DEV).bfloat16()
+    b = (torch.randn(Nn, generator=g) * 0.1).to(DEV)
+    h_ref = DF._hip_linear(x, w, b)
+    h, act = DF._hip_linear_gelu(x, w, b)
+    assert torch.equal(h, h_ref)
+    a_ref = torch.nn.functional.gelu(h_ref, approximate="tanh")
+    d = (act.float() - a_ref.float()).abs()
+    tol = a_ref.float().abs() * 2.0 ** -7 + 1e-6 * h_ref.float().abs()
+    assert (d <= tol).all(), (d - tol).max().item()
+    assert (act != a_ref).float().mean().item() < 1e-3
+
+
+def test_mlp_fc1_gelu_fused_vs_unfused(monkeypatch):
+    """hyena_lm.Mlp under bf16 autocast with fc1's GELU in the GEMM epilogue
+    (DNA_GELU_FC1_FUSED=1, default) against torch's separate GELU pass (=0): output and every
+    parameter / input gradient within bf16 rounding of each other."""
+    from dna_amd.hyena_lm import Mlp
+    torch.manual_seed(0)
+    m = Mlp(256, 1024).to(DEV)
+    x = torch.randn(4, 2048, 256, device=DEV)
+    dy = torch.randn(4, 2048, 256, device=DEV)
+    res = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DNA_GELU_FC1_FUSED", fused)
+        m.zero_grad(set_to_none=True)
+        xx = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(xx)
+        y.float().backward(dy)
+        res.append((y.detach().float(), xx.grad, [p.grad.clone() for p in m.parameters()]))
+    (y1, dx1, g1), (y2, dx2, g2) = res
+    rel = lambda a, b: (a - b).abs().max().item() / max(b.abs().max().item(), 1e-12)
+    assert rel(y1, y2) < 2e-2
+    assert rel(dx1, dx2) < 2e-2
+    for a, b in zip(g1, g2):
+        assert rel(a, b) < 2e-2
