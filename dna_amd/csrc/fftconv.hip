@@ -517,6 +517,7 @@ __global__ __launch_bounds__(RB_NT, MINB) void row_bwd_kernel(cf* __restrict__ z
   const int d = blockIdx.y;
   const size_t roff = (size_t)k10 * M2;
   make_table(tw, g.logM2);
+  static_assert(PPT == 16, "row_bwd_kernel: acc[] in two halves of 8");
   cf acc[PPT];
 #pragma unroll
   for (int it = 0; it < PPT; ++it) acc[it] = make_float2(0.f, 0.f);
@@ -558,7 +559,11 @@ __global__ __launch_bounds__(RB_NT, MINB) void row_bwd_kernel(cf* __restrict__ z
         const int a = lds_at(e >> g.logM2, e & (M2 - 1), S);
         if (e < rw * M2) {
           const cf z = buf[a];
-          if (DK) acc[c0 + it] = cadd(acc[c0 + it], cmul(cconj(uv[it]), z));
+          // (static indices in both arms: a run-time acc[c0 + it] put acc in scratch memory)
+          if (DK) {
+            if (c0 == 0) acc[it] = cadd(acc[it], cmul(cconj(uv[it]), z));
+            else acc[8 + it] = cadd(acc[8 + it], cmul(cconj(uv[it]), z));
+          }
           if (DU) buf[a] = cmul(z, cconj(kv[it]));
         }
       }
