@@ -991,11 +991,14 @@ void launch_row(cf* ws, const cf* kspec, Pairing pr, const Geo& g, int P, hipStr
 template <bool DK, bool DU>
 void launch_row_bwd(cf* zy, const cf* zu, const cf* kspec, int BP, int D, const Geo& g, cf* pk,
                     hipStream_t s) {
-  // DNA_FFT_RB_BLOCKS=4 (A/B): four blocks per CU (128 VGPRs, spills) instead of three
-  static const bool rb4 = getenv("DNA_FFT_RB_BLOCKS") && atoi(getenv("DNA_FFT_RB_BLOCKS")) == 4;
+  // DNA_FFT_RB_BLOCKS=4 / 2 (A/B): four blocks per CU (128 VGPRs, spills) or two (256 VGPRs)
+  // instead of three
+  static const int rbb = getenv("DNA_FFT_RB_BLOCKS") ? atoi(getenv("DNA_FFT_RB_BLOCKS")) : 3;
 #define L_(LN)                                                                                   \
   {                                                                                              \
-    auto k = (DK && DU && rb4) ? row_bwd_kernel<LN, DK, DU, 4> : row_bwd_kernel<LN, DK, DU>;     \
+    auto k = (DK && DU && rbb == 4)   ? row_bwd_kernel<LN, DK, DU, 4>                            \
+             : (DK && DU && rbb == 2) ? row_bwd_kernel<LN, DK, DU, 2>                            \
+                                      : row_bwd_kernel<LN, DK, DU>;                              \
     const size_t lds = ((size_t)(1 << log_rowbwd_group(g)) * seq_stride(g.logM2, false) +        \
                         (1u << g.logM2)) * sizeof(cf);                                           \
     allow_lds(k, lds);                                                                           \
