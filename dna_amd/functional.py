@@ -748,19 +748,29 @@ def _hip_linear(x, w_nk, bias):
     return y
 
 
-def bias_grad(dy):
+def bias_grad(dy, bias=None):
     """fp32 sum over rows of dy [rows, cols] (a Linear's bias gradient): bf16 CUDA gradients
     with cols % 64 == 0 on the native two-stage column sum (dna_colsum_bf16, deterministic);
     everything else torch's sum."""
     rows, cols = dy.shape
     if (dy.dtype == torch.bfloat16 and dy.is_cuda and cols % 64 == 0 and rows >= 1
             and dy.is_contiguous() and dy.data_ptr() % 16 == 0):
-        out = torch.empty(cols, device=dy.device, dtype=torch.float32)
+        # bias: the parameter; under FlatParams direct gradients the column sum is added straight
+        # into its fp32 .grad view (the kernel's accumulate mode) and None is returned -- no
+        # AccumulateGrad add launch per bias and step (DNA_BIAS_GRAD_DIRECT=0: returned, A/B)
+        direct = (bias is not None and os.environ.get("DNA_BIAS_GRAD_DIRECT", "1") != "0"
+                  and _param_grads_direct((bias,)) and bias.grad.numel() == cols)
+        out = bias.grad if direct else torch.empty(cols, device=dy.device, dtype=torch.float32)
         nws = N.lib().dna_colsum_bf16_workspace(rows, cols)
         ws = torch.empty(nws, device=dy.device, dtype=torch.uint8)
         with _timed("colsum", rows * cols * 2, "byte"):
-            N.call("dna_colsum_bf16", dy.data_ptr(), rows, cols, out.data_ptr(), 0, ws.data_ptr(),
-                   nws, N.stream_ptr())
+            N.call("dna_colsum_bf16", dy.data_ptr(), rows, cols, out.data_ptr(), int(direct),
+                   ws.data_ptr(), nws, N.stream_ptr())
+        if direct:
+            notify = getattr(bias, "_dna_notify", None)
+            if notify is not None:
+                notify(bias)
+            return None
         return out
     return dy.sum(0, dtype=torch.float32)
 
@@ -783,6 +793,7 @@ class GeluLinear(torch.autograd.Function):
             o = _hip_linear(a, w_lp, None if b is None else b.float())
         ctx.save_for_backward(h, a, w_lpt)
         ctx.weight = w
+        ctx.bias = b
         ctx.has_b = b is not None
         return o
 
@@ -798,7 +809,7 @@ class GeluLinear(torch.autograd.Function):
             N.call("dna_gelu_linear_dgrad_p", do.data_ptr(), w_lpt.data_ptr(), h.data_ptr(), M, F_,
                    Nn, dh.data_ptr(), N.stream_ptr())
         dw = _weight_grad(ctx.weight, do, a, flops)
-        db = bias_grad(do) if ctx.has_b else None
+        db = bias_grad(do, ctx.bias) if ctx.has_b else None
         return dh, dw, db, None, None, None
 
 
@@ -833,6 +844,7 @@ class Linear(torch.autograd.Function):
     def forward(ctx, x, w, w_lp, b, w_lpt, geglu=None, gelu=False):
         ctx.save_for_backward(x, w_lp, w_lpt)
         ctx.weight = w
+        ctx.bias = b
         ctx.has_b = b is not None
         flops = 2.0 * x.shape[0] * w_lp.shape[0] * w_lp.shape[1]
         if geglu is not None and b is None and _geglu_fused_ok(x, w_lp):
@@ -889,7 +901,7 @@ class Linear(torch.autograd.Function):
         if ctx.has_b:
             db = getattr(dy, "_dna_colsum", None)  # fused upstream (AlibiAttention.backward)
             if db is None:
-                db = bias_grad(dy)
+                db = bias_grad(dy, ctx.bias)
         return dx, dw, None, db, None, None, None
 
 
